@@ -1,0 +1,391 @@
+"""CPU oracle: a numpy restatement of the STIF ``LunaTokis`` forward.
+
+TEST INFRASTRUCTURE ONLY.  Only ``tests/``, ``__graft_entry__.smoke()`` and the
+``cpu_baseline`` leg of ``bench.py`` may import this module, and only as the
+checker / the timed CPU baseline -- never as a product code path.
+
+Every function follows the reference file:line it cites (paths relative to the
+reference's ``codes/``).  Feature arithmetic runs in ``dtype`` (float64 by
+default, so the oracle is a "truth" that both the reference's fp32 CPU run and
+the HIP path are measured against); every *discrete* decision the reference
+takes from fp32 coordinates (``make_coord``, ``grid_sample`` nearest rounding,
+``linspace``) is reproduced in float32 exactly as the reference computes it.
+
+Parity status: pinned against ``tests/golden/*.npz``, which were produced by
+running the reference model itself (``tests/golden/make_golden.py``).  The one
+piece the reference cannot run here is the DCNv2 native op (it needs the removed
+THC API); its restatement below is pinned by the reference's zero-offset
+known-answer test (``DCNv2/test.py:32-67``) and by the reference ``DCN_sep``
+module run on that restatement.
+"""
+from __future__ import annotations
+
+import numpy as np
+from numpy.lib.stride_tricks import sliding_window_view
+
+F32 = np.float32
+
+
+# ----------------------------------------------------------------------------- basic ops
+def conv2d(x, w, b, stride=1, pad=None, dtype=np.float64):
+    """nn.Conv2d forward (NCHW).  x [N,C,H,W], w [Co,C,kh,kw]."""
+    Co, C, kh, kw = w.shape
+    if pad is None:
+        pad = kh // 2
+    x = np.asarray(x, dtype)
+    if pad:
+        x = np.pad(x, ((0, 0), (0, 0), (pad, pad), (pad, pad)))
+    win = sliding_window_view(x, (kh, kw), axis=(2, 3))[:, :, ::stride, ::stride]
+    out = np.tensordot(win, np.asarray(w, dtype), axes=([1, 4, 5], [1, 2, 3]))  # [N,Ho,Wo,Co]
+    out = out.transpose(0, 3, 1, 2) + np.asarray(b, dtype)[None, :, None, None]
+    return np.ascontiguousarray(out)
+
+
+def lrelu(x):
+    """nn.LeakyReLU(negative_slope=0.1) (Sakuya_arch_test.py:69)."""
+    return np.where(x >= 0, x, x * 0.1)
+
+
+def relu(x):
+    return np.maximum(x, 0)
+
+
+def sigmoid(x):
+    return 1.0 / (1.0 + np.exp(-x))
+
+
+def _up2_index(n_in):
+    """Source indices/weights of F.interpolate(scale_factor=2, bilinear, align_corners=False)."""
+    d = np.arange(2 * n_in, dtype=np.float64)
+    src = np.maximum(0.5 * (d + 0.5) - 0.5, 0.0)
+    i0 = src.astype(np.int64)
+    i1 = np.where(i0 < n_in - 1, i0 + 1, i0)
+    l1 = src - i0
+    return i0, i1, 1.0 - l1, l1
+
+
+def upsample2x(x):
+    """F.interpolate(x, scale_factor=2, mode='bilinear', align_corners=False)
+    as used by PCD_Align (Sakuya_arch_test.py:86,90,95,99,112,116,121,125)."""
+    N, C, H, W = x.shape
+    h0, h1, lh0, lh1 = _up2_index(H)
+    w0, w1, lw0, lw1 = _up2_index(W)
+    top = x[:, :, h0][:, :, :, w0] * lw0 + x[:, :, h0][:, :, :, w1] * lw1
+    bot = x[:, :, h1][:, :, :, w0] * lw0 + x[:, :, h1][:, :, :, w1] * lw1
+    return top * lh0[:, None] + bot * lh1[:, None]
+
+
+# ----------------------------------------------------------------------------- DCNv2
+def dcn_v2_forward(inp, weight, bias, offset, mask, kh, kw, sh, sw, ph, pw, dh, dw, dg,
+                   dtype=np.float64):
+    """Restatement of ``dcn_v2_cuda_forward`` (DCNv2/src/cuda/dcn_v2_cuda.cu:42-172):
+    output = bias + W . columns, where columns come from
+    ``modulated_deformable_im2col_gpu_kernel`` (dcn_v2_im2col_cuda.cu:125-195):
+      h_im = h_out*stride - pad + i*dil + offset_h   (fp32 in the reference)
+      sampled only if h_im > -1 && w_im > -1 && h_im < H && w_im < W,
+      bilinear with per-corner zero padding (dmcn_im2col_bilinear, :25-54),
+      times the modulation mask.
+    Offset channel of (group g, tap k): g*2*K + 2k (+0 for h, +1 for w); mask: g*K + k.
+    """
+    inp = np.asarray(inp, dtype)
+    B, C, H, W = inp.shape
+    Co = weight.shape[0]
+    Ho = (H + 2 * ph - (dh * (kh - 1) + 1)) // sh + 1
+    Wo = (W + 2 * pw - (dw * (kw - 1) + 1)) // sw + 1
+    K = kh * kw
+    cpg = C // dg
+    off = np.asarray(offset, F32).reshape(B, dg, K, 2, Ho, Wo)
+    msk = np.asarray(mask, dtype).reshape(B, dg, K, Ho, Wo)
+    h_in = (np.arange(Ho) * sh - ph).reshape(1, 1, Ho, 1)
+    w_in = (np.arange(Wo) * sw - pw).reshape(1, 1, 1, Wo)
+    img = inp.reshape(B, dg, cpg, H * W)
+    cols = np.zeros((B, dg, cpg, K, Ho, Wo), dtype)
+    bidx = np.arange(B)[:, None, None, None, None]
+    gidx = np.arange(dg)[None, :, None, None, None]
+    cidx = np.arange(cpg)[None, None, :, None, None]
+    for i in range(kh):
+        for j in range(kw):
+            k = i * kw + j
+            h_im = (h_in + i * dh).astype(F32) + off[:, :, k, 0]     # fp32 as the reference
+            w_im = (w_in + j * dw).astype(F32) + off[:, :, k, 1]
+            inside = (h_im > -1) & (w_im > -1) & (h_im < H) & (w_im < W)
+            h_low = np.floor(h_im)
+            w_low = np.floor(w_im)
+            lh = (h_im - h_low).astype(dtype)
+            lw = (w_im - w_low).astype(dtype)
+            hh, hw = 1 - lh, 1 - lw
+            h_low = h_low.astype(np.int64)
+            w_low = w_low.astype(np.int64)
+            h_high, w_high = h_low + 1, w_low + 1
+
+            def corner(hc, wc, ok):
+                idx = (np.clip(hc, 0, H - 1) * W + np.clip(wc, 0, W - 1))[:, :, None]
+                v = img[bidx, gidx, cidx, idx]                      # [B,dg,cpg,Ho,Wo]
+                return np.where(ok[:, :, None], v, 0)
+
+            v1 = corner(h_low, w_low, (h_low >= 0) & (w_low >= 0))
+            v2 = corner(h_low, w_high, (h_low >= 0) & (w_high <= W - 1))
+            v3 = corner(h_high, w_low, (h_high <= H - 1) & (w_low >= 0))
+            v4 = corner(h_high, w_high, (h_high <= H - 1) & (w_high <= W - 1))
+            e = lambda t: t[:, :, None]
+            val = e(hh * hw) * v1 + e(hh * lw) * v2 + e(lh * hw) * v3 + e(lh * lw) * v4
+            val = np.where(e(inside), val, 0)
+            cols[:, :, :, k] = val * e(msk[:, :, k])
+    cols = cols.reshape(B, C * K, Ho * Wo)
+    out = np.einsum("ok,bkn->bon", np.asarray(weight, dtype).reshape(Co, C * K), cols, optimize=True)
+    out = out + np.asarray(bias, dtype)[None, :, None]
+    return out.reshape(B, Co, Ho, Wo)
+
+
+def dcn_sep(inp, fea, sd, name, groups=8, dtype=np.float64):
+    """DCN_sep.forward (DCNv2/dcn_v2.py:127-140): offsets/mask from a separate feature."""
+    out = conv2d(fea, sd[name + ".conv_offset_mask.weight"], sd[name + ".conv_offset_mask.bias"], dtype=dtype)
+    n = out.shape[1] // 3
+    offset = out[:, :2 * n]                   # cat(o1, o2) == first two chunks
+    mask = sigmoid(out[:, 2 * n:])
+    w = sd[name + ".weight"]
+    return dcn_v2_forward(inp, w, sd[name + ".bias"], offset, mask, 3, 3, 1, 1, 1, 1, 1, 1, groups, dtype)
+
+
+# ----------------------------------------------------------------------------- encoder
+def resblock(x, sd, name, dtype):
+    """ResidualBlock_noBN (module_util.py:48-52): x + conv2(relu(conv1(x)))."""
+    out = relu(conv2d(x, sd[name + ".conv1.weight"], sd[name + ".conv1.bias"], dtype=dtype))
+    return x + conv2d(out, sd[name + ".conv2.weight"], sd[name + ".conv2.bias"], dtype=dtype)
+
+
+def pcd_align(fea1, fea2, sd, p, dtype):
+    """PCD_Align.forward (Sakuya_arch_test.py:71-130).  fea* = [L1, L2, L3]."""
+    c = lambda n, t, **kw: conv2d(t, sd[p + n + ".weight"], sd[p + n + ".bias"], dtype=dtype, **kw)
+    cat = lambda *t: np.concatenate(t, axis=1)
+    y = []
+    for d, (fa, fb) in ((1, (fea1, fea2)), (2, (fea2, fea1))):
+        s = f"_{d}"
+        L3_off = lrelu(c("L3_offset_conv1" + s, cat(fa[2], fb[2])))
+        L3_off = lrelu(c("L3_offset_conv2" + s, L3_off))
+        L3_fea = lrelu(dcn_sep(fa[2], L3_off, sd, p + "L3_dcnpack" + s, dtype=dtype))
+        L2_off = lrelu(c("L2_offset_conv1" + s, cat(fa[1], fb[1])))
+        L3_off = upsample2x(L3_off)
+        L2_off = lrelu(c("L2_offset_conv2" + s, cat(L2_off, L3_off * 2)))
+        L2_off = lrelu(c("L2_offset_conv3" + s, L2_off))
+        L2_fea = dcn_sep(fa[1], L2_off, sd, p + "L2_dcnpack" + s, dtype=dtype)
+        L3_fea = upsample2x(L3_fea)
+        L2_fea = lrelu(c("L2_fea_conv" + s, cat(L2_fea, L3_fea)))
+        L1_off = lrelu(c("L1_offset_conv1" + s, cat(fa[0], fb[0])))
+        L2_off = upsample2x(L2_off)
+        L1_off = lrelu(c("L1_offset_conv2" + s, cat(L1_off, L2_off * 2)))
+        L1_off = lrelu(c("L1_offset_conv3" + s, L1_off))
+        L1_fea = dcn_sep(fa[0], L1_off, sd, p + "L1_dcnpack" + s, dtype=dtype)
+        L2_fea = upsample2x(L2_fea)
+        L1_fea = c("L1_fea_conv" + s, cat(L1_fea, L2_fea))
+        y.append(L1_fea)
+    return np.concatenate(y, axis=1)
+
+
+def pyramid(L1, sd, p, dtype):
+    """fea_L2_conv1/2 + fea_L3_conv1/2 with lrelu (Sakuya_arch_test.py:321-325, :152-156)."""
+    c = lambda n, t, s: lrelu(conv2d(t, sd[p + n + ".weight"], sd[p + n + ".bias"], stride=s, dtype=dtype))
+    L2 = c("fea_L2_conv2", c("fea_L2_conv1", L1, 2), 1)
+    L3 = c("fea_L3_conv2", c("fea_L3_conv1", L2, 2), 1)
+    return L2, L3
+
+
+def easy_pcd(f1, f2, sd, p, dtype):
+    """Easy_PCD.forward (Sakuya_arch_test.py:144-166)."""
+    B = f1.shape[0]
+    L1 = np.concatenate([f1, f2], axis=0)          # stack on a batch axis; convs are per-image
+    L2, L3 = pyramid(L1, sd, p, dtype)
+    fea1 = [f1, L2[:B], L3[:B]]
+    fea2 = [f2, L2[B:], L3[B:]]
+    al = pcd_align(fea1, fea2, sd, p + "pcd_align.", dtype)
+    return conv2d(al, sd[p + "fusion.weight"], sd[p + "fusion.bias"], dtype=dtype)
+
+
+def conv_lstm_cell(x, h, c, sd, p, dtype):
+    """ConvLSTMCell.forward (convlstm.py:42-58)."""
+    cc = conv2d(np.concatenate([x, h], axis=1), sd[p + "conv.weight"], sd[p + "conv.bias"], dtype=dtype)
+    nh = h.shape[1]
+    i, f, o, g = (cc[:, k * nh:(k + 1) * nh] for k in range(4))
+    c_next = sigmoid(f) * c + sigmoid(i) * np.tanh(g)
+    h_next = sigmoid(o) * np.tanh(c_next)
+    return h_next, c_next
+
+
+def deformable_conv_lstm(xs, sd, p, dtype):
+    """DeformableConvLSTM.forward (Sakuya_arch_test.py:192-242), one layer, zero initial state
+    (convlstm.py:60-63).  xs: list over time of [B,64,H,W]."""
+    h = np.zeros_like(xs[0])
+    c = np.zeros_like(xs[0])
+    outs = []
+    for x in xs:
+        ht = easy_pcd(x, h, sd, p + "pcd_h.", dtype)
+        ct = easy_pcd(x, c, sd, p + "pcd_c.", dtype)
+        h, c = conv_lstm_cell(x, ht, ct, sd, p + "cell_list.0.", dtype)
+        outs.append(h)
+    return outs
+
+
+def bi_convlstm(xs, sd, dtype):
+    """BiDeformableConvLSTM.forward (Sakuya_arch_test.py:256-266): same weights both directions."""
+    p = "ConvBLSTM.forward_net."
+    fwd = deformable_conv_lstm(xs, sd, p, dtype)
+    rev = deformable_conv_lstm(xs[::-1], sd, p, dtype)[::-1]
+    return [conv2d(np.concatenate([a, b], axis=1), sd["ConvBLSTM.conv_1x1.weight"],
+                   sd["ConvBLSTM.conv_1x1.bias"], dtype=dtype) for a, b in zip(fwd, rev)]
+
+
+def frame_features(frames, sd, front_RBs=5, dtype=np.float64):
+    """Per-frame part of gen_feat (Sakuya_arch_test.py:318-325): [N,3,H,W] -> (L1, L2, L3)."""
+    L1 = lrelu(conv2d(frames, sd["conv_first.weight"], sd["conv_first.bias"], dtype=dtype))
+    for i in range(front_RBs):
+        L1 = resblock(L1, sd, f"feature_extraction.{i}", dtype)
+    L2, L3 = pyramid(L1, sd, "", dtype)
+    return L1, L2, L3
+
+
+def gen_feat(x, sd, front_RBs=5, back_RBs=40, dtype=np.float64, capture=None):
+    """LunaTokis.gen_feat (Sakuya_arch_test.py:313-362) for N=2 frames: x [B,2,3,H,W] -> [B,3,64,H,W]."""
+    B, N, C, H, W = x.shape
+    L1, L2, L3 = frame_features(np.asarray(x, dtype).reshape(B * N, C, H, W), sd, front_RBs, dtype)
+    lv = [t.reshape(B, N, *t.shape[1:]) for t in (L1, L2, L3)]
+    fea1 = [t[:, 0] for t in lv]
+    fea2 = [t[:, 1] for t in lv]
+    aligned = pcd_align(fea1, fea2, sd, "pcd_align.", dtype)
+    fused = conv2d(aligned, sd["fusion.weight"], sd["fusion.bias"], dtype=dtype)
+    if capture is not None:
+        capture["pcd_align"] = aligned
+        capture["fusion"] = fused
+    xs = [fea1[0], fused, fea2[0]]
+    feats = bi_convlstm(xs, sd, dtype)
+    if capture is not None:
+        capture["bilstm"] = np.stack(feats, axis=1)
+    out = np.concatenate(feats, axis=0)            # [3B,...] ordered t-major
+    for i in range(back_RBs):
+        out = resblock(out, sd, f"recon_trunk.{i}", dtype)
+    out = out.reshape(3, B, 64, H, W).transpose(1, 0, 2, 3, 4)
+    return np.ascontiguousarray(out)
+
+
+# ----------------------------------------------------------------------------- decoder
+def make_coord_1d(n):
+    """One axis of make_coord (Sakuya_arch_test.py:1233-1248) in the reference's fp32:
+    seq = fp32(-1 + r) + fp32(2r) * arange(n).float(), r = 1/n."""
+    r = 2.0 / (2 * n)
+    return (F32(2 * r) * np.arange(n, dtype=F32)).astype(F32) + F32(-1 + r)
+
+
+def linspace_f32(n):
+    """torch.linspace(-1, 1, n) on CPU in fp32 (warplayer.py:27-30)."""
+    if n == 1:
+        return np.array([-1.0], F32)
+    step = F32((1.0 - -1.0) / (n - 1))
+    i = np.arange(n)
+    lo = (F32(-1.0) + step * i.astype(F32)).astype(F32)
+    hi = (F32(1.0) - step * (n - 1 - i).astype(F32)).astype(F32)
+    return np.where(i < n // 2, lo, hi).astype(F32)
+
+
+
+def nearest_index(coord, n):
+    """grid_sample(mode='nearest', align_corners=False) source index: round-half-even in fp32."""
+    coord = np.asarray(coord, F32)
+    src = ((coord + F32(1)) * F32(n) - F32(1)) / F32(2)
+    return np.rint(src).astype(np.int64)
+
+
+def bilinear_sample(img, gx, gy, dtype=np.float64):
+    """F.grid_sample(img, grid, 'bilinear', padding_mode='zeros', align_corners=False).
+    img [B,C,H,W], gx/gy [B,Q] normalised (x along W, y along H) -> [B,Q,C]."""
+    B, C, H, W = img.shape
+    ix = ((np.asarray(gx, dtype) + 1) * W - 1) / 2
+    iy = ((np.asarray(gy, dtype) + 1) * H - 1) / 2
+    x0 = np.floor(ix)
+    y0 = np.floor(iy)
+    x1, y1 = x0 + 1, y0 + 1
+    wnw = (x1 - ix) * (y1 - iy)
+    wne = (ix - x0) * (y1 - iy)
+    wsw = (x1 - ix) * (iy - y0)
+    wse = (ix - x0) * (iy - y0)
+    flat = np.asarray(img, dtype).reshape(B, C, H * W).transpose(0, 2, 1)   # [B,HW,C]
+    b = np.arange(B)[:, None]
+    out = 0
+    for xx, yy, ww in ((x0, y0, wnw), (x1, y0, wne), (x0, y1, wsw), (x1, y1, wse)):
+        xi = xx.astype(np.int64)
+        yi = yy.astype(np.int64)
+        ok = (xi >= 0) & (xi < W) & (yi >= 0) & (yi < H)
+        v = flat[b, np.clip(yi, 0, H - 1) * W + np.clip(xi, 0, W - 1)]
+        out = out + np.where(ok[..., None], v, 0) * ww[..., None]
+    return out
+
+
+def siren(x, sd, p, n_sine, dtype):
+    """Siren.forward (SIREN.py:74-79): n_sine x sin(30*(xW^T+b)) then a final Linear."""
+    for i in range(n_sine):
+        x = np.sin(30.0 * (x @ np.asarray(sd[f"{p}net.{i}.linear.weight"], dtype).T
+                           + np.asarray(sd[f"{p}net.{i}.linear.bias"], dtype)))
+    return x @ np.asarray(sd[f"{p}net.{n_sine}.weight"], dtype).T + np.asarray(sd[f"{p}net.{n_sine}.bias"], dtype)
+
+
+def decoding(feat, inp, times, sd, scale=None, dtype=np.float64, capture=None):
+    """LunaTokis.decoding (Sakuya_arch_test.py:364-459).
+    feat [B,3,64,H,W], inp [B,2,3,H,W], times: list of floats -> list of [B,3,HH,WW]."""
+    B = feat.shape[0]
+    H, W = feat.shape[-2:]
+    featc = np.asarray(feat, dtype).reshape(B, 192, H, W)          # cat(feat[:,0..2]) (:365)
+    inpc = np.asarray(inp, dtype).reshape(B, 6, H, W)
+    HH, WW = (H * 4, W * 4) if scale is None else (int(scale[0]), int(scale[1]))
+    lo, hi = F32(-1 + 1e-6), F32(1 - 1e-6)
+    cy = np.clip(make_coord_1d(HH), lo, hi)                          # coord_highres (:373), row/col
+    cx = np.clip(make_coord_1d(WW), lo, hi)
+    ly, lx = make_coord_1d(H), make_coord_1d(W)                      # feat_coord (:375)
+    iy = np.clip(nearest_index(cy, H), 0, H - 1)
+    ix = np.clip(nearest_index(cx, W), 0, W - 1)
+    rel_y = ((cy - ly[iy]) * F32(H)).astype(F32)                     # (:394-396)
+    rel_x = ((cx - lx[ix]) * F32(W)).astype(F32)
+    Q = HH * WW
+    qy = np.repeat(np.arange(HH), WW)
+    qx = np.tile(np.arange(WW), HH)
+    gy = np.broadcast_to(cy[qy], (B, Q))
+    gx = np.broadcast_to(cx[qx], (B, Q))
+    lin = featc.reshape(B, 192, H * W).transpose(0, 2, 1)
+    q_feat = lin[:, iy[qy] * W + ix[qx]]                              # nearest (:382-385)
+    q_inp = inpc.reshape(B, 6, H * W).transpose(0, 2, 1)[:, iy[qy] * W + ix[qx]]
+    rel = np.stack([np.broadcast_to(rel_y[qy], (B, Q)), np.broadcast_to(rel_x[qx], (B, Q))], -1).astype(dtype)
+    gxs, gys = linspace_f32(WW), linspace_f32(HH)                     # warpgrid base (warplayer.py:27-31)
+    preds = []
+    for t in times:
+        pe = np.full((B, Q, 1), t, dtype)
+        x1 = np.concatenate([q_feat, q_inp, rel, pe], -1)             # 201 (:399)
+        hrfeat = siren(x1, sd, "feat_imnet.", 3, dtype)               # [B,Q,64] (:400)
+        # q_feat at the HR centres is HRfeat itself (nearest at its own pixel centres, :406-409)
+        hr_img = hrfeat.transpose(0, 2, 1).reshape(B, 64, HH, WW)
+        q_inp2 = bilinear_sample(inpc, gx, gy, dtype)                 # (:410-413)
+        q_feat0 = bilinear_sample(featc, gx, gy, dtype)               # (:414-417)
+        flow = siren(np.concatenate([hrfeat, q_feat0, q_inp2, pe], -1), sd, "flow_imnet.", 3, dtype)  # 263
+        if capture is not None:
+            capture.setdefault("hrfeat", []).append(hrfeat)
+            capture.setdefault("flow", []).append(flow)
+        fx = flow[..., [0, 2]]
+        fy = flow[..., [1, 3]]
+        # warpgrid (warplayer.py:25-39): base linspace grid + flow / ((n-1)/2); then clamp (:428,441)
+        bx = gxs[qx].astype(dtype)[None]
+        by = gys[qy].astype(dtype)[None]
+        feats = []
+        imgs = []
+        for k in range(2):
+            g_x = np.clip(bx + fx[..., k] / ((WW - 1.0) / 2.0), lo, hi)
+            g_y = np.clip(by + fy[..., k] / ((HH - 1.0) / 2.0), lo, hi)
+            feats.append((bilinear_sample(hr_img, g_x, g_y, dtype), bilinear_sample(featc, g_x, g_y, dtype)))
+            imgs.append(bilinear_sample(inpc, g_x, g_y, dtype))
+        x3 = np.concatenate([feats[0][0], feats[1][0], feats[0][1], feats[1][1], imgs[0], imgs[1], pe], -1)  # 525
+        pred = siren(x3, sd, "encode_imnet.", 4, dtype)                # (:456)
+        preds.append(pred.transpose(0, 2, 1).reshape(B, 3, HH, WW))
+    return preds
+
+
+def forward(x, times, sd, scale=None, front_RBs=5, back_RBs=40, dtype=np.float64, capture=None):
+    """LunaTokis.forward(x, times, scale, test=False) (Sakuya_arch_test.py:1222-1231)."""
+    feat = gen_feat(x, sd, front_RBs, back_RBs, dtype, capture)
+    if capture is not None:
+        capture["feat"] = feat
+    return decoding(feat, x, times, sd, scale, dtype, capture)

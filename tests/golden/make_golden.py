@@ -1,0 +1,251 @@
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE
+STIF model (``/root/reference/codes``) on CPU in this container.
+
+Only this script touches ``/root/reference``; it is run by hand (it skips when the
+reference is absent) and its outputs -- inputs + expected outputs, plain data --
+are committed.  The GPU box never sees the reference.
+
+Three shims make the reference importable without CUDA:
+  1. a stub ``torchvision`` (``SIREN.py:8`` imports names it never uses);
+  2. a stub ``_ext`` whose ``dcn_v2_forward`` is a CPU restatement of
+     ``dcn_v2_cuda_forward`` (``DCNv2/src/cuda/dcn_v2_cuda.cu:42-172``) with the
+     sampling of ``modulated_deformable_im2col_gpu_kernel`` /
+     ``dmcn_im2col_bilinear`` (``dcn_v2_im2col_cuda.cu:25-54,125-195``).  The
+     native extension itself cannot be built here (it needs the removed THC API),
+     so the DCN core is pinned by the reference's own zero-offset known-answer
+     test (``DCNv2/test.py:32-67``), which this script also records;
+  3. ``Tensor.cuda = identity`` for the hard ``.cuda()`` calls
+     (``convlstm.py:62-63``, ``Sakuya_arch_test.py:372-375``).
+Weights come from ``stif_amd.weights.make_state_dict(seed=0)`` and are loaded
+with ``load_state_dict(strict=True)``.
+
+Usage:  python tests/golden/make_golden.py
+"""
+import json
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference/codes"
+
+
+def dcn_v2_forward_cpu(input, weight, bias, offset, mask, kh, kw, sh, sw, ph, pw, dh, dw, dg):
+    """fp32 CPU restatement of the reference CUDA forward (see module docstring)."""
+    B, C, H, W = input.shape
+    Co = weight.shape[0]
+    Ho = (H + 2 * ph - (dh * (kh - 1) + 1)) // sh + 1
+    Wo = (W + 2 * pw - (dw * (kw - 1) + 1)) // sw + 1
+    cpg = C // dg
+    K = kh * kw
+    cols = torch.zeros(B, C, K, Ho, Wo, dtype=torch.float32)
+    h_in = (torch.arange(Ho) * sh - ph).view(1, 1, Ho, 1)
+    w_in = (torch.arange(Wo) * sw - pw).view(1, 1, 1, Wo)
+    img = input.reshape(B, C, H * W)
+    for i in range(kh):
+        for j in range(kw):
+            k = i * kw + j
+            off = offset.view(B, dg, K, 2, Ho, Wo)
+            off_h = off[:, :, k, 0]
+            off_w = off[:, :, k, 1]
+            m = mask.view(B, dg, K, Ho, Wo)[:, :, k]
+            h_im = (h_in + i * dh).float() + off_h          # [B, dg, Ho, Wo]
+            w_im = (w_in + j * dw).float() + off_w
+            inside = (h_im > -1) & (w_im > -1) & (h_im < H) & (w_im < W)
+            h_low = torch.floor(h_im)
+            w_low = torch.floor(w_im)
+            lh = h_im - h_low
+            lw = w_im - w_low
+            hh = 1 - lh
+            hw = 1 - lw
+            h_low = h_low.long()
+            w_low = w_low.long()
+            h_high = h_low + 1
+            w_high = w_low + 1
+
+            def corner(hc, wc, ok):
+                idx = (hc.clamp(0, H - 1) * W + wc.clamp(0, W - 1))     # [B, dg, Ho, Wo]
+                idx = idx.repeat_interleave(cpg, dim=1).view(B, C, Ho * Wo)
+                v = torch.gather(img, 2, idx).view(B, C, Ho, Wo)
+                return torch.where(ok.repeat_interleave(cpg, dim=1), v, torch.zeros((), dtype=v.dtype))
+
+            v1 = corner(h_low, w_low, (h_low >= 0) & (w_low >= 0))
+            v2 = corner(h_low, w_high, (h_low >= 0) & (w_high <= W - 1))
+            v3 = corner(h_high, w_low, (h_high <= H - 1) & (w_low >= 0))
+            v4 = corner(h_high, w_high, (h_high <= H - 1) & (w_high <= W - 1))
+            rep = lambda t: t.repeat_interleave(cpg, dim=1)
+            w1, w2, w3, w4 = rep(hh * hw), rep(hh * lw), rep(lh * hw), rep(lh * lw)
+            val = w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4
+            val = torch.where(rep(inside), val, torch.zeros((), dtype=val.dtype))
+            cols[:, :, k] = val * rep(m)
+    cols = cols.view(B, C * K, Ho * Wo)
+    out = torch.einsum("ok,bkn->bon", weight.reshape(Co, C * K), cols) + bias.view(1, Co, 1)
+    return out.view(B, Co, Ho, Wo)
+
+
+def install_shims():
+    tv = types.ModuleType("torchvision")
+    tvt = types.ModuleType("torchvision.transforms")
+    for n in ["Resize", "Compose", "ToTensor", "Normalize"]:
+        setattr(tvt, n, object)
+    tv.transforms = tvt
+    sys.modules["torchvision"] = tv
+    sys.modules["torchvision.transforms"] = tvt
+    ext = types.ModuleType("_ext")
+    ext.dcn_v2_forward = dcn_v2_forward_cpu
+    sys.modules["_ext"] = ext
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    sys.path.insert(0, REF)
+
+
+def f32(t):
+    return t.detach().cpu().numpy().astype(np.float32)
+
+
+def main():
+    if not os.path.isdir(REF):
+        print("reference absent; nothing to do")
+        return
+    install_shims()
+    sys.path.insert(0, REPO)
+    import stif_pkg
+    stif = stif_pkg.load()
+    import models.modules.Sakuya_arch_test as S
+    import models.modules.warplayer as WL
+    from models.modules.convlstm import ConvLSTMCell
+    from models.modules.DCNv2.dcn_v2 import dcn_v2_conv, DCNv2
+
+    torch.set_num_threads(8)
+    sd_np = stif.weights.make_state_dict(seed=0)
+    model = S.LunaTokis(64, 6, 8, 5, 40)
+    ref_sd = model.state_dict()
+    json.dump([[k, list(v.shape)] for k, v in ref_sd.items()],
+              open(os.path.join(HERE, "state_dict_spec.json"), "w"))
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd_np.items()}, strict=True)
+    model.eval()
+
+    # ---------------- full model, small non-square LR -----------------
+    cap = {}
+
+    def hook(name):
+        def fn(mod, inp, out):
+            cap.setdefault(name, []).append(out)
+        return fn
+
+    model.pcd_align.register_forward_hook(hook("pcd_align"))
+    model.fusion.register_forward_hook(hook("fusion"))
+    model.ConvBLSTM.register_forward_hook(hook("bilstm"))
+    model.feat_imnet.register_forward_hook(hook("feat_imnet"))
+    model.flow_imnet.register_forward_hook(hook("flow_imnet"))
+    model.ConvBLSTM.forward_net.pcd_h.register_forward_hook(hook("pcd_h"))
+    model.ConvBLSTM.forward_net.cell_list[0].register_forward_hook(hook("cell"))
+
+    g = torch.Generator().manual_seed(1234)
+    H, W = 16, 20
+    x = torch.rand(1, 2, 3, H, W, generator=g)
+    times = [0.0, 0.25, 0.5, 0.75]
+    with torch.no_grad():
+        outs = model(x, [torch.tensor([[t]]) for t in times])
+        feat = model.feat
+        out25 = model.decoding([torch.tensor([[0.5]])], scale=(40, 50))[0]
+    hr = cap["feat_imnet"][2].view(1, H * 4 * W * 4, 64)
+    fl = cap["flow_imnet"][2].view(1, H * 4 * W * 4, 4)
+    np.savez_compressed(
+        os.path.join(HERE, "model_16x20.npz"),
+        x=f32(x), times=np.array(times, np.float32), out=np.stack([f32(o[0]) for o in outs]),
+        feat=f32(feat[0]), out_scale_40x50=f32(out25[0]),
+        pcd_align=f32(cap["pcd_align"][0][0]), fusion=f32(cap["fusion"][0][0]),
+        bilstm=f32(cap["bilstm"][0][0]), pcd_h_t0=f32(cap["pcd_h"][0][0]),
+        cell_h_t0=f32(cap["cell"][0][0][0]), cell_c_t0=f32(cap["cell"][0][1][0]),
+        hrfeat_t05=f32(hr[0]), flow_t05=f32(fl[0]),
+    )
+    print("model: out", [tuple(o.shape) for o in outs], "range", float(outs[2].min()), float(outs[2].max()))
+
+    # ---------------- 7-frame sliding window (custom_video_test.py:81-97) -----
+    g = torch.Generator().manual_seed(4321)
+    frames = torch.rand(7, 3, 16, 16, generator=g)
+    wouts = []
+    with torch.no_grad():
+        for i in range(6):
+            wouts.append(model(frames[i:i + 2][None], [torch.tensor([[0.5]])])[0][0])
+    np.savez_compressed(os.path.join(HERE, "window_7x16x16.npz"),
+                        frames=f32(frames), out=np.stack([f32(o) for o in wouts]))
+    print("window done")
+
+    # ---------------- per-op fixtures -----------------
+    ops = {}
+    g = torch.Generator().manual_seed(99)
+    # DCN zero-offset KAT, DCNv2/test.py:32-67 (identity kernel, mask = sigmoid(0))
+    N_, C_, H_, W_ = 2, 2, 4, 4
+    inp = torch.randn(N_, C_, H_, W_, generator=g)
+    wid = torch.zeros(C_, C_, 3, 3)
+    for p in range(C_):
+        wid[p, p, 1, 1] = 1.0
+    off0 = torch.zeros(N_, 2 * 9, H_, W_)
+    m0 = torch.sigmoid(torch.zeros(N_, 9, H_, W_))
+    out_kat = dcn_v2_conv(inp, off0, m0, wid, torch.zeros(C_), 1, 1, 1, 1)
+    assert float((inp - 2 * out_kat).abs().max()) < 1e-10
+    ops["kat_input"] = f32(inp)
+
+    # DCN_sep module of the reference on random tensors (dcn_v2.py:127-140)
+    dsep = model.pcd_align.L2_dcnpack_1
+    a = torch.rand(2, 64, 9, 11, generator=g)
+    b = torch.rand(2, 64, 9, 11, generator=g) * 2 - 0.5
+    with torch.no_grad():
+        ops["dcnsep_out"] = f32(dsep(a, b))
+    ops["dcnsep_in"] = f32(a)
+    ops["dcnsep_fea"] = f32(b)
+
+    # bilinear x2 upsample (PCD_Align uses it 4x per direction, :86-125)
+    u = torch.randn(2, 5, 6, 7, generator=g)
+    ops["up2_in"] = f32(u)
+    ops["up2_out"] = f32(F.interpolate(u, scale_factor=2, mode="bilinear", align_corners=False))
+
+    # grid_sample bilinear, zeros padding, align_corners=False with out-of-range grid points
+    gi = torch.randn(1, 7, 9, 11, generator=g)
+    gg = torch.rand(1, 1, 500, 2, generator=g) * 2.6 - 1.3
+    ops["gs_in"] = f32(gi)
+    ops["gs_grid"] = f32(gg)
+    ops["gs_bilinear"] = f32(F.grid_sample(gi, gg, mode="bilinear", align_corners=False))
+    ops["gs_nearest"] = f32(F.grid_sample(gi, gg, mode="nearest", align_corners=False))
+
+    # nearest-index maps of the decoder's first gather (Sakuya_arch_test.py:382-393), incl. 2.5x ties
+    sizes = [(16, 20, 40, 50), (24, 32, 60, 80), (135, 240, 337, 600), (32, 32, 128, 128), (5, 7, 13, 17), (16, 20, 64, 80)]
+    for (h, w, hh, ww) in sizes:
+        c = S.make_coord((hh, ww)).clamp(-1 + 1e-6, 1 - 1e-6)
+        idx_img = torch.arange(h * w).float().view(1, 1, h, w)
+        o = F.grid_sample(idx_img, c.flip(-1).unsqueeze(0).unsqueeze(0), mode="nearest", align_corners=False)
+        o = o[0, 0, 0].long().view(hh, ww)
+        ops[f"nearest_{h}x{w}_{hh}x{ww}_row"] = (o[:, 0] // w).numpy().astype(np.int32)
+        ops[f"nearest_{h}x{w}_{hh}x{ww}_col"] = (o[0, :] % w).numpy().astype(np.int32)
+        ops[f"coord_{hh}x{ww}"] = f32(S.make_coord((hh, ww)))
+
+    # SIREN (feat_imnet) on random input
+    si = torch.rand(100, 201, generator=g) * 2 - 1
+    with torch.no_grad():
+        ops["siren_in"] = f32(si)
+        ops["siren_out"] = f32(model.feat_imnet(si))
+
+    # warpgrid (warplayer.py:25-39)
+    fl_in = torch.randn(1, 2, 12, 16, generator=g) * 3
+    ops["warp_flow"] = f32(fl_in)
+    ops["warp_grid"] = f32(WL.warpgrid(torch.zeros(1, 3, 12, 16), fl_in)[0])
+
+    # ConvLSTMCell (convlstm.py:42-58) with the model's cell weights
+    cx = torch.randn(1, 64, 6, 8, generator=g)
+    ch = torch.randn(1, 64, 6, 8, generator=g)
+    cc = torch.randn(1, 64, 6, 8, generator=g)
+    with torch.no_grad():
+        hn, cn = model.ConvBLSTM.forward_net.cell_list[0](cx, [ch, cc])
+    ops.update(cell_x=f32(cx), cell_h=f32(ch), cell_c=f32(cc), cell_hn=f32(hn), cell_cn=f32(cn))
+    np.savez_compressed(os.path.join(HERE, "ops.npz"), **ops)
+    print("ops done:", len(ops))
+
+
+if __name__ == "__main__":
+    main()
