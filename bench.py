@@ -1,0 +1,190 @@
+"""Benchmark of the STIF LunaTokis forward on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): a synthetic 7-frame 3x256x256 window = 6
+adjacent pairs, 4x spatial, one interpolated time t=0.5 -> 6 x 1024x1024 output
+pixels per GPU per step.  A step = gen_feat over the window (per-frame encoder,
+PCD alignment, Bi-Deformable-ConvLSTM, 40-block trunk) + the implicit decoder,
+with inputs already resident in HBM.  Multi-GPU: one process per GPU; rank r owns
+frames [6r, 6r+6] of a (6N+1)-frame sequence (the shared boundary frame is the
+temporal halo), so per-GPU work is fixed (weak scaling) and no collective is on
+the data path.  Rank 0 prints one JSON line.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c0|c2]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+BASE = json.load(open(os.path.join(REPO, "BASELINE.json")))
+CONFIGS = {
+    # name: (frames, H, W, scale, times)
+    "c0": (7, 128, 128, 4, [0.5]),
+    "c1": (7, 256, 256, 4, [0.5]),
+    "c2": (7, 540, 960, 4, [0.25, 0.5, 0.75]),
+}
+FP32_PEAK_TFLOPS = 157.3   # MI355X dense fp32 MFMA (MI355X_MICROARCH.md, chip-level parameters)
+
+
+class KernelTimer:
+    """HIP-event timing of every launch of one kernel variant, on the launch stream."""
+
+    def __init__(self, kind):
+        self.kind = kind
+        self.rec = []
+        self._cur = None
+
+    def begin(self, kind, flops):
+        if kind == self.kind:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            self._cur = (e0, e1, flops)
+
+    def end(self):
+        if self._cur is not None:
+            self._cur[1].record()
+            self.rec.append(self._cur)
+            self._cur = None
+
+    def summary(self):
+        ms = [a.elapsed_time(b) for a, b, _ in self.rec]
+        fl = [f for _, _, f in self.rec]
+        return len(ms), float(np.mean(ms)) if ms else 0.0, float(np.mean(fl)) if fl else 0.0
+
+
+def synth_frames(first, count, H, W, device):
+    """Deterministic synthetic frames: frame k = U[0,1) from a generator seeded by its global index."""
+    out = torch.empty(count, 3, H, W)
+    for i in range(count):
+        g = torch.Generator().manual_seed(1234 + first + i)
+        out[i] = torch.rand(3, H, W, generator=g)
+    return out.to(device)
+
+
+def cpu_baseline(stif, sd, frames_cpu, times, scale):
+    """The numpy oracle (fp32) on ONE pair of the same window, all host BLAS threads."""
+    from oracle import stif_oracle as O
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:
+        threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    x = frames_cpu[0:2].numpy()[None]
+    t0 = time.perf_counter()
+    O.forward(x, times, sd, dtype=np.float32)
+    dt = time.perf_counter() - t0
+    H, W = x.shape[-2:]
+    mpix = len(times) * H * scale * W * scale / 1e6
+    return {"value": mpix / dt, "unit": "Mpix/s", "cores": threads, "kind": "port",
+            "sample": f"1 pair (frames 0-1) of the same window, {H}x{W} -> {H * scale}x{W * scale}, "
+                      f"t={times}, numpy fp32 restatement (oracle/stif_oracle.py), {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c1", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_r01.json"))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as td
+        torch.cuda.set_device(local)
+        td.init_process_group("nccl")
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    import stif_pkg
+    stif = stif_pkg.load()
+    nframes, H, W, scale, times = CONFIGS[args.config]
+    pairs = nframes - 1
+    sd = stif.weights.make_state_dict(seed=0)
+    model = stif.LunaTokis(64, 6, 8, 5, 40, device=device)
+    model.load_state_dict(sd, strict=True)
+    frames_cpu = synth_frames(rank * pairs, nframes, H, W, "cpu")
+    frames = frames_cpu.to(device)
+    tq = [torch.tensor([[t]], device=device) for t in times]
+
+    def step():
+        model.gen_feat_window(frames)
+        return model.decoding(tq)
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        timer = KernelTimer(("conv", 3, 1, stif._lib.EPI_RES, 0, 64))
+        stif.ops.TRACE = timer
+        if dist:
+            td.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        if dist:
+            td.barrier()
+        elapsed = time.perf_counter() - t0
+        stif.ops.TRACE = None
+    if dist:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        td.all_reduce(t, op=td.ReduceOp.MAX)
+        elapsed = float(t.item())
+    n_launch, avg_ms, avg_flops = timer.summary()
+
+    out_pix = pairs * len(times) * (H * scale) * (W * scale)
+    value = world * out_pix * args.steps / elapsed / 1e6
+    if rank == 0:
+        achieved = avg_flops / (avg_ms * 1e-3) / 1e12 if avg_ms else 0.0
+        traffic = None
+        if os.path.exists(args.traffic):
+            try:
+                traffic = json.load(open(args.traffic)).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        res = {
+            "metric": BASE["metric"],
+            "value": round(value, 4),
+            "unit": "Mpix/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (U[0,1) frames, seeded; deterministic generated weights: checkpoint not in tree)",
+            "config": {"workload": f"{nframes}x3x{H}x{W} window ({pairs} pairs), {scale}x spatial, t={times}",
+                       "frames_per_gpu": nframes, "lr_hw": [H, W], "scale": scale, "times": times,
+                       "parallelism": f"pair-sharded x{world} (1-frame halo, no collective)"},
+            "roofline": {"bound": "mfma", "kernel": "k_conv<3,1,2,2,0,EPI_RES> (3x3 64->64 conv + residual)",
+                         "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+                         "launches": n_launch, "avg_launch_us": round(avg_ms * 1e3, 2),
+                         "flops_per_launch": avg_flops},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            res["cpu_baseline"] = cpu_baseline(stif, sd, frames_cpu, times, scale)
+        print(json.dumps(res), flush=True)
+    if dist:
+        td.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

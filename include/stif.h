@@ -1,0 +1,172 @@
+/*
+ * stif.h -- C ABI of libstif_hip.so, the MI355X (gfx950) engine for the STIF
+ * LunaTokis forward (reference: codes/models/modules/Sakuya_arch_test.py).
+ *
+ * Conventions (every entry point):
+ *   - plain device pointers (fp32), sizes as ints; no framework types;
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream);
+ *   - outputs and workspaces are caller-allocated; nothing allocates per call;
+ *   - stateless and reentrant; returns 0 on success or a STIF_E_* code, with a
+ *     message retrievable through stif_last_error() (thread-local);
+ *   - feature maps are NHWC ([item][y][x][channel]) unless a name says NCHW.
+ *
+ * The drop-in for the reference's native operator is stif_dcn_v2_forward; it
+ * replaces `_ext.dcn_v2_forward` (DCNv2/src/vision.cpp:4, declared
+ * DCNv2/src/dcn_v2.h:9-23, CUDA body DCNv2/src/cuda/dcn_v2_cuda.cu:42-172).
+ * The remaining entry points are the fused stages the engine's LunaTokis host
+ * (stif_amd.model) drives; INTEGRATION.md shows the reference-side bindings.
+ */
+#ifndef STIF_H
+#define STIF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  STIF_OK = 0,
+  STIF_E_INVALID = 1,   /* bad argument / unsupported shape */
+  STIF_E_LAUNCH = 2,    /* kernel launch failed */
+  STIF_E_WORKSPACE = 3  /* workspace too small */
+};
+
+/* activation / epilogue selector of stif_conv2d_nhwc and stif_dcn_nhwc */
+enum {
+  STIF_EPI_NONE = 0,
+  STIF_EPI_LRELU = 1,   /* LeakyReLU(0.1)  (Sakuya_arch_test.py:69) */
+  STIF_EPI_RELU = 2,    /* ReLU            (module_util.py:51) */
+  STIF_EPI_RES = 3,     /* out = res + conv (ResidualBlock_noBN, module_util.py:48-52) */
+  STIF_EPI_OFFMASK = 4, /* sigmoid on the mask channels of a DCN offset/mask conv (dcn_v2.py:134-138) */
+  STIF_EPI_LSTM = 5     /* ConvLSTMCell gates (convlstm.py:47-56): out=h_next, out2=c_next, res=c_cur */
+};
+
+#define STIF_MAX_GROUPS 8
+
+/* Direct/implicit-GEMM convolution on NHWC fp32 maps (replaces nn.Conv2d in the
+ * hot path).  The input is the channel concatenation [in0 | in1] (so torch.cat
+ * never materialises); in1 may be read through a fused bilinear x2 upsample
+ * (F.interpolate(scale_factor=2, mode='bilinear', align_corners=False) times
+ * in1_scale, Sakuya_arch_test.py:86-87).  A launch covers `ngroups` weight sets
+ * x `nitems` items per set (item i of set g uses in0[g] + i*in0_item, ...).
+ * Weights are packed by stif_pack_conv_weight. */
+typedef struct {
+  const float* in0[STIF_MAX_GROUPS];
+  const float* in1[STIF_MAX_GROUPS];
+  const float* w[STIF_MAX_GROUPS];     /* packed, see stif_pack_conv_weight */
+  const float* bias[STIF_MAX_GROUPS];  /* [cout_pad], packed order */
+  float* out[STIF_MAX_GROUPS];
+  const float* res[STIF_MAX_GROUPS];   /* STIF_EPI_RES: residual; STIF_EPI_LSTM: c_cur */
+  float* out2[STIF_MAX_GROUPS];        /* STIF_EPI_LSTM: c_next */
+  long long in0_item, in1_item, out_item, res_item, out2_item;  /* element strides between items */
+  int ngroups, nitems;
+  int H, W, C0;            /* in0: H x W x C0, C0 % 8 == 0 */
+  int C1, in1_mode;        /* in1_mode: 0 none, 1 same resolution, 2 half resolution + x2 bilinear */
+  float in1_scale;
+  int Ho, Wo;              /* output resolution */
+  int cout;                /* logical output channels (64, 216, 256) */
+  int ks, stride;          /* 1 or 3; 1 or 2 (padding = ks/2) */
+  int epi;                 /* STIF_EPI_* */
+} stif_conv_args;
+
+int stif_conv2d_nhwc(const stif_conv_args* args, void* stream);
+
+/* conv_first (3 -> 64, 3x3) + LeakyReLU, reading NCHW RGB frames [n,3,h,w]
+ * (Sakuya_arch_test.py:318) and writing NHWC [n,h,w,64]. w: [64,3,3,3] as in the state dict. */
+int stif_conv_first(const float* x_nchw, const float* w, const float* b, float* out,
+                    int n, int h, int w_, void* stream);
+
+/* Fused modulated deformable conv (DCN_sep core, 64 -> 64, 3x3, 8 groups):
+ * bilinear sampling (dmcn_im2col_bilinear semantics) straight into LDS and an
+ * fp32-MFMA contraction; no columns buffer.  offmask is the NHWC output of the
+ * offset/mask conv packed with STIF_PACK_OFFMASK (216 channels per pixel,
+ * [group][tap][dy, dx, sigmoid(mask)]). */
+typedef struct {
+  const float* in[STIF_MAX_GROUPS];
+  const float* offmask[STIF_MAX_GROUPS];
+  const float* w[STIF_MAX_GROUPS];     /* packed like a 64->64 3x3 conv */
+  const float* bias[STIF_MAX_GROUPS];
+  float* out[STIF_MAX_GROUPS];
+  long long in_item, om_item, out_item;
+  int ngroups, nitems, H, W;
+  int epi;                              /* STIF_EPI_NONE or STIF_EPI_LRELU */
+} stif_dcn_args;
+
+int stif_dcn_nhwc(const stif_dcn_args* args, void* stream);
+
+/* Drop-in for `_ext.dcn_v2_forward` (dcn_v2.h:9-23): NCHW fp32 input [b,c,h,w],
+ * weight [co,c,kh,kw], bias [co], offset [b, dg*2*kh*kw, ho, wo],
+ * mask [b, dg*kh*kw, ho, wo]; output [b, co, ho, wo] (caller-allocated).
+ * Any kernel/stride/pad/dilation/group combination of the reference is
+ * accepted.  workspace: see stif_dcn_v2_workspace_size (0 bytes suffice for the
+ * generic path). */
+size_t stif_dcn_v2_workspace_size(int batch, int channels, int height, int width, int channels_out,
+                                  int kernel_h, int kernel_w, int stride_h, int stride_w, int pad_h,
+                                  int pad_w, int dilation_h, int dilation_w, int deformable_group);
+int stif_dcn_v2_forward(const float* input, const float* weight, const float* bias,
+                        const float* offset, const float* mask, float* output,
+                        int batch, int channels, int height, int width, int channels_out,
+                        int kernel_h, int kernel_w, int stride_h, int stride_w, int pad_h, int pad_w,
+                        int dilation_h, int dilation_w, int deformable_group,
+                        void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---- implicit decoder (LunaTokis.decoding, Sakuya_arch_test.py:364-459) ---- */
+
+/* Assemble the decoder's LR source map [n,h,w,200] = [feat t0 | t1 | t2 | inp rgb0 rgb1 | 0 0]
+ * from the three NHWC latent maps and the NCHW input pair x [n,2,3,h,w]. */
+int stif_dec_pack_lr(const float* f0, const float* f1, const float* f2, const float* x_nchw,
+                     float* out, int n, int h, int w, void* stream);
+
+/* Per-axis sampling tables of the HR query grid (host-computed, fp32, see
+ * stif_amd.coords): for every HR row (then column): nearest LR index, rel
+ * coordinate, bilinear LR indices i0/i1, weights w0/w1 (0 if out of range), and
+ * the warpgrid linspace base. Layout: struct of arrays, one float/int per entry. */
+typedef struct {
+  const int* near_y; const float* rel_y; const int* by0; const int* by1; const float* wy0; const float* wy1;
+  const float* lin_y;
+  const int* near_x; const float* rel_x; const int* bx0; const int* bx1; const float* wx0; const float* wx1;
+  const float* lin_x;
+} stif_dec_tables;
+
+/* Stage 1 (per HR pixel): feat_imnet -> HRfeat [n,HH,WW,64]; flow_imnet -> flow [n,HH,WW,4].
+ * proj: [n,h,w,256] LR projections (P1 | P2 | P3 | P4) from stif_conv2d_nhwc (1x1, packed by
+ * stif_pack_dec_proj).  mlp: packed by stif_pack_dec_mlp.  t: [n] query time per item. */
+int stif_dec_stage1(const float* proj, const float* mlp, const stif_dec_tables* tab, const float* t,
+                    float* hrfeat, float* flow, int n, int h, int w, int HH, int WW, void* stream);
+
+/* Stage 2 (per HR pixel): warp grids from flow, bilinear HRfeat / projections, encode_imnet
+ * -> RGB, written NCHW [n,3,HH,WW] (LunaTokis output layout, unclamped). */
+int stif_dec_stage2(const float* proj, const float* mlp, const float* hrfeat, const float* flow,
+                    const stif_dec_tables* tab, const float* t, float* out_nchw,
+                    int n, int h, int w, int HH, int WW, void* stream);
+
+/* ---- host-side weight packing (pure CPU, callable without a GPU) ---- */
+enum { STIF_PACK_PLAIN = 0, STIF_PACK_OFFMASK = 1, STIF_PACK_LSTM = 2 };
+
+/* Size in floats of a packed conv weight / bias. */
+size_t stif_conv_weight_floats(int cout, int cin, int ks);
+size_t stif_conv_bias_floats(int cout);
+/* w_oihw: [cout][cin][ks][ks] (nn.Conv2d layout).  dst layout: [cin/8][cout_pad][ks*ks][8],
+ * cout_pad = cout rounded up to 32, rows permuted per `mode`. */
+int stif_pack_conv_weight(const float* w_oihw, const float* b, int cout, int cin, int ks, int mode,
+                          float* w_dst, float* b_dst);
+
+size_t stif_dec_proj_floats(void);   /* packed 1x1 weight of the LR projection: [25][256][1][8] */
+int stif_pack_dec_proj(const float* feat_w0, const float* feat_b0, const float* flow_w0,
+                       const float* enc_w0, float* w_dst, float* b_dst);
+size_t stif_dec_mlp_floats(void);
+/* Packs every remaining feat/flow/encode_imnet weight (state-dict shapes, see stif_amd.weights)
+ * in the order stif_dec_stage1/2 consume them. Pointers follow the Siren layer order:
+ * feat: w0,b0,w1,b1,w2,b2,w3,b3; flow: same; enc: w0..w4, b0..b4 interleaved. */
+int stif_pack_dec_mlp(const float* const* feat, const float* const* flow, const float* const* enc,
+                      float* dst);
+
+const char* stif_last_error(void);
+const char* stif_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* STIF_H */

@@ -1,5 +1,27 @@
 """stif_amd: MI355X-native (gfx950) engine for the STIF LunaTokis forward.
 
 Import through ``stif_pkg.load()`` (the directory name is not a Python identifier).
+Layout:
+  csrc/       HIP kernels (conv, DCN, decoder) + C ABI (include/stif.h) + host packing
+  _lib.py     ctypes binding of libstif_hip.so (no fallback: missing library -> error)
+  ops.py      torch-buffer wrappers of the C ABI
+  model.py    LunaTokis host (reference API: forward / gen_feat / decoding / load_state_dict)
+  dcn_v2.py   reference DCNv2 plugin API (dcn_v2_conv, DCN_sep, ...) on the drop-in op
+  coords.py   fp32 query-grid tables of the decoder
+  weights.py  state-dict spec + deterministic weight generator
+  video.py    custom_video_test-style sliding-window driver
+  parallel.py frame-pair sharding over ranks
 """
 from . import weights  # noqa: F401
+from . import coords  # noqa: F401
+
+
+def __getattr__(name):
+    # torch-dependent parts load lazily so that weight/coords utilities work without torch/GPU
+    if name in ("ops", "model", "dcn_v2", "video", "parallel", "_lib"):
+        import importlib
+        return importlib.import_module(f"{__name__}.{name}")
+    if name == "LunaTokis":
+        from .model import LunaTokis
+        return LunaTokis
+    raise AttributeError(name)

@@ -1,0 +1,92 @@
+"""ctypes binding of libstif_hip.so (the C ABI declared in include/stif.h).
+
+The library is built in-tree (``make`` / ``__graft_entry__.build()``).  There is
+no fallback: if the library is missing or fails to load, every op raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libstif_hip.so")
+
+MAXG = 8
+EPI_NONE, EPI_LRELU, EPI_RELU, EPI_RES, EPI_OFFMASK, EPI_LSTM = range(6)
+PACK_PLAIN, PACK_OFFMASK, PACK_LSTM = range(3)
+
+_P = C.c_void_p
+_PA = _P * MAXG
+
+
+class ConvArgs(C.Structure):
+    _fields_ = [
+        ("in0", _PA), ("in1", _PA), ("w", _PA), ("bias", _PA), ("out", _PA), ("res", _PA), ("out2", _PA),
+        ("in0_item", C.c_longlong), ("in1_item", C.c_longlong), ("out_item", C.c_longlong),
+        ("res_item", C.c_longlong), ("out2_item", C.c_longlong),
+        ("ngroups", C.c_int), ("nitems", C.c_int),
+        ("H", C.c_int), ("W", C.c_int), ("C0", C.c_int),
+        ("C1", C.c_int), ("in1_mode", C.c_int), ("in1_scale", C.c_float),
+        ("Ho", C.c_int), ("Wo", C.c_int), ("cout", C.c_int), ("ks", C.c_int), ("stride", C.c_int),
+        ("epi", C.c_int),
+    ]
+
+
+class DcnArgs(C.Structure):
+    _fields_ = [
+        ("inp", _PA), ("offmask", _PA), ("w", _PA), ("bias", _PA), ("out", _PA),
+        ("in_item", C.c_longlong), ("om_item", C.c_longlong), ("out_item", C.c_longlong),
+        ("ngroups", C.c_int), ("nitems", C.c_int), ("H", C.c_int), ("W", C.c_int), ("epi", C.c_int),
+    ]
+
+
+class DecTables(C.Structure):
+    _fields_ = [(n, _P) for n in ("near_y", "rel_y", "by0", "by1", "wy0", "wy1", "lin_y",
+                                  "near_x", "rel_x", "bx0", "bx1", "wx0", "wx1", "lin_x")]
+
+
+EXPORTS = {
+    # name: (restype, argtypes)
+    "stif_conv2d_nhwc": (C.c_int, [C.POINTER(ConvArgs), _P]),
+    "stif_conv_first": (C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, C.c_int, _P]),
+    "stif_dcn_nhwc": (C.c_int, [C.POINTER(DcnArgs), _P]),
+    "stif_dcn_v2_workspace_size": (C.c_size_t, [C.c_int] * 14),
+    "stif_dcn_v2_forward": (C.c_int, [_P] * 6 + [C.c_int] * 14 + [_P, C.c_size_t, _P]),
+    "stif_dec_pack_lr": (C.c_int, [_P, _P, _P, _P, _P, C.c_int, C.c_int, C.c_int, _P]),
+    "stif_dec_stage1": (C.c_int, [_P, _P, C.POINTER(DecTables), _P, _P, _P] + [C.c_int] * 5 + [_P]),
+    "stif_dec_stage2": (C.c_int, [_P, _P, _P, _P, C.POINTER(DecTables), _P, _P] + [C.c_int] * 5 + [_P]),
+    "stif_conv_weight_floats": (C.c_size_t, [C.c_int, C.c_int, C.c_int]),
+    "stif_conv_bias_floats": (C.c_size_t, [C.c_int]),
+    "stif_pack_conv_weight": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P]),
+    "stif_dec_proj_floats": (C.c_size_t, []),
+    "stif_pack_dec_proj": (C.c_int, [_P] * 6),
+    "stif_dec_mlp_floats": (C.c_size_t, []),
+    "stif_pack_dec_mlp": (C.c_int, [C.POINTER(_P), C.POINTER(_P), C.POINTER(_P), _P]),
+    "stif_last_error": (C.c_char_p, []),
+    "stif_version": (C.c_char_p, []),
+}
+
+_lib = None
+
+
+class StifError(RuntimeError):
+    """Raised for any non-zero status of the C ABI (the reference surfaces AT_ERROR as RuntimeError)."""
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise StifError(f"{LIB_PATH} not built; run `make` (or __graft_entry__.build())")
+        h = C.CDLL(LIB_PATH)
+        for name, (res, args) in EXPORTS.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = h
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().stif_last_error().decode(errors="replace")
+        raise StifError(f"{what} failed (code {rc}): {msg}")

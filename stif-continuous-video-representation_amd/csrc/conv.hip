@@ -1,0 +1,318 @@
+// Implicit-GEMM convolution on NHWC fp32 maps with fp32 MFMA (v_mfma_f32_32x32x2_f32).
+//
+// Replaces every nn.Conv2d of the STIF encoder (Sakuya_arch_test.py:282-293, PCD_Align
+// :29-67, Easy_PCD :136-141, ConvLSTMCell convlstm.py:36-40, BiDeformableConvLSTM :254)
+// and fuses what the reference runs as separate ATen ops around them:
+//   * torch.cat of the two inputs       -> read from two pointers (in0 | in1)
+//   * F.interpolate(x2, bilinear) (*2)  -> computed while staging in1 into LDS
+//   * bias + LeakyReLU / ReLU / residual add / sigmoid(mask) / ConvLSTM gates -> epilogue
+//
+// GEMM view: M = output pixels, N = output channels, K = cin * ks * ks.
+// Workgroup = 4 waves; tile = (4*MT) output rows x 32 columns x (32*NT) couts.
+// Wave w owns MT rows (one 32-pixel MFMA M-tile each) x NT N-tiles.
+// K is walked in chunks of 8 input channels: the chunk's halo tile and weight
+// slice are staged in LDS, then every tap issues 4 MFMAs per (M,N) tile: lane
+// half h supplies channels 4h..4h+3 of the chunk through one ds_read_b128 for A
+// (input) and one for B (weights) -- the K order inside a chunk is a permutation
+// shared by both operands, so no shuffles are needed.
+#include "stif_common.h"
+#include "stif.h"
+#include "abi_util.h"
+
+namespace {
+
+template <int KS, int S, int MT, int NT, int IN1, int EPI>
+__global__ __launch_bounds__(256) void k_conv(stif_conv_args a) {
+  constexpr int TH = 4 * MT;               // output rows per workgroup
+  constexpr int HR = (TH - 1) * S + KS;    // halo rows
+  constexpr int HC = 31 * S + KS;          // halo cols
+  constexpr int PS = 12;                   // floats per staged pixel (8 + 4 pad: conflict-free b128)
+  constexpr int T2 = KS * KS;
+  constexpr int WS = T2 * 8 + 4;           // floats per staged weight row
+  constexpr int NJ = NT * 32;              // couts per workgroup
+  constexpr int PAD = KS / 2;
+  __shared__ __attribute__((aligned(16))) float smem[HR * HC * PS + NJ * WS];
+  float* s_in = smem;
+  float* s_w = smem + HR * HC * PS;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = tid >> 6;
+  const int l32 = lane & 31;
+  const int hf = lane >> 5;
+  const int tiles_x = (a.Wo + 31) >> 5;
+  const int tx = blockIdx.x % tiles_x;
+  const int ty = blockIdx.x / tiles_x;
+  const int slice = blockIdx.y;
+  const int g = blockIdx.z / a.nitems;
+  const int n = blockIdx.z - g * a.nitems;
+
+  const float* in0 = a.in0[g] + (size_t)n * a.in0_item;
+  const float* in1 = IN1 ? a.in1[g] + (size_t)n * a.in1_item : nullptr;
+  const int H = a.H, W = a.W, C0 = a.C0, C1 = a.C1;
+  const int oy0 = ty * TH, ox0 = tx * 32;
+  const int iy0 = oy0 * S - PAD, ix0 = ox0 * S - PAD;
+  const int NC0 = C0 >> 3;
+  const int NC = NC0 + (IN1 ? (C1 >> 3) : 0);
+  const int cout_pad = (a.cout + 31) & ~31;
+  const float* wbase = a.w[g] + (size_t)slice * NJ * T2 * 8;
+  const size_t wchunk = (size_t)cout_pad * T2 * 8;
+  const int H1 = H >> 1, W1 = W >> 1;
+
+  f32x16 acc[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x16{0};
+
+  for (int c = 0; c < NC; ++c) {
+    // ---- stage the input halo of this 8-channel chunk
+    for (int e = tid; e < HR * HC * 2; e += 256) {
+      const int half = e & 1;
+      const int pix = e >> 1;
+      const int r = pix / HC;
+      const int cc = pix - r * HC;
+      const int y = iy0 + r, x = ix0 + cc;
+      f32x4 v = f32x4{0};
+      const bool inside = (y >= 0) & (y < H) & (x >= 0) & (x < W);
+      if (inside) {
+        if (c < NC0) {
+          v = ld4(in0 + ((size_t)y * W + x) * C0 + c * 8 + half * 4);
+        } else if (IN1 == 1) {
+          v = ld4(in1 + ((size_t)y * W + x) * C1 + (c - NC0) * 8 + half * 4);
+        } else if (IN1 == 2) {
+          // upsample_bilinear2d, align_corners=False, scale 2 (PyTorch area_pixel_compute_source_index)
+          const float sy = fmaxf(0.5f * ((float)y + 0.5f) - 0.5f, 0.f);
+          const float sx = fmaxf(0.5f * ((float)x + 0.5f) - 0.5f, 0.f);
+          const int y0 = (int)sy, x0 = (int)sx;
+          const int y1 = y0 + (y0 < H1 - 1 ? 1 : 0);
+          const int x1 = x0 + (x0 < W1 - 1 ? 1 : 0);
+          const float ly1 = sy - (float)y0, lx1 = sx - (float)x0;
+          const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
+          const int co = (c - NC0) * 8 + half * 4;
+          const f32x4 v00 = ld4(in1 + ((size_t)y0 * W1 + x0) * C1 + co);
+          const f32x4 v01 = ld4(in1 + ((size_t)y0 * W1 + x1) * C1 + co);
+          const f32x4 v10 = ld4(in1 + ((size_t)y1 * W1 + x0) * C1 + co);
+          const f32x4 v11 = ld4(in1 + ((size_t)y1 * W1 + x1) * C1 + co);
+          v = (ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11)) * a.in1_scale;
+        }
+      }
+      st4(s_in + pix * PS + half * 4, v);
+    }
+    // ---- stage the weight slice of this chunk: NJ rows x (T2*8) contiguous floats
+    const float* wc = wbase + (size_t)c * wchunk;
+    for (int e = tid; e < NJ * T2 * 2; e += 256) {
+      const int j = e / (T2 * 2);
+      const int q = e - j * (T2 * 2);
+      const f32x4 v = (slice * NJ + j < cout_pad) ? ld4(wc + (size_t)j * T2 * 8 + q * 4) : f32x4{0};
+      st4(s_w + j * WS + q * 4, v);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int tap = 0; tap < T2; ++tap) {
+      const int ky = tap / KS, kx = tap % KS;
+      f32x4 av[MT], bv[NT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int oy = wv * MT + mt;
+        av[mt] = ld4(s_in + ((oy * S + ky) * HC + l32 * S + kx) * PS + hf * 4);
+      }
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) bv[nt] = ld4(s_w + (nt * 32 + l32) * WS + tap * 8 + hf * 4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma32(av[mt][q], bv[nt][q], acc[mt][nt]);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane holds cout l32 of tile nt for pixels x = mfma_row(r, lane)
+  const float* bias = a.bias[g] + slice * NJ;
+  if constexpr (EPI == STIF_EPI_LSTM) {
+    static_assert(NT == 4, "LSTM epilogue needs the i,f,o,g tiles of one hidden channel in one lane");
+    float* hout = a.out[g] + (size_t)n * a.out_item;
+    float* cout_ = a.out2[g] + (size_t)n * a.out2_item;
+    const float* ccur = a.res[g] + (size_t)n * a.res_item;
+    const int hc = slice * 32 + l32;   // hidden channel (weights packed with STIF_PACK_LSTM)
+    const float bi = bias[l32], bff = bias[32 + l32], bo = bias[64 + l32], bg = bias[96 + l32];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int y = oy0 + wv * MT + mt;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int x = ox0 + mfma_row(r, lane);
+        if (y < a.Ho && x < a.Wo) {
+          const size_t p = ((size_t)y * a.Wo + x) * 64 + hc;
+          const float i_ = sigmoidf_(acc[mt][0][r] + bi);
+          const float f_ = sigmoidf_(acc[mt][1][r] + bff);
+          const float o_ = sigmoidf_(acc[mt][2][r] + bo);
+          const float g_ = tanhf(acc[mt][3][r] + bg);
+          const float cn = f_ * ccur[p] + i_ * g_;
+          cout_[p] = cn;
+          hout[p] = o_ * tanhf(cn);
+        }
+      }
+    }
+  } else {
+    float* out = a.out[g] + (size_t)n * a.out_item;
+    const float* res = (EPI == STIF_EPI_RES) ? a.res[g] + (size_t)n * a.res_item : nullptr;
+    const int cstride = a.cout;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int co = slice * NJ + nt * 32 + l32;
+      if (co >= a.cout) continue;
+      const float bv = bias[nt * 32 + l32];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int y = oy0 + wv * MT + mt;
+        if (y >= a.Ho) continue;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int x = ox0 + mfma_row(r, lane);
+          if (x >= a.Wo) continue;
+          const size_t p = ((size_t)y * a.Wo + x) * cstride + co;
+          float v = acc[mt][nt][r] + bv;
+          if (EPI == STIF_EPI_LRELU) v = lrelu01(v);
+          if (EPI == STIF_EPI_RELU) v = fmaxf(v, 0.f);
+          if (EPI == STIF_EPI_RES) v = res[p] + v;
+          if (EPI == STIF_EPI_OFFMASK) {
+            if (co < 216 && (co % 3) == 2) v = sigmoidf_(v);
+          }
+          out[p] = v;
+        }
+      }
+    }
+  }
+}
+
+template <int KS, int S, int MT, int NT, int IN1, int EPI>
+int launch(const stif_conv_args& a, hipStream_t st) {
+  constexpr int TH = 4 * MT;
+  const int tiles = ((a.Wo + 31) / 32) * ((a.Ho + TH - 1) / TH);
+  const int slices = ((a.cout + 31) / 32 + NT - 1) / NT;
+  dim3 grid(tiles, slices, a.ngroups * a.nitems);
+  hipLaunchKernelGGL((k_conv<KS, S, MT, NT, IN1, EPI>), grid, dim3(256), 0, st, a);
+  return stif_check_launch("stif_conv2d_nhwc");
+}
+
+// ---------------------------------------------------------------- conv_first (3 -> 64)
+__global__ __launch_bounds__(256) void k_conv_first(const float* __restrict__ x, const float* __restrict__ w,
+                                                    const float* __restrict__ b, float* __restrict__ out,
+                                                    int n, int h, int wd) {
+  __shared__ float s_w[27 * 64];   // [cin*9+tap][cout]
+  __shared__ float s_b[64];
+  for (int e = threadIdx.x; e < 27 * 64; e += 256) {
+    const int co = e & 63, k = e >> 6;
+    s_w[e] = w[co * 27 + k];
+  }
+  if (threadIdx.x < 64) s_b[threadIdx.x] = b[threadIdx.x];
+  __syncthreads();
+  // thread = (pixel, 16-cout quarter)
+  const long long total = (long long)n * h * wd * 4;
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const int qd = (int)(e & 3);
+    const long long pix = e >> 2;
+    const int xx = (int)(pix % wd);
+    const int yy = (int)((pix / wd) % h);
+    const int img = (int)(pix / ((long long)wd * h));
+    float acc[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+#pragma unroll 1
+    for (int ci = 0; ci < 3; ++ci) {
+      const float* xp = x + ((size_t)img * 3 + ci) * h * wd;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int y = yy + t / 3 - 1, xq = xx + t % 3 - 1;
+        const float v = (y >= 0 && y < h && xq >= 0 && xq < wd) ? xp[(size_t)y * wd + xq] : 0.f;
+        const float* wr = s_w + (ci * 9 + t) * 64 + qd * 16;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[j] = fmaf(v, wr[j], acc[j]);
+      }
+    }
+    float* op = out + pix * 64 + qd * 16;
+#pragma unroll
+    for (int j = 0; j < 16; j += 4) {
+      f32x4 v;
+      v[0] = lrelu01(acc[j] + s_b[qd * 16 + j]);
+      v[1] = lrelu01(acc[j + 1] + s_b[qd * 16 + j + 1]);
+      v[2] = lrelu01(acc[j + 2] + s_b[qd * 16 + j + 2]);
+      v[3] = lrelu01(acc[j + 3] + s_b[qd * 16 + j + 3]);
+      st4(op + j, v);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int stif_conv2d_nhwc(const stif_conv_args* pa, void* stream) {
+  if (!pa) return stif_fail(STIF_E_INVALID, "stif_conv2d_nhwc: null args");
+  const stif_conv_args& a = *pa;
+  hipStream_t st = (hipStream_t)stream;
+  if (a.ngroups < 1 || a.ngroups > STIF_MAX_GROUPS || a.nitems < 1)
+    return stif_fail(STIF_E_INVALID, "stif_conv2d_nhwc: bad ngroups/nitems");
+  if (a.C0 % 8 || a.C0 <= 0 || (a.in1_mode && (a.C1 % 8 || a.C1 <= 0)))
+    return stif_fail(STIF_E_INVALID, "stif_conv2d_nhwc: channel counts must be multiples of 8");
+  const int pad = a.ks / 2;
+  if ((a.ks != 1 && a.ks != 3) || (a.stride != 1 && a.stride != 2) ||
+      a.Ho != (a.H + 2 * pad - a.ks) / a.stride + 1 || a.Wo != (a.W + 2 * pad - a.ks) / a.stride + 1)
+    return stif_fail(STIF_E_INVALID, "stif_conv2d_nhwc: bad ks/stride/output size");
+  if (a.in1_mode == 2 && (a.H % 2 || a.W % 2))
+    return stif_fail(STIF_E_INVALID, "stif_conv2d_nhwc: x2 upsample input needs even H, W");
+  if ((a.epi == STIF_EPI_RES || a.epi == STIF_EPI_LSTM) && !a.res[0])
+    return stif_fail(STIF_E_INVALID, "stif_conv2d_nhwc: epilogue needs res");
+
+  // dispatch on the shapes the STIF graph uses
+  if (a.ks == 3 && a.stride == 1 && a.epi == STIF_EPI_LSTM) {
+    if (a.cout != 256 || a.in1_mode != 1) return stif_fail(STIF_E_INVALID, "LSTM conv must be 128->256");
+    return launch<3, 1, 1, 4, 1, STIF_EPI_LSTM>(a, st);
+  }
+  if (a.ks == 3 && a.stride == 1 && a.epi == STIF_EPI_OFFMASK) {
+    if (a.in1_mode != 0 || a.cout > 224) return stif_fail(STIF_E_INVALID, "offset conv must be 64->216");
+    return launch<3, 1, 1, 7, 0, STIF_EPI_OFFMASK>(a, st);
+  }
+  if (a.ks == 3 && a.stride == 2) {
+    if (a.in1_mode != 0) return stif_fail(STIF_E_INVALID, "strided conv takes one input");
+    switch (a.epi) {
+      case STIF_EPI_LRELU: return launch<3, 2, 1, 2, 0, STIF_EPI_LRELU>(a, st);
+      case STIF_EPI_NONE: return launch<3, 2, 1, 2, 0, STIF_EPI_NONE>(a, st);
+      default: break;
+    }
+    return stif_fail(STIF_E_INVALID, "strided conv: unsupported epilogue");
+  }
+  if (a.ks == 1) {
+    if (a.epi != STIF_EPI_NONE) return stif_fail(STIF_E_INVALID, "1x1 conv: unsupported epilogue");
+    if (a.in1_mode == 0) return launch<1, 1, 2, 2, 0, STIF_EPI_NONE>(a, st);
+    if (a.in1_mode == 1) return launch<1, 1, 2, 2, 1, STIF_EPI_NONE>(a, st);
+    return stif_fail(STIF_E_INVALID, "1x1 conv: unsupported in1 mode");
+  }
+  // 3x3 stride 1
+#define STIF_CONV_CASE(IN1)                                                   \
+  switch (a.epi) {                                                            \
+    case STIF_EPI_NONE: return launch<3, 1, 2, 2, IN1, STIF_EPI_NONE>(a, st); \
+    case STIF_EPI_LRELU: return launch<3, 1, 2, 2, IN1, STIF_EPI_LRELU>(a, st); \
+    case STIF_EPI_RELU: return launch<3, 1, 2, 2, IN1, STIF_EPI_RELU>(a, st); \
+    case STIF_EPI_RES: return launch<3, 1, 2, 2, IN1, STIF_EPI_RES>(a, st);   \
+    default: break;                                                           \
+  }
+  if (a.in1_mode == 0) { STIF_CONV_CASE(0) }
+  else if (a.in1_mode == 1) { STIF_CONV_CASE(1) }
+  else if (a.in1_mode == 2) { STIF_CONV_CASE(2) }
+#undef STIF_CONV_CASE
+  return stif_fail(STIF_E_INVALID, "stif_conv2d_nhwc: unsupported combination");
+}
+
+extern "C" int stif_conv_first(const float* x, const float* w, const float* b, float* out, int n, int h,
+                               int wd, void* stream) {
+  if (!x || !w || !b || !out || n <= 0 || h <= 0 || wd <= 0)
+    return stif_fail(STIF_E_INVALID, "stif_conv_first: bad arguments");
+  const long long total = (long long)n * h * wd * 4;
+  long long blocks = (total + 255) / 256;
+  if (blocks > 65535) blocks = 65535;
+  hipLaunchKernelGGL(k_conv_first, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, w, b, out, n,
+                     h, wd);
+  return stif_check_launch("stif_conv_first");
+}

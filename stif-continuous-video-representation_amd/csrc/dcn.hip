@@ -1,0 +1,264 @@
+// Modulated deformable convolution (DCNv2) for gfx950.
+//
+// 1. k_dcn: the fused STIF path (64 -> 64, 3x3, stride 1, pad 1, 8 deformable groups).
+//    Reference: DCN_sep.forward (DCNv2/dcn_v2.py:127-140) -> dcn_v2_cuda_forward
+//    (src/cuda/dcn_v2_cuda.cu:42-172) = im2col into an HBM columns buffer + batched
+//    SGEMM.  Here each workgroup owns 4 rows x 32 columns of output pixels; for each
+//    deformable group (= 8 input channels = one K chunk) it bilinearly samples the
+//    group's 9 taps straight into an LDS A-tile (semantics of
+//    modulated_deformable_im2col_gpu_kernel / dmcn_im2col_bilinear,
+//    dcn_v2_im2col_cuda.cu:25-54,125-195), stages the group's weight slice, and
+//    contracts with fp32 MFMA.  The columns buffer never exists.
+// 2. stif_dcn_v2_forward: drop-in for `_ext.dcn_v2_forward` (NCHW, any shape): an
+//    im2col kernel into a caller workspace + an fp32-MFMA GEMM with fused bias.
+#include "stif_common.h"
+#include "stif.h"
+#include "abi_util.h"
+
+namespace {
+
+constexpr int OMC = 216;   // offmask channels per pixel: [group][tap][dy, dx, mask]
+
+STIF_DEV f32x4 dcn_sample4(const float* __restrict__ img, int H, int W, float h, float w, int coff) {
+  // dmcn_im2col_bilinear (dcn_v2_im2col_cuda.cu:25-54) on 4 channels of an NHWC 64-ch map.
+  const int h_low = (int)floorf(h);
+  const int w_low = (int)floorf(w);
+  const int h_high = h_low + 1, w_high = w_low + 1;
+  const float lh = h - (float)h_low, lw = w - (float)w_low;
+  const float hh = 1.f - lh, hw = 1.f - lw;
+  f32x4 v1 = f32x4{0}, v2 = f32x4{0}, v3 = f32x4{0}, v4 = f32x4{0};
+  if (h_low >= 0 && w_low >= 0) v1 = ld4(img + ((size_t)h_low * W + w_low) * 64 + coff);
+  if (h_low >= 0 && w_high <= W - 1) v2 = ld4(img + ((size_t)h_low * W + w_high) * 64 + coff);
+  if (h_high <= H - 1 && w_low >= 0) v3 = ld4(img + ((size_t)h_high * W + w_low) * 64 + coff);
+  if (h_high <= H - 1 && w_high <= W - 1) v4 = ld4(img + ((size_t)h_high * W + w_high) * 64 + coff);
+  const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
+  return w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4;
+}
+
+template <int EPI>
+__global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
+  constexpr int NPX = 128;        // 4 rows x 32 cols
+  constexpr int AS = 9 * 8 + 4;   // floats per staged pixel row of the A tile
+  constexpr int WS = 9 * 8 + 4;
+  constexpr int NJ = 64;
+  __shared__ __attribute__((aligned(16))) float smem[NPX * AS + NJ * WS];
+  float* s_a = smem;
+  float* s_w = smem + NPX * AS;
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l32 = lane & 31, hf = lane >> 5;
+  const int H = a.H, W = a.W;
+  const int tiles_x = (W + 31) >> 5;
+  const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+  const int g = blockIdx.z / a.nitems, n = blockIdx.z - g * a.nitems;
+  const float* in = a.in[g] + (size_t)n * a.in_item;
+  const float* om = a.offmask[g] + (size_t)n * a.om_item;
+  const float* wt = a.w[g];
+  const int oy0 = ty * 4, ox0 = tx * 32;
+
+  f32x16 acc0 = f32x16{0}, acc1 = f32x16{0};
+  for (int dg = 0; dg < 8; ++dg) {
+    for (int e = tid; e < NPX * 9 * 2; e += 256) {
+      const int half = e & 1;
+      const int it = e >> 1;
+      const int px = it / 9, tap = it - px * 9;
+      const int oy = oy0 + (px >> 5), ox = ox0 + (px & 31);
+      f32x4 v = f32x4{0};
+      if (oy < H && ox < W) {
+        const float* o = om + ((size_t)oy * W + ox) * OMC + dg * 27 + tap * 3;
+        const float h_im = (float)(oy - 1 + tap / 3) + o[0];
+        const float w_im = (float)(ox - 1 + tap % 3) + o[1];
+        if (h_im > -1.f && w_im > -1.f && h_im < (float)H && w_im < (float)W)
+          v = dcn_sample4(in, H, W, h_im, w_im, dg * 8 + half * 4) * o[2];
+      }
+      st4(s_a + px * AS + tap * 8 + half * 4, v);
+    }
+    const float* wc = wt + (size_t)dg * NJ * 72;
+    for (int e = tid; e < NJ * 18; e += 256) {
+      const int j = e / 18, q = e - j * 18;
+      st4(s_w + j * WS + q * 4, ld4(wc + j * 72 + q * 4));
+    }
+    __syncthreads();
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const f32x4 av = ld4(s_a + (wv * 32 + l32) * AS + tap * 8 + hf * 4);
+      const f32x4 b0 = ld4(s_w + l32 * WS + tap * 8 + hf * 4);
+      const f32x4 b1 = ld4(s_w + (32 + l32) * WS + tap * 8 + hf * 4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc0 = mfma32(av[q], b0[q], acc0);
+        acc1 = mfma32(av[q], b1[q], acc1);
+      }
+    }
+    __syncthreads();
+  }
+  float* out = a.out[g] + (size_t)n * a.out_item;
+  const float* bias = a.bias[g];
+  const int y = oy0 + wv;
+  if (y >= H) return;
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int co = nt * 32 + l32;
+    const float bv = bias[co];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int x = ox0 + mfma_row(r, lane);
+      if (x >= W) continue;
+      float v = (nt ? acc1[r] : acc0[r]) + bv;
+      if (EPI == STIF_EPI_LRELU) v = lrelu01(v);
+      out[((size_t)y * W + x) * 64 + co] = v;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ generic drop-in path
+// columns[b][c*K + k][ho*Wo + wo], exactly the reference's im2col layout (dcn_v2_cuda.cu:90).
+__global__ __launch_bounds__(256) void k_im2col(const float* __restrict__ im, const float* __restrict__ off,
+                                                const float* __restrict__ msk, float* __restrict__ col,
+                                                int B, int C, int H, int W, int Ho, int Wo, int kh, int kw,
+                                                int sh, int sw, int ph, int pw, int dh, int dw, int dg) {
+  const long long n = (long long)B * C * Ho * Wo;
+  const int K = kh * kw;
+  const int cpg = C / dg;
+  for (long long idx = (long long)blockIdx.x * 256 + threadIdx.x; idx < n; idx += (long long)gridDim.x * 256) {
+    const int wo = (int)(idx % Wo);
+    const int ho = (int)((idx / Wo) % Ho);
+    const int c = (int)((idx / ((long long)Wo * Ho)) % C);
+    const int b = (int)(idx / ((long long)Wo * Ho * C));
+    const int g = c / cpg;
+    const int h_in = ho * sh - ph, w_in = wo * sw - pw;
+    const float* img = im + ((size_t)b * C + c) * H * W;
+    const float* o = off + ((size_t)b * dg + g) * 2 * K * Ho * Wo;
+    const float* m = msk + ((size_t)b * dg + g) * K * Ho * Wo;
+    float* cp = col + (((size_t)b * C + c) * K) * Ho * Wo + (size_t)ho * Wo + wo;
+    for (int i = 0; i < kh; ++i)
+      for (int j = 0; j < kw; ++j) {
+        const int k = i * kw + j;
+        const float oh = o[((size_t)2 * k * Ho + ho) * Wo + wo];
+        const float ow = o[((size_t)(2 * k + 1) * Ho + ho) * Wo + wo];
+        const float mk = m[((size_t)k * Ho + ho) * Wo + wo];
+        const float h = (float)(h_in + i * dh) + oh;
+        const float w = (float)(w_in + j * dw) + ow;
+        float val = 0.f;
+        if (h > -1.f && w > -1.f && h < (float)H && w < (float)W) {
+          const int h_low = (int)floorf(h), w_low = (int)floorf(w);
+          const int h_high = h_low + 1, w_high = w_low + 1;
+          const float lh = h - (float)h_low, lw = w - (float)w_low, hh = 1.f - lh, hw = 1.f - lw;
+          const float v1 = (h_low >= 0 && w_low >= 0) ? img[(size_t)h_low * W + w_low] : 0.f;
+          const float v2 = (h_low >= 0 && w_high <= W - 1) ? img[(size_t)h_low * W + w_high] : 0.f;
+          const float v3 = (h_high <= H - 1 && w_low >= 0) ? img[(size_t)h_high * W + w_low] : 0.f;
+          const float v4 = (h_high <= H - 1 && w_high <= W - 1) ? img[(size_t)h_high * W + w_high] : 0.f;
+          val = hh * hw * v1 + hh * lw * v2 + lh * hw * v3 + lh * lw * v4;
+        }
+        cp[(size_t)k * Ho * Wo] = val * mk;
+      }
+  }
+}
+
+// out[b][m][p] = bias[m] + sum_k A[m][k] * Bm[b][k][p]   (fp32 MFMA, 64x64 tile per workgroup)
+__global__ __launch_bounds__(256) void k_gemm_bias(const float* __restrict__ A, const float* __restrict__ Bm,
+                                                   const float* __restrict__ bias, float* __restrict__ out,
+                                                   int M, int K, int N) {
+  constexpr int LS = 12;
+  __shared__ __attribute__((aligned(16))) float sA[64 * LS];
+  __shared__ __attribute__((aligned(16))) float sB[64 * LS];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l32 = lane & 31, hf = lane >> 5;
+  const int m0 = blockIdx.y * 64, p0 = blockIdx.x * 64, b = blockIdx.z;
+  const float* Bb = Bm + (size_t)b * K * N;
+  const int mi = wv >> 1, ni = wv & 1;
+  f32x16 acc = f32x16{0};
+  for (int k0 = 0; k0 < K; k0 += 8) {
+    for (int e = tid; e < 512; e += 256) {
+      const int r = e >> 3, kk = e & 7;   // A: row r, k kk
+      const int m = m0 + r, k = k0 + kk;
+      sA[r * LS + kk] = (m < M && k < K) ? A[(size_t)m * K + k] : 0.f;
+      const int kb = e >> 6, p = e & 63;  // B: k kb, col p
+      const int kq = k0 + kb, pp = p0 + p;
+      sB[p * LS + kb] = (kq < K && pp < N) ? Bb[(size_t)kq * N + pp] : 0.f;
+    }
+    __syncthreads();
+    const f32x4 av = ld4(sA + (mi * 32 + l32) * LS + hf * 4);
+    const f32x4 bv = ld4(sB + (ni * 32 + l32) * LS + hf * 4);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc = mfma32(av[q], bv[q], acc);
+    __syncthreads();
+  }
+  const int p = p0 + ni * 32 + l32;
+  if (p >= N) return;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = m0 + mi * 32 + mfma_row(r, lane);
+    if (m < M) out[((size_t)b * M + m) * N + p] = acc[r] + bias[m];
+  }
+}
+
+}  // namespace
+
+extern "C" int stif_dcn_nhwc(const stif_dcn_args* pa, void* stream) {
+  if (!pa) return stif_fail(STIF_E_INVALID, "stif_dcn_nhwc: null args");
+  const stif_dcn_args& a = *pa;
+  if (a.ngroups < 1 || a.ngroups > STIF_MAX_GROUPS || a.nitems < 1 || a.H < 1 || a.W < 1)
+    return stif_fail(STIF_E_INVALID, "stif_dcn_nhwc: bad sizes");
+  dim3 grid(((a.W + 31) / 32) * ((a.H + 3) / 4), 1, a.ngroups * a.nitems);
+  if (a.epi == STIF_EPI_LRELU)
+    hipLaunchKernelGGL(k_dcn<STIF_EPI_LRELU>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  else if (a.epi == STIF_EPI_NONE)
+    hipLaunchKernelGGL(k_dcn<STIF_EPI_NONE>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  else
+    return stif_fail(STIF_E_INVALID, "stif_dcn_nhwc: epilogue must be NONE or LRELU");
+  return stif_check_launch("stif_dcn_nhwc");
+}
+
+static bool dcn_dims(int H, int W, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw, int* Ho,
+                     int* Wo) {
+  *Ho = (H + 2 * ph - (dh * (kh - 1) + 1)) / sh + 1;
+  *Wo = (W + 2 * pw - (dw * (kw - 1) + 1)) / sw + 1;
+  return *Ho > 0 && *Wo > 0;
+}
+
+extern "C" size_t stif_dcn_v2_workspace_size(int batch, int channels, int height, int width, int channels_out,
+                                             int kernel_h, int kernel_w, int stride_h, int stride_w, int pad_h,
+                                             int pad_w, int dilation_h, int dilation_w, int deformable_group) {
+  (void)channels_out;
+  (void)deformable_group;
+  int Ho, Wo;
+  if (!dcn_dims(height, width, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w, dilation_h, dilation_w, &Ho,
+                &Wo))
+    return 0;
+  return (size_t)batch * channels * kernel_h * kernel_w * Ho * Wo * sizeof(float);
+}
+
+extern "C" int stif_dcn_v2_forward(const float* input, const float* weight, const float* bias, const float* offset,
+                                   const float* mask, float* output, int batch, int channels, int height, int width,
+                                   int channels_out, int kernel_h, int kernel_w, int stride_h, int stride_w,
+                                   int pad_h, int pad_w, int dilation_h, int dilation_w, int deformable_group,
+                                   void* workspace, size_t workspace_bytes, void* stream) {
+  // argument checks mirror dcn_v2_cuda_forward's AT_ASSERTMs (dcn_v2_cuda.cu:60-84)
+  if (!input || !weight || !bias || !offset || !mask || !output)
+    return stif_fail(STIF_E_INVALID, "dcn_v2_forward: null tensor");
+  if (batch < 1 || channels < 1 || channels_out < 1 || kernel_h < 1 || kernel_w < 1 || stride_h < 1 ||
+      stride_w < 1 || dilation_h < 1 || dilation_w < 1 || deformable_group < 1 || channels % deformable_group)
+    return stif_fail(STIF_E_INVALID, "dcn_v2_forward: invalid shape arguments");
+  int Ho, Wo;
+  if (!dcn_dims(height, width, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w, dilation_h, dilation_w, &Ho,
+                &Wo))
+    return stif_fail(STIF_E_INVALID, "dcn_v2_forward: empty output");
+  const size_t need = stif_dcn_v2_workspace_size(batch, channels, height, width, channels_out, kernel_h, kernel_w,
+                                                 stride_h, stride_w, pad_h, pad_w, dilation_h, dilation_w,
+                                                 deformable_group);
+  if (!workspace || workspace_bytes < need)
+    return stif_fail(STIF_E_WORKSPACE, "dcn_v2_forward: workspace too small");
+  float* cols = (float*)workspace;
+  hipStream_t st = (hipStream_t)stream;
+  const long long n = (long long)batch * channels * Ho * Wo;
+  long long blocks = (n + 255) / 256;
+  if (blocks > 1 << 20) blocks = 1 << 20;
+  hipLaunchKernelGGL(k_im2col, dim3((unsigned)blocks), dim3(256), 0, st, input, offset, mask, cols, batch, channels,
+                     height, width, Ho, Wo, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w, dilation_h,
+                     dilation_w, deformable_group);
+  int rc = stif_check_launch("dcn_v2_forward/im2col");
+  if (rc) return rc;
+  const int K = channels * kernel_h * kernel_w, N = Ho * Wo;
+  dim3 grid((N + 63) / 64, (channels_out + 63) / 64, batch);
+  hipLaunchKernelGGL(k_gemm_bias, grid, dim3(256), 0, st, weight, cols, bias, output, channels_out, K, N);
+  return stif_check_launch("dcn_v2_forward/gemm");
+}

@@ -1,0 +1,41 @@
+// Packed layout of the implicit-decoder MLP weights (shared by pack.cpp and decoder.hip).
+//
+// The decoder runs every SIREN layer as D^T = W . X^T on v_mfma_f32_32x32x2_f32 with
+// the HR pixel on the lane (j = lane & 31) and features in registers: a 32-feature
+// tile lives in 16 accumulator registers, register r of lane half h holding feature
+// F(r, h) = (r & 3) + 8 * (r >> 2) + 4 * h.  That register tile is directly the B
+// operand of the next layer if the next layer's weights are read in the same K
+// order, so one weight tile (32 out x 32 in) is stored as
+//   [v = 0..3][lane = 0..63][e = 0..3]  ->  W[32*ot + (lane & 31)][32*kt + F(4v + e, lane >> 5)]
+// (1024 floats; each wave-instruction of a float4 load reads 1 KiB contiguously).
+#pragma once
+
+namespace stif_dec {
+
+constexpr int T = 1024;  // floats per packed 32x32 weight tile
+
+// feat_imnet (201 -> 64 -> 64 -> 256 -> 64); layer 0's 198 LR inputs live in the projection P1
+constexpr int F_WRY = 0, F_WRX = 64, F_WT = 128;
+constexpr int F_W1 = 192, F_B1 = F_W1 + 4 * T;
+constexpr int F_W2 = F_B1 + 64, F_B2 = F_W2 + 16 * T;
+constexpr int F_W3 = F_B2 + 256, F_B3 = F_W3 + 16 * T;
+constexpr int F_END = F_B3 + 64;
+// flow_imnet (263 -> 64 -> 64 -> 256 -> 4); layer 0: HRfeat part packed, feat/inp part in P2
+constexpr int L_W0 = F_END, L_WT = L_W0 + 4 * T, L_B0 = L_WT + 64;
+constexpr int L_W1 = L_B0 + 64, L_B1 = L_W1 + 4 * T;
+constexpr int L_W2 = L_B1 + 64, L_B2 = L_W2 + 16 * T;
+constexpr int L_W3 = L_B2 + 256, L_B3 = L_W3 + 8 * T;
+constexpr int L_END = L_B3 + 32;
+// encode_imnet (525 -> 64 -> 64 -> 256 -> 256 -> 3); layer 0: q_feat1|q_feat2 packed, rest in P3/P4
+constexpr int E_W0 = L_END, E_WT = E_W0 + 8 * T, E_B0 = E_WT + 64;
+constexpr int E_W1 = E_B0 + 64, E_B1 = E_W1 + 4 * T;
+constexpr int E_W2 = E_B1 + 64, E_B2 = E_W2 + 16 * T;
+constexpr int E_W3 = E_B2 + 256, E_B3 = E_W3 + 64 * T;
+constexpr int E_W4 = E_B3 + 256, E_B4 = E_W4 + 8 * T;
+constexpr int E_END = E_B4 + 32;
+
+constexpr int MLP_FLOATS = E_END;
+constexpr int PROJ_C = 256;   // LR projection channels: P1 | P2 | P3 | P4
+constexpr int SRC_C = 200;    // LR source channels: feat t0|t1|t2 (192) + rgb0 rgb1 (6) + 2 zero
+
+}  // namespace stif_dec

@@ -1,0 +1,364 @@
+// Implicit SIREN decoder of LunaTokis.decoding (Sakuya_arch_test.py:364-459) for gfx950.
+//
+// The reference materialises, per query time t, ~2,300 floats per HR pixel of
+// grid_sample gathers and torch.cat results and runs three nn.Linear stacks over
+// them.  Here the work is split into:
+//   (0) an LR projection (stif_conv2d_nhwc, 1x1, 200 -> 256 channels): every linear
+//       input block that is gathered from the LR maps (feat 192 + inp 6) is projected
+//       once per LR pixel -- nearest/bilinear sampling commutes with a linear map,
+//       so the per-HR-pixel work gathers 64-wide projections instead of 198-wide
+//       inputs (P1 nearest, P2 bilinear at the HR centre, P3/P4 bilinear at the
+//       warped grids);
+//   (1) k_dec1: per HR pixel feat_imnet -> HRfeat (64) and flow_imnet -> flow (4);
+//   (2) k_dec2: per HR pixel warpgrid (warplayer.py:25-39) + bilinear HRfeat at both
+//       warped grids + encode_imnet -> RGB.
+// Each wave owns 32 HR pixels (one per lane, both lane halves hold the same pixel);
+// every SIREN layer is a chain of v_mfma_f32_32x32x2_f32 with features in the
+// accumulator registers (layout in dec_layout.h), sin(30 z) applied in registers.
+#include "dec_layout.h"
+#include "stif_common.h"
+#include "stif.h"
+#include "abi_util.h"
+
+namespace {
+
+using namespace stif_dec;
+
+// acc += W_tile(ot) . X  over KT K-tiles; wt points at tile (ot, kt=0); x = KT register tiles
+template <int KT>
+STIF_DEV void mlp_acc(f32x16& acc, const float* __restrict__ wt, const f32x16* x, int lane) {
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) {
+    const float* b = wt + kt * T + lane * 4;
+    const f32x4 w0 = ld4(b), w1 = ld4(b + 256), w2 = ld4(b + 512), w3 = ld4(b + 768);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc = mfma32(w0[e], x[kt][e], acc);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc = mfma32(w1[e], x[kt][4 + e], acc);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc = mfma32(w2[e], x[kt][8 + e], acc);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc = mfma32(w3[e], x[kt][12 + e], acc);
+  }
+}
+
+// SineLayer: sin(30 * (z + b))  (SIREN.py:44-45, omega_0 = 30)
+STIF_DEV f32x16 bias_sin(f32x16 z, const float* __restrict__ b, int hf) {
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const f32x4 bb = ld4(b + 8 * v + 4 * hf);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) z[4 * v + e] = stif_sin(30.0f * (z[4 * v + e] + bb[e]));
+  }
+  return z;
+}
+
+STIF_DEV f32x16 bias_add(f32x16 z, const float* __restrict__ b, int hf) {
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const f32x4 bb = ld4(b + 8 * v + 4 * hf);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) z[4 * v + e] += bb[e];
+  }
+  return z;
+}
+
+struct Bilin {  // grid_sample bilinear corners (align_corners=False, zeros padding)
+  int o00, o01, o10, o11;      // element offsets (pixel index)
+  float w00, w01, w10, w11;    // weights, 0 for out-of-range corners
+};
+
+// ATen grid_sampler_2d bilinear: ix = ((x + 1) * W - 1) / 2, corner weights
+// nw = (ix_se - ix) * (iy_se - iy), ...; corners outside the map contribute 0.
+STIF_DEV Bilin bilin(float gx, float gy, int Wd, int Hd) {
+  const float ix = ((gx + 1.f) * (float)Wd - 1.f) / 2.f;
+  const float iy = ((gy + 1.f) * (float)Hd - 1.f) / 2.f;
+  const float fx0 = floorf(ix), fy0 = floorf(iy);
+  const int x0 = (int)fx0, y0 = (int)fy0, x1 = x0 + 1, y1 = y0 + 1;
+  const float wx1 = ix - fx0, wx0 = (fx0 + 1.f) - ix;
+  const float wy1 = iy - fy0, wy0 = (fy0 + 1.f) - iy;
+  const bool vx0 = x0 >= 0 && x0 < Wd, vx1 = x1 >= 0 && x1 < Wd;
+  const bool vy0 = y0 >= 0 && y0 < Hd, vy1 = y1 >= 0 && y1 < Hd;
+  const int cx0 = min(max(x0, 0), Wd - 1), cx1 = min(max(x1, 0), Wd - 1);
+  const int cy0 = min(max(y0, 0), Hd - 1), cy1 = min(max(y1, 0), Hd - 1);
+  Bilin b;
+  b.o00 = cy0 * Wd + cx0; b.o01 = cy0 * Wd + cx1; b.o10 = cy1 * Wd + cx0; b.o11 = cy1 * Wd + cx1;
+  b.w00 = (vx0 && vy0) ? wx0 * wy0 : 0.f;
+  b.w01 = (vx1 && vy0) ? wx1 * wy0 : 0.f;
+  b.w10 = (vx0 && vy1) ? wx0 * wy1 : 0.f;
+  b.w11 = (vx1 && vy1) ? wx1 * wy1 : 0.f;
+  return b;
+}
+
+// bilinear sample of channel block [c0, c0+64) of an NHWC map with `stride` channels,
+// into two register tiles (features F(r, hf) of each 32-block)
+STIF_DEV void gather64(f32x16* dst, const float* __restrict__ base, int stride, int c0, const Bilin& b, int hf) {
+#pragma unroll
+  for (int ot = 0; ot < 2; ++ot)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int c = c0 + ot * 32 + 8 * v + 4 * hf;
+      const f32x4 s = b.w00 * ld4(base + (size_t)b.o00 * stride + c) + b.w01 * ld4(base + (size_t)b.o01 * stride + c) +
+                      b.w10 * ld4(base + (size_t)b.o10 * stride + c) + b.w11 * ld4(base + (size_t)b.o11 * stride + c);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dst[ot][4 * v + e] = s[e];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_dec1(const float* __restrict__ proj, const float* __restrict__ mlp,
+                                              stif_dec_tables tb, const float* __restrict__ tq,
+                                              float* __restrict__ hrfeat, float* __restrict__ flow, int n, int h,
+                                              int w, int HH, int WW) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, hf = lane >> 5;
+  const long long total = (long long)n * HH * WW;
+  const long long p = ((long long)blockIdx.x * 4 + wv) * 32 + (lane & 31);
+  const bool valid = p < total;
+  const long long pc = valid ? p : total - 1;
+  const int item = (int)(pc / ((long long)HH * WW));
+  const int rem = (int)(pc - (long long)item * HH * WW);
+  const int py = rem / WW, px = rem - py * WW;
+  const float t = tq[item];
+  const float* P = proj + (size_t)item * h * w * PROJ_C;
+
+  // ---- feat_imnet layer 0: z = P1[nearest] + w_rel . rel + w_t * t  (bias folded into P1)
+  f32x16 x0[2];
+  {
+    const float ry = tb.rel_y[py], rx = tb.rel_x[px];
+    const float* p1 = P + ((size_t)tb.near_y[py] * w + tb.near_x[px]) * PROJ_C;
+#pragma unroll
+    for (int ot = 0; ot < 2; ++ot)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int f = ot * 32 + 8 * v + 4 * hf;
+        const f32x4 z = ld4(p1 + f) + ld4(mlp + F_WRY + f) * ry + ld4(mlp + F_WRX + f) * rx + ld4(mlp + F_WT + f) * t;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x0[ot][4 * v + e] = stif_sin(30.0f * z[e]);
+      }
+  }
+  // ---- layer 1: 64 -> 64
+  f32x16 x1[2];
+#pragma unroll
+  for (int ot = 0; ot < 2; ++ot) {
+    f32x16 acc = f32x16{0};
+    mlp_acc<2>(acc, mlp + F_W1 + ot * 2 * T, x0, lane);
+    x1[ot] = bias_sin(acc, mlp + F_B1 + ot * 32, hf);
+  }
+  // ---- layer 2 (64 -> 256, sine) streamed into layer 3 (256 -> 64, linear)
+  f32x16 hr[2] = {f32x16{0}, f32x16{0}};
+#pragma unroll 1
+  for (int kt = 0; kt < 8; ++kt) {
+    f32x16 acc = f32x16{0};
+    mlp_acc<2>(acc, mlp + F_W2 + kt * 2 * T, x1, lane);
+    f32x16 h2[1] = {bias_sin(acc, mlp + F_B2 + kt * 32, hf)};
+#pragma unroll
+    for (int ot = 0; ot < 2; ++ot) mlp_acc<1>(hr[ot], mlp + F_W3 + (ot * 8 + kt) * T, h2, lane);
+  }
+#pragma unroll
+  for (int ot = 0; ot < 2; ++ot) hr[ot] = bias_add(hr[ot], mlp + F_B3 + ot * 32, hf);
+  if (valid) {
+    float* o = hrfeat + (size_t)pc * 64;
+#pragma unroll
+    for (int ot = 0; ot < 2; ++ot)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        f32x4 s;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s[e] = hr[ot][4 * v + e];
+        st4(o + ot * 32 + 8 * v + 4 * hf, s);
+      }
+  }
+
+  // ---- flow_imnet layer 0: W[:, :64] . HRfeat + bilinear(P2 at the HR centre) + w_t * t + b
+  f32x16 z[2];
+  {
+    Bilin b;
+    const int y0 = tb.by0[py], y1 = tb.by1[py], x0_ = tb.bx0[px], x1_ = tb.bx1[px];
+    const float wy0 = tb.wy0[py], wy1 = tb.wy1[py], wx0 = tb.wx0[px], wx1 = tb.wx1[px];
+    b.o00 = y0 * w + x0_; b.o01 = y0 * w + x1_; b.o10 = y1 * w + x0_; b.o11 = y1 * w + x1_;
+    b.w00 = wx0 * wy0; b.w01 = wx1 * wy0; b.w10 = wx0 * wy1; b.w11 = wx1 * wy1;
+    gather64(z, P, PROJ_C, 64, b, hf);
+#pragma unroll
+    for (int ot = 0; ot < 2; ++ot)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int f = ot * 32 + 8 * v + 4 * hf;
+        const f32x4 wt = ld4(mlp + L_WT + f), bb = ld4(mlp + L_B0 + f);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) z[ot][4 * v + e] += wt[e] * t + bb[e];
+      }
+  }
+#pragma unroll
+  for (int ot = 0; ot < 2; ++ot) {
+    mlp_acc<2>(z[ot], mlp + L_W0 + ot * 2 * T, hr, lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) z[ot][r] = stif_sin(30.0f * z[ot][r]);
+  }
+#pragma unroll
+  for (int ot = 0; ot < 2; ++ot) {
+    f32x16 acc = f32x16{0};
+    mlp_acc<2>(acc, mlp + L_W1 + ot * 2 * T, z, lane);
+    x1[ot] = bias_sin(acc, mlp + L_B1 + ot * 32, hf);
+  }
+  f32x16 fl[1] = {f32x16{0}};
+#pragma unroll 1
+  for (int kt = 0; kt < 8; ++kt) {
+    f32x16 acc = f32x16{0};
+    mlp_acc<2>(acc, mlp + L_W2 + kt * 2 * T, x1, lane);
+    f32x16 h2[1] = {bias_sin(acc, mlp + L_B2 + kt * 32, hf)};
+    mlp_acc<1>(fl[0], mlp + L_W3 + kt * T, h2, lane);
+  }
+  if (valid && hf == 0) {
+    const f32x4 bb = ld4(mlp + L_B3);
+    f32x4 s;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s[e] = fl[0][e] + bb[e];
+    st4(flow + (size_t)pc * 4, s);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_dec2(const float* __restrict__ proj, const float* __restrict__ mlp,
+                                              const float* __restrict__ hrfeat, const float* __restrict__ flow,
+                                              stif_dec_tables tb, const float* __restrict__ tq,
+                                              float* __restrict__ out, int n, int h, int w, int HH, int WW) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, hf = lane >> 5;
+  const long long total = (long long)n * HH * WW;
+  const long long p = ((long long)blockIdx.x * 4 + wv) * 32 + (lane & 31);
+  const bool valid = p < total;
+  const long long pc = valid ? p : total - 1;
+  const int item = (int)(pc / ((long long)HH * WW));
+  const int rem = (int)(pc - (long long)item * HH * WW);
+  const int py = rem / WW, px = rem - py * WW;
+  const float t = tq[item];
+  const float* P = proj + (size_t)item * h * w * PROJ_C;
+  const float* HRF = hrfeat + (size_t)item * HH * WW * 64;
+
+  // warpgrid (warplayer.py:25-39): linspace grid + flow / ((n - 1) / 2), then the decoder's
+  // clamp to (-1 + 1e-6, 1 - 1e-6) (Sakuya_arch_test.py:428,441)
+  const f32x4 fv = ld4(flow + (size_t)pc * 4);
+  const float lo = -1.f + 1e-6f, hi = 1.f - 1e-6f;
+  const float dx = ((float)WW - 1.f) / 2.f, dy = ((float)HH - 1.f) / 2.f;
+  const float bx = tb.lin_x[px], by = tb.lin_y[py];
+  const float g1x = fminf(fmaxf(bx + fv[0] / dx, lo), hi), g1y = fminf(fmaxf(by + fv[1] / dy, lo), hi);
+  const float g2x = fminf(fmaxf(bx + fv[2] / dx, lo), hi), g2y = fminf(fmaxf(by + fv[3] / dy, lo), hi);
+
+  // ---- encode_imnet layer 0: W[:, :128] . [q_feat1 | q_feat2] + P3(grid1) + P4(grid2) + w_t t + b
+  f32x16 q[4];
+  gather64(q, HRF, 64, 0, bilin(g1x, g1y, WW, HH), hf);
+  gather64(q + 2, HRF, 64, 0, bilin(g2x, g2y, WW, HH), hf);
+  f32x16 z[2], z2[2];
+  gather64(z, P, PROJ_C, 128, bilin(g1x, g1y, w, h), hf);
+  gather64(z2, P, PROJ_C, 192, bilin(g2x, g2y, w, h), hf);
+#pragma unroll
+  for (int ot = 0; ot < 2; ++ot)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int f = ot * 32 + 8 * v + 4 * hf;
+      const f32x4 wt = ld4(mlp + E_WT + f), bb = ld4(mlp + E_B0 + f);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) z[ot][4 * v + e] += z2[ot][4 * v + e] + wt[e] * t + bb[e];
+    }
+#pragma unroll
+  for (int ot = 0; ot < 2; ++ot) {
+    mlp_acc<4>(z[ot], mlp + E_W0 + ot * 4 * T, q, lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) z[ot][r] = stif_sin(30.0f * z[ot][r]);
+  }
+  f32x16 x1[2];
+#pragma unroll
+  for (int ot = 0; ot < 2; ++ot) {
+    f32x16 acc = f32x16{0};
+    mlp_acc<2>(acc, mlp + E_W1 + ot * 2 * T, z, lane);
+    x1[ot] = bias_sin(acc, mlp + E_B1 + ot * 32, hf);
+  }
+  // layer 2 (64 -> 256, sine) streamed into layer 3 (256 -> 256) accumulators
+  f32x16 a3[8];
+#pragma unroll
+  for (int ot = 0; ot < 8; ++ot) a3[ot] = f32x16{0};
+#pragma unroll 1
+  for (int kt = 0; kt < 8; ++kt) {
+    f32x16 acc = f32x16{0};
+    mlp_acc<2>(acc, mlp + E_W2 + kt * 2 * T, x1, lane);
+    f32x16 h2[1] = {bias_sin(acc, mlp + E_B2 + kt * 32, hf)};
+#pragma unroll
+    for (int ot = 0; ot < 8; ++ot) mlp_acc<1>(a3[ot], mlp + E_W3 + (ot * 8 + kt) * T, h2, lane);
+  }
+  // layer 3 sine streamed into layer 4 (256 -> 3, linear)
+  f32x16 o4[1] = {f32x16{0}};
+#pragma unroll
+  for (int kt = 0; kt < 8; ++kt) {
+    f32x16 h3[1] = {bias_sin(a3[kt], mlp + E_B3 + kt * 32, hf)};
+    mlp_acc<1>(o4[0], mlp + E_W4 + kt * T, h3, lane);
+  }
+  if (valid && hf == 0) {
+    const size_t plane = (size_t)HH * WW;
+    float* o = out + (size_t)item * 3 * plane + (size_t)py * WW + px;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) o[c * plane] = o4[0][c] + mlp[E_B4 + c];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_pack_lr(const float* __restrict__ f0, const float* __restrict__ f1,
+                                                 const float* __restrict__ f2, const float* __restrict__ x,
+                                                 float* __restrict__ out, int n, int h, int w) {
+  const long long npix = (long long)n * h * w;
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < npix * 50; e += (long long)gridDim.x * 256) {
+    const long long pix = e / 50;
+    const int q = (int)(e - pix * 50);
+    f32x4 v;
+    if (q < 48) {
+      const float* src = q < 16 ? f0 : (q < 32 ? f1 : f2);
+      v = ld4(src + pix * 64 + (q & 15) * 4);
+    } else {
+      const int item = (int)(pix / ((long long)h * w));
+      const long long yx = pix - (long long)item * h * w;
+      const float* xi = x + (size_t)item * 6 * h * w + yx;   // [2][3][h][w] of this item
+      const size_t pl = (size_t)h * w;
+      if (q == 48) { v[0] = xi[0]; v[1] = xi[pl]; v[2] = xi[2 * pl]; v[3] = xi[3 * pl]; }
+      else { v[0] = xi[4 * pl]; v[1] = xi[5 * pl]; v[2] = 0.f; v[3] = 0.f; }
+    }
+    st4(out + pix * SRC_C + q * 4, v);
+  }
+}
+
+bool tables_ok(const stif_dec_tables* t) {
+  return t && t->near_y && t->rel_y && t->by0 && t->by1 && t->wy0 && t->wy1 && t->lin_y && t->near_x &&
+         t->rel_x && t->bx0 && t->bx1 && t->wx0 && t->wx1 && t->lin_x;
+}
+
+}  // namespace
+
+extern "C" int stif_dec_pack_lr(const float* f0, const float* f1, const float* f2, const float* x, float* out,
+                                int n, int h, int w, void* stream) {
+  if (!f0 || !f1 || !f2 || !x || !out || n < 1 || h < 1 || w < 1)
+    return stif_fail(STIF_E_INVALID, "stif_dec_pack_lr: bad arguments");
+  const long long work = (long long)n * h * w * 50;
+  long long blocks = (work + 255) / 256;
+  if (blocks > 1 << 16) blocks = 1 << 16;
+  hipLaunchKernelGGL(k_pack_lr, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, f0, f1, f2, x, out, n, h,
+                     w);
+  return stif_check_launch("stif_dec_pack_lr");
+}
+
+extern "C" int stif_dec_stage1(const float* proj, const float* mlp, const stif_dec_tables* tab, const float* t,
+                               float* hrfeat, float* flow, int n, int h, int w, int HH, int WW, void* stream) {
+  if (!proj || !mlp || !tables_ok(tab) || !t || !hrfeat || !flow || n < 1 || h < 1 || w < 1 || HH < 2 || WW < 2)
+    return stif_fail(STIF_E_INVALID, "stif_dec_stage1: bad arguments");
+  const long long total = (long long)n * HH * WW;
+  const long long blocks = (total + 127) / 128;
+  hipLaunchKernelGGL(k_dec1, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, proj, mlp, *tab, t, hrfeat,
+                     flow, n, h, w, HH, WW);
+  return stif_check_launch("stif_dec_stage1");
+}
+
+extern "C" int stif_dec_stage2(const float* proj, const float* mlp, const float* hrfeat, const float* flow,
+                               const stif_dec_tables* tab, const float* t, float* out, int n, int h, int w, int HH,
+                               int WW, void* stream) {
+  if (!proj || !mlp || !hrfeat || !flow || !tables_ok(tab) || !t || !out || n < 1 || h < 1 || w < 1 || HH < 2 ||
+      WW < 2)
+    return stif_fail(STIF_E_INVALID, "stif_dec_stage2: bad arguments");
+  const long long total = (long long)n * HH * WW;
+  const long long blocks = (total + 127) / 128;
+  hipLaunchKernelGGL(k_dec2, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, proj, mlp, hrfeat, flow,
+                     *tab, t, out, n, h, w, HH, WW);
+  return stif_check_launch("stif_dec_stage2");
+}

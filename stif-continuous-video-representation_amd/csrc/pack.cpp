@@ -1,0 +1,169 @@
+// Host-side (CPU) weight packing for the gfx950 kernels.  Pure C++, no GPU needed;
+// runs once per load_state_dict (reference weight layouts: nn.Conv2d [cout][cin][k][k],
+// nn.Linear [out][in], as in the 442-key LunaTokis state dict).
+#include <string.h>
+
+#include <vector>
+
+#include "dec_layout.h"
+#include "stif.h"
+
+extern int stif_fail(int code, const char* msg);
+
+namespace {
+
+int round32(int x) { return (x + 31) & ~31; }
+
+// source row of packed output channel j
+int src_row(int j, int cout, int mode) {
+  if (j >= cout) return -1;
+  if (mode == STIF_PACK_OFFMASK) {
+    // packed [group][tap][dy, dx, mask]  <-  reference channels: offset = cat(o1, o2) = ch 0..143 with
+    // (group g, tap k) at g*18 + 2k (+1 for w); mask = ch 144 + g*9 + k (dcn_v2.py:134-138,
+    // dcn_v2_im2col_cuda.cu:160-167)
+    const int g = j / 27, k = (j % 27) / 3, e = j % 3;
+    if (e == 0) return g * 18 + 2 * k;
+    if (e == 1) return g * 18 + 2 * k + 1;
+    return 144 + g * 9 + k;
+  }
+  if (mode == STIF_PACK_LSTM) {
+    // packed slice s (128 outputs) = gates i, f, o, g of hidden channels 32s..32s+31 (convlstm.py:49)
+    const int s = j / 128, gate = (j % 128) / 32, jj = j % 32;
+    return gate * 64 + s * 32 + jj;
+  }
+  return j;
+}
+
+// F(q, h): feature held by MFMA accumulator register q of lane half h (see dec_layout.h)
+inline int feat_of(int q, int h) { return (q & 3) + 8 * (q >> 2) + 4 * h; }
+
+// pack W[rows x cols] (row-major, leading dim ld, sub-block starting at (r0, c0), n_out x k_in)
+void pack_tiles(float* dst, const float* W, int ld, int r0, int c0, int n_out, int k_in) {
+  const int OT = (n_out + 31) / 32, KT = (k_in + 31) / 32;
+  for (int ot = 0; ot < OT; ++ot)
+    for (int kt = 0; kt < KT; ++kt)
+      for (int v = 0; v < 4; ++v)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int e = 0; e < 4; ++e) {
+            const int q = 4 * v + e;
+            const int row = ot * 32 + (lane & 31);
+            const int col = kt * 32 + feat_of(q, lane >> 5);
+            const float val = (row < n_out && col < k_in) ? W[(size_t)(r0 + row) * ld + c0 + col] : 0.f;
+            dst[((((size_t)ot * KT + kt) * 4 + v) * 64 + lane) * 4 + e] = val;
+          }
+}
+
+void copy_vec(float* dst, const float* src, int n, int npad) {
+  for (int i = 0; i < npad; ++i) dst[i] = i < n ? src[i] : 0.f;
+}
+
+void column(float* dst, const float* W, int ld, int rows, int col) {
+  for (int i = 0; i < rows; ++i) dst[i] = W[(size_t)i * ld + col];
+}
+
+}  // namespace
+
+extern "C" size_t stif_conv_weight_floats(int cout, int cin, int ks) {
+  return (size_t)round32(cout) * cin * ks * ks;
+}
+
+extern "C" size_t stif_conv_bias_floats(int cout) { return (size_t)round32(cout); }
+
+extern "C" int stif_pack_conv_weight(const float* w, const float* b, int cout, int cin, int ks, int mode,
+                                     float* w_dst, float* b_dst) {
+  if (!w || !w_dst || cout <= 0 || cin <= 0 || cin % 8 || (ks != 1 && ks != 3))
+    return stif_fail(STIF_E_INVALID, "stif_pack_conv_weight: bad arguments");
+  if (mode == STIF_PACK_OFFMASK && cout != 216) return stif_fail(STIF_E_INVALID, "offmask pack needs cout=216");
+  if (mode == STIF_PACK_LSTM && cout != 256) return stif_fail(STIF_E_INVALID, "lstm pack needs cout=256");
+  const int cp = round32(cout), T2 = ks * ks, NC = cin / 8;
+  for (int c = 0; c < NC; ++c)
+    for (int j = 0; j < cp; ++j) {
+      const int sr = src_row(j, cout, mode);
+      for (int t = 0; t < T2; ++t)
+        for (int ci = 0; ci < 8; ++ci)
+          w_dst[(((size_t)c * cp + j) * T2 + t) * 8 + ci] =
+              sr < 0 ? 0.f : w[((size_t)sr * cin + c * 8 + ci) * T2 + t];
+    }
+  if (b_dst)
+    for (int j = 0; j < cp; ++j) {
+      const int sr = src_row(j, cout, mode);
+      b_dst[j] = (sr < 0 || !b) ? 0.f : b[sr];
+    }
+  return STIF_OK;
+}
+
+extern "C" size_t stif_dec_proj_floats(void) { return stif_conv_weight_floats(256, stif_dec::SRC_C, 1); }
+
+extern "C" int stif_pack_dec_proj(const float* feat_w0, const float* feat_b0, const float* flow_w0,
+                                  const float* enc_w0, float* w_dst, float* b_dst) {
+  // P1 = feat_imnet.net.0 on [q_feat(192) | q_inp(6)] + bias        (Sakuya_arch_test.py:399)
+  // P2 = flow_imnet.net.0 on [q_feat0(192) | q_inp(6)]             (:418, input cols 64..261)
+  // P3 = encode_imnet.net.0 on [q_feat3(192) | q_img1(6)]          (:455, cols 128..319, 512..517)
+  // P4 = encode_imnet.net.0 on [q_feat4(192) | q_img2(6)]          (cols 320..511, 518..523)
+  if (!feat_w0 || !feat_b0 || !flow_w0 || !enc_w0 || !w_dst || !b_dst)
+    return stif_fail(STIF_E_INVALID, "stif_pack_dec_proj: null");
+  const int C = stif_dec::SRC_C;
+  std::vector<float> W((size_t)256 * C, 0.f), B(256, 0.f);
+  for (int o = 0; o < 64; ++o) {
+    for (int c = 0; c < 198; ++c) {
+      W[(size_t)o * C + c] = feat_w0[(size_t)o * 201 + c];
+      W[(size_t)(64 + o) * C + c] = flow_w0[(size_t)o * 263 + 64 + c];
+    }
+    for (int c = 0; c < 192; ++c) {
+      W[(size_t)(128 + o) * C + c] = enc_w0[(size_t)o * 525 + 128 + c];
+      W[(size_t)(192 + o) * C + c] = enc_w0[(size_t)o * 525 + 320 + c];
+    }
+    for (int c = 0; c < 6; ++c) {
+      W[(size_t)(128 + o) * C + 192 + c] = enc_w0[(size_t)o * 525 + 512 + c];
+      W[(size_t)(192 + o) * C + 192 + c] = enc_w0[(size_t)o * 525 + 518 + c];
+    }
+    B[o] = feat_b0[o];
+  }
+  return stif_pack_conv_weight(W.data(), B.data(), 256, C, 1, STIF_PACK_PLAIN, w_dst, b_dst);
+}
+
+extern "C" size_t stif_dec_mlp_floats(void) { return stif_dec::MLP_FLOATS; }
+
+extern "C" int stif_pack_dec_mlp(const float* const* f, const float* const* l, const float* const* e,
+                                 float* d) {
+  using namespace stif_dec;
+  if (!f || !l || !e || !d) return stif_fail(STIF_E_INVALID, "stif_pack_dec_mlp: null");
+  for (int i = 0; i < 8; ++i)
+    if (!f[i] || !l[i]) return stif_fail(STIF_E_INVALID, "stif_pack_dec_mlp: null layer");
+  for (int i = 0; i < 10; ++i)
+    if (!e[i]) return stif_fail(STIF_E_INVALID, "stif_pack_dec_mlp: null layer");
+  memset(d, 0, sizeof(float) * MLP_FLOATS);
+  // feat_imnet: f = {w0[64x201], b0, w1[64x64], b1, w2[256x64], b2, w3[64x256], b3}
+  column(d + F_WRY, f[0], 201, 64, 198);
+  column(d + F_WRX, f[0], 201, 64, 199);
+  column(d + F_WT, f[0], 201, 64, 200);
+  pack_tiles(d + F_W1, f[2], 64, 0, 0, 64, 64);
+  copy_vec(d + F_B1, f[3], 64, 64);
+  pack_tiles(d + F_W2, f[4], 64, 0, 0, 256, 64);
+  copy_vec(d + F_B2, f[5], 256, 256);
+  pack_tiles(d + F_W3, f[6], 256, 0, 0, 64, 256);
+  copy_vec(d + F_B3, f[7], 64, 64);
+  // flow_imnet: l = {w0[64x263], b0, w1[64x64], b1, w2[256x64], b2, w3[4x256], b3}
+  pack_tiles(d + L_W0, l[0], 263, 0, 0, 64, 64);
+  column(d + L_WT, l[0], 263, 64, 262);
+  copy_vec(d + L_B0, l[1], 64, 64);
+  pack_tiles(d + L_W1, l[2], 64, 0, 0, 64, 64);
+  copy_vec(d + L_B1, l[3], 64, 64);
+  pack_tiles(d + L_W2, l[4], 64, 0, 0, 256, 64);
+  copy_vec(d + L_B2, l[5], 256, 256);
+  pack_tiles(d + L_W3, l[6], 256, 0, 0, 4, 256);
+  copy_vec(d + L_B3, l[7], 4, 32);
+  // encode_imnet: e = {w0[64x525], b0, w1[64x64], b1, w2[256x64], b2, w3[256x256], b3, w4[3x256], b4}
+  pack_tiles(d + E_W0, e[0], 525, 0, 0, 64, 128);
+  column(d + E_WT, e[0], 525, 64, 524);
+  copy_vec(d + E_B0, e[1], 64, 64);
+  pack_tiles(d + E_W1, e[2], 64, 0, 0, 64, 64);
+  copy_vec(d + E_B1, e[3], 64, 64);
+  pack_tiles(d + E_W2, e[4], 64, 0, 0, 256, 64);
+  copy_vec(d + E_B2, e[5], 256, 256);
+  pack_tiles(d + E_W3, e[6], 256, 0, 0, 256, 256);
+  copy_vec(d + E_B3, e[7], 256, 256);
+  pack_tiles(d + E_W4, e[8], 256, 0, 0, 3, 256);
+  copy_vec(d + E_B4, e[9], 3, 32);
+  return STIF_OK;
+}

@@ -1,0 +1,46 @@
+// Shared device helpers for the STIF gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define STIF_DEV __device__ __forceinline__
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// v_mfma_f32_32x32x2_f32: D[32x32] += A[32x2] * B[2x32].
+// lane l supplies A[i = l&31][k = l>>5] and B[k = l>>5][j = l&31];
+// D/C: 16 regs, col = l&31, row = (r&3) + 8*(r>>2) + 4*(l>>5).
+STIF_DEV f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+STIF_DEV int mfma_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+STIF_DEV f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+STIF_DEV void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+
+STIF_DEV float lrelu01(float x) { return x >= 0.f ? x : x * 0.1f; }
+STIF_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+enum { STIF_ACT_NONE = 0, STIF_ACT_LRELU = 1, STIF_ACT_RELU = 2, STIF_ACT_RES = 3,
+       STIF_ACT_OFFMASK = 4, STIF_ACT_LSTM = 5 };
+
+// sin(x) with Cody-Waite reduction by pi/2 (3-part constant, exact q*C1 for |q| < 2^16)
+// and the cephes minimax polynomials on [-pi/4, pi/4].  Max abs error 9.3e-8 over
+// |x| <= 3000 (glibc sinf: 3.3e-8); SIREN arguments 30*z stay far inside the range.
+// Used instead of ocml sinf, whose Payne-Hanek path costs ~200 VGPRs in the MLP kernels.
+STIF_DEV float stif_sin(float x) {
+  const float q = rintf(x * 0.636619772367581343f);
+  const int qi = (int)q;
+  float r = fmaf(q, -1.5703125f, x);
+  r = fmaf(q, -4.837512969970703125e-4f, r);
+  r = fmaf(q, -7.54978995489188216e-8f, r);
+  const float r2 = r * r;
+  const float s = fmaf(r * r2, fmaf(r2, fmaf(r2, -1.9515295891e-4f, 8.3321608736e-3f), -1.6666654611e-1f), r);
+  const float c = fmaf(r2 * r2, fmaf(r2, fmaf(r2, 2.443315711809948e-5f, -1.388731625493765e-3f),
+                                     4.166664568298827e-2f),
+                       fmaf(-0.5f, r2, 1.0f));
+  const float res = (qi & 1) ? c : s;
+  return (qi & 2) ? -res : res;
+}

@@ -1,0 +1,195 @@
+"""Thin torch-facing wrappers over the C ABI.
+
+Torch tensors are only device buffers here: every op passes ``data_ptr()``s,
+sizes and the current HIP stream to libstif_hip.so.  Feature maps are NHWC
+``[items, H, W, C]`` fp32 tensors (any item stride; rows/pixels contiguous).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from .coords import TABLE_ORDER, dec_tables
+
+# Optional launch tracer (bench.py sets it to time the dominant kernel with HIP events on
+# the launch stream): an object with begin(kind: tuple, flops: float) and end().
+TRACE = None
+
+
+def _vp(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _item_stride(ts: Sequence[Optional[torch.Tensor]], what: str) -> int:
+    strides = {t.stride(0) for t in ts if t is not None}
+    if len(strides) > 1:
+        raise ValueError(f"{what}: groups must share the item stride, got {strides}")
+    for t in ts:
+        if t is None:
+            continue
+        if t.dtype != torch.float32 or not t.is_cuda:
+            raise ValueError(f"{what}: expected float32 CUDA tensors")
+        _, h, w, c = t.shape
+        if t.stride(3) != 1 or t.stride(2) != c or t.stride(1) != w * c:
+            raise ValueError(f"{what}: pixels of an item must be contiguous NHWC")
+    return strides.pop() if strides else 0
+
+
+@dataclass
+class PackedConv:
+    """A conv layer repacked for stif_conv2d_nhwc (see stif_pack_conv_weight)."""
+    w: torch.Tensor
+    b: torch.Tensor
+    cout: int
+    cin: int
+    ks: int
+    mode: int
+
+
+def pack_conv(weight: np.ndarray, bias: np.ndarray, mode: int = L.PACK_PLAIN, device="cuda") -> PackedConv:
+    weight = np.ascontiguousarray(weight, np.float32)
+    bias = np.ascontiguousarray(bias, np.float32)
+    cout, cin, ks, _ = weight.shape
+    lib = L.lib()
+    wd = np.empty(lib.stif_conv_weight_floats(cout, cin, ks), np.float32)
+    bd = np.empty(lib.stif_conv_bias_floats(cout), np.float32)
+    L.check(lib.stif_pack_conv_weight(weight.ctypes.data, bias.ctypes.data, cout, cin, ks, mode,
+                                      wd.ctypes.data, bd.ctypes.data), "stif_pack_conv_weight")
+    return PackedConv(torch.from_numpy(wd).to(device), torch.from_numpy(bd).to(device), cout, cin, ks, mode)
+
+
+def conv2d(groups, *, epi=L.EPI_NONE, in1_mode=0, in1_scale=1.0, stride=None):
+    """groups: list of dicts {layer: PackedConv, in0, [in1], out, [res], [out2]} with tensors
+    [nitems, H, W, C].  All groups share shapes and item strides."""
+    if not 1 <= len(groups) <= L.MAXG:
+        raise ValueError("conv2d: 1..8 groups")
+    g0 = groups[0]
+    lay: PackedConv = g0["layer"]
+    in0 = g0["in0"]
+    nitems, H, W, C0 = in0.shape
+    C1 = g0["in1"].shape[3] if in1_mode else 0
+    ks = lay.ks
+    if stride is None:
+        stride = 1
+    pad = ks // 2
+    Ho = (H + 2 * pad - ks) // stride + 1
+    Wo = (W + 2 * pad - ks) // stride + 1
+    a = L.ConvArgs()
+    for i, g in enumerate(groups):
+        if g["layer"].cin != C0 + C1 or g["layer"].ks != ks:
+            raise ValueError("conv2d: layer shape mismatch")
+        a.in0[i] = _vp(g["in0"])
+        a.in1[i] = _vp(g.get("in1"))
+        a.w[i] = _vp(g["layer"].w)
+        a.bias[i] = _vp(g["layer"].b)
+        a.out[i] = _vp(g["out"])
+        a.res[i] = _vp(g.get("res"))
+        a.out2[i] = _vp(g.get("out2"))
+        if tuple(g["out"].shape[:3]) != (nitems, Ho, Wo):
+            raise ValueError(f"conv2d: output shape {tuple(g['out'].shape)} != {(nitems, Ho, Wo)}")
+    a.in0_item = _item_stride([g["in0"] for g in groups], "in0")
+    a.in1_item = _item_stride([g.get("in1") for g in groups], "in1") if in1_mode else 0
+    a.out_item = _item_stride([g["out"] for g in groups], "out")
+    a.res_item = _item_stride([g.get("res") for g in groups], "res")
+    a.out2_item = _item_stride([g.get("out2") for g in groups], "out2")
+    a.ngroups, a.nitems = len(groups), nitems
+    a.H, a.W, a.C0, a.C1 = H, W, C0, C1
+    a.in1_mode, a.in1_scale = in1_mode, in1_scale
+    a.Ho, a.Wo, a.cout, a.ks, a.stride, a.epi = Ho, Wo, lay.cout, ks, stride, epi
+    tr = TRACE
+    if tr is not None:
+        tr.begin(("conv", ks, stride, epi, in1_mode, lay.cout),
+                 2.0 * lay.cout * (C0 + C1) * ks * ks * Ho * Wo * nitems * len(groups))
+    L.check(L.lib().stif_conv2d_nhwc(C.byref(a), _stream()), "stif_conv2d_nhwc")
+    if tr is not None:
+        tr.end()
+
+
+def conv_first(x_nchw: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: torch.Tensor):
+    n, c, h, wd = x_nchw.shape
+    assert c == 3 and x_nchw.is_contiguous() and out.is_contiguous()
+    L.check(L.lib().stif_conv_first(_vp(x_nchw), _vp(w), _vp(b), _vp(out), n, h, wd, _stream()), "stif_conv_first")
+
+
+def dcn(groups, *, epi=L.EPI_NONE):
+    """Fused DCN_sep core. groups: list of {layer: PackedConv (64->64 3x3), inp, offmask, out}."""
+    g0 = groups[0]
+    nitems, H, W, Cc = g0["inp"].shape
+    assert Cc == 64
+    a = L.DcnArgs()
+    for i, g in enumerate(groups):
+        a.inp[i] = _vp(g["inp"])
+        a.offmask[i] = _vp(g["offmask"])
+        a.w[i] = _vp(g["layer"].w)
+        a.bias[i] = _vp(g["layer"].b)
+        a.out[i] = _vp(g["out"])
+    a.in_item = _item_stride([g["inp"] for g in groups], "dcn in")
+    a.om_item = _item_stride([g["offmask"] for g in groups], "dcn offmask")
+    a.out_item = _item_stride([g["out"] for g in groups], "dcn out")
+    a.ngroups, a.nitems, a.H, a.W, a.epi = len(groups), nitems, H, W, epi
+    L.check(L.lib().stif_dcn_nhwc(C.byref(a), _stream()), "stif_dcn_nhwc")
+
+
+def dcn_v2_forward(input, weight, bias, offset, mask, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w,
+                   dilation_h, dilation_w, deformable_group):
+    """Drop-in for ``_ext.dcn_v2_forward`` (DCNv2/src/dcn_v2.h:9-23): NCHW in, new NCHW tensor out."""
+    for t in (input, weight, bias, offset, mask):
+        if not (t.is_cuda and t.dtype == torch.float32):
+            raise RuntimeError("dcn_v2_forward: tensors must be float32 on the GPU")
+    input, weight, bias, offset, mask = (t.contiguous() for t in (input, weight, bias, offset, mask))
+    b, c, h, w = input.shape
+    co, ci, kh, kw = weight.shape
+    if (kh, kw) != (kernel_h, kernel_w):
+        raise RuntimeError(f"Input shape and kernel shape wont match: ({kernel_h} x {kernel_w} vs {kh} x {kw}).")
+    if ci != c:
+        raise RuntimeError(f"Input shape and kernel channels wont match: ({c} vs {ci}).")
+    ho = (h + 2 * pad_h - (dilation_h * (kernel_h - 1) + 1)) // stride_h + 1
+    wo = (w + 2 * pad_w - (dilation_w * (kernel_w - 1) + 1)) // stride_w + 1
+    out = torch.empty(b, co, ho, wo, device=input.device, dtype=torch.float32)
+    lib = L.lib()
+    dims = (b, c, h, w, co, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w, dilation_h, dilation_w,
+            deformable_group)
+    nbytes = lib.stif_dcn_v2_workspace_size(*dims)
+    ws = torch.empty(max(nbytes // 4, 1), device=input.device, dtype=torch.float32)
+    L.check(lib.stif_dcn_v2_forward(_vp(input), _vp(weight), _vp(bias), _vp(offset), _vp(mask), _vp(out), *dims,
+                                    _vp(ws), nbytes, _stream()), "dcn_v2_forward")
+    return out
+
+
+class DecTablesDev:
+    """Device copies of coords.dec_tables(h, w, HH, WW) + the C struct pointing at them."""
+
+    def __init__(self, h, w, HH, WW, device="cuda"):
+        tab = dec_tables(h, w, HH, WW)
+        self._t = {k: torch.from_numpy(np.ascontiguousarray(tab[k])).to(device) for k in TABLE_ORDER}
+        self.c = L.DecTables(*[self._t[k].data_ptr() for k in TABLE_ORDER])
+        self.shape = (h, w, HH, WW)
+
+
+def dec_pack_lr(f0, f1, f2, x, out):
+    n, h, w, _ = f0.shape
+    L.check(L.lib().stif_dec_pack_lr(_vp(f0), _vp(f1), _vp(f2), _vp(x), _vp(out), n, h, w, _stream()),
+            "stif_dec_pack_lr")
+
+
+def dec_stage1(proj, mlp, tables: DecTablesDev, t, hrfeat, flow):
+    n, h, w, _ = proj.shape
+    HH, WW = hrfeat.shape[1:3]
+    L.check(L.lib().stif_dec_stage1(_vp(proj), _vp(mlp), C.byref(tables.c), _vp(t), _vp(hrfeat), _vp(flow), n, h, w,
+                                    HH, WW, _stream()), "stif_dec_stage1")
+
+
+def dec_stage2(proj, mlp, hrfeat, flow, tables: DecTablesDev, t, out):
+    n, h, w, _ = proj.shape
+    HH, WW = hrfeat.shape[1:3]
+    L.check(L.lib().stif_dec_stage2(_vp(proj), _vp(mlp), _vp(hrfeat), _vp(flow), C.byref(tables.c), _vp(t),
+                                    _vp(out), n, h, w, HH, WW, _stream()), "stif_dec_stage2")

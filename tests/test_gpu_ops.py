@@ -1,0 +1,226 @@
+"""Per-kernel parity of the HIP path (through the C ABI) against the CPU oracle."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import stif_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5   # fp32 MFMA vs fp64 oracle, relative to max |ref|
+
+
+def relmax(a, b):
+    a = a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else a
+    return float(np.abs(np.asarray(a, np.float64) - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def nhwc(x_nchw):
+    return torch.from_numpy(np.ascontiguousarray(np.asarray(x_nchw, np.float32).transpose(0, 2, 3, 1))).cuda()
+
+
+def to_nchw(t):
+    return t.detach().cpu().numpy().transpose(0, 3, 1, 2)
+
+
+@pytest.fixture(scope="module")
+def L(stif):
+    return stif._lib
+
+
+@pytest.fixture(scope="module")
+def ops(stif):
+    return stif.ops
+
+
+def rnd(*shape, seed=0, scale=1.0):
+    return (np.random.default_rng(seed).standard_normal(shape) * scale).astype(np.float32)
+
+
+@pytest.mark.parametrize("epi", ["none", "lrelu", "relu", "res"])
+@pytest.mark.parametrize("hw", [(13, 37), (8, 32), (33, 70)])
+def test_conv3x3(ops, L, epi, hw):
+    H, W = hw
+    x = rnd(3, 64, H, W, seed=1)
+    w = rnd(64, 64, 3, 3, seed=2, scale=0.05)
+    b = rnd(64, seed=3)
+    r = rnd(3, 64, H, W, seed=4)
+    ref = O.conv2d(x, w, b)
+    e = dict(none=L.EPI_NONE, lrelu=L.EPI_LRELU, relu=L.EPI_RELU, res=L.EPI_RES)[epi]
+    if epi == "lrelu":
+        ref = O.lrelu(ref)
+    if epi == "relu":
+        ref = O.relu(ref)
+    if epi == "res":
+        ref = ref + r
+    layer = ops.pack_conv(w, b)
+    out = torch.empty(3, H, W, 64, device="cuda")
+    ops.conv2d([dict(layer=layer, in0=nhwc(x), out=out, res=nhwc(r) if epi == "res" else None)], epi=e)
+    assert relmax(to_nchw(out), ref) < RTOL
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_conv_two_inputs_and_upsample(ops, L, mode):
+    H, W = 14, 38
+    x0 = rnd(2, 64, H, W, seed=5)
+    h1, w1 = (H, W) if mode == 1 else (H // 2, W // 2)
+    x1 = rnd(2, 64, h1, w1, seed=6)
+    w = rnd(64, 128, 3, 3, seed=7, scale=0.04)
+    b = rnd(64, seed=8)
+    up = x1.astype(np.float64) if mode == 1 else O.upsample2x(x1.astype(np.float64)) * 2
+    ref = O.lrelu(O.conv2d(np.concatenate([x0, up], 1), w, b))
+    out = torch.empty(2, H, W, 64, device="cuda")
+    ops.conv2d([dict(layer=ops.pack_conv(w, b), in0=nhwc(x0), in1=nhwc(x1), out=out)], epi=L.EPI_LRELU,
+               in1_mode=mode, in1_scale=1.0 if mode == 1 else 2.0)
+    assert relmax(to_nchw(out), ref) < RTOL
+
+
+def test_conv_groups_and_strided_items(ops, L):
+    """Two weight groups over strided item views (the PCD direction batching)."""
+    H, W = 12, 20
+    fr = rnd(6, 64, H, W, seed=9)
+    wa, wb = rnd(64, 128, 3, 3, seed=10, scale=0.04), rnd(64, 128, 3, 3, seed=11, scale=0.04)
+    ba, bb = rnd(64, seed=12), rnd(64, seed=13)
+    t = nhwc(fr)
+    f1, f2 = t[0::2], t[1::2]
+    out = torch.empty(2, 3, H, W, 64, device="cuda")
+    ops.conv2d([dict(layer=ops.pack_conv(wa, ba), in0=f1, in1=f2, out=out[0]),
+                dict(layer=ops.pack_conv(wb, bb), in0=f2, in1=f1, out=out[1])], in1_mode=1)
+    refa = O.conv2d(np.concatenate([fr[0::2], fr[1::2]], 1), wa, ba)
+    refb = O.conv2d(np.concatenate([fr[1::2], fr[0::2]], 1), wb, bb)
+    assert relmax(to_nchw(out[0]), refa) < RTOL
+    assert relmax(to_nchw(out[1]), refb) < RTOL
+
+
+def test_conv_stride2(ops, L):
+    x = rnd(2, 64, 20, 36, seed=14)
+    w = rnd(64, 64, 3, 3, seed=15, scale=0.05)
+    b = rnd(64, seed=16)
+    out = torch.empty(2, 10, 18, 64, device="cuda")
+    ops.conv2d([dict(layer=ops.pack_conv(w, b), in0=nhwc(x), out=out)], epi=L.EPI_LRELU, stride=2)
+    assert relmax(to_nchw(out), O.lrelu(O.conv2d(x, w, b, stride=2))) < RTOL
+
+
+def test_conv1x1_wide(ops, L):
+    x = rnd(2, 200, 9, 11, seed=17)
+    w = rnd(256, 200, 1, 1, seed=18, scale=0.05)
+    b = rnd(256, seed=19)
+    out = torch.empty(2, 9, 11, 256, device="cuda")
+    ops.conv2d([dict(layer=ops.pack_conv(w, b), in0=nhwc(x), out=out)])
+    assert relmax(to_nchw(out), O.conv2d(x, w, b)) < RTOL
+
+
+def test_offmask_conv(ops, L):
+    x = rnd(2, 64, 10, 40, seed=20)
+    w = rnd(216, 64, 3, 3, seed=21, scale=0.05)
+    b = rnd(216, seed=22)
+    out = torch.empty(2, 10, 40, 216, device="cuda")
+    ops.conv2d([dict(layer=ops.pack_conv(w, b, L.PACK_OFFMASK), in0=nhwc(x), out=out)], epi=L.EPI_OFFMASK)
+    ref = O.conv2d(x, w, b)
+    got = out.cpu().numpy().reshape(2, 10, 40, 8, 9, 3)
+    for g in range(8):
+        for k in range(9):
+            assert relmax(got[..., g, k, 0], ref[:, g * 18 + 2 * k]) < RTOL
+            assert relmax(got[..., g, k, 1], ref[:, g * 18 + 2 * k + 1]) < RTOL
+            assert relmax(got[..., g, k, 2], O.sigmoid(ref[:, 144 + g * 9 + k])) < RTOL
+
+
+def test_lstm_cell_conv(ops, L, sd):
+    x, h, c = rnd(2, 64, 6, 40, seed=23), rnd(2, 64, 6, 40, seed=24), rnd(2, 64, 6, 40, seed=25)
+    p = "ConvBLSTM.forward_net.cell_list.0."
+    hn, cn = O.conv_lstm_cell(x, h, c, sd, p, np.float64)
+    layer = ops.pack_conv(sd[p + "conv.weight"], sd[p + "conv.bias"], L.PACK_LSTM)
+    ho = torch.empty(2, 6, 40, 64, device="cuda")
+    co = torch.empty(2, 6, 40, 64, device="cuda")
+    ops.conv2d([dict(layer=layer, in0=nhwc(x), in1=nhwc(h), res=nhwc(c), out=ho, out2=co)], epi=L.EPI_LSTM,
+               in1_mode=1)
+    assert relmax(to_nchw(ho), hn) < RTOL
+    assert relmax(to_nchw(co), cn) < RTOL
+
+
+def test_conv_first(ops):
+    x = np.random.default_rng(26).random((3, 3, 12, 20)).astype(np.float32)
+    w = rnd(64, 3, 3, 3, seed=27, scale=0.2)
+    b = rnd(64, seed=28)
+    out = torch.empty(3, 12, 20, 64, device="cuda")
+    ops.conv_first(torch.from_numpy(x).cuda(), torch.from_numpy(w).cuda(), torch.from_numpy(b).cuda(), out)
+    assert relmax(to_nchw(out), O.lrelu(O.conv2d(x, w, b))) < RTOL
+
+
+def _offsets(B, H, W, seed):
+    rng = np.random.default_rng(seed)
+    off = (rng.standard_normal((B, 144, H, W)) * 2.0).astype(np.float32)
+    off[:, 0, 0, 0] = -1.0        # exactly on the `> -1` gate
+    off[:, 1, 2, 3] = -2.0
+    off[:, 2, 1, 1] = float(H)    # exactly on the `< H` gate
+    off[:, 5, 3, 2] = 0.5
+    mask = rng.random((B, 72, H, W)).astype(np.float32)
+    return off, mask
+
+
+@pytest.mark.parametrize("epi", ["none", "lrelu"])
+@pytest.mark.parametrize("hw", [(9, 11), (16, 40)])
+def test_dcn_fused(ops, L, epi, hw):
+    H, W = hw
+    B = 2
+    x = rnd(B, 64, H, W, seed=30)
+    w = rnd(64, 64, 3, 3, seed=31, scale=0.05)
+    b = rnd(64, seed=32)
+    off, mask = _offsets(B, H, W, 33)
+    ref = O.dcn_v2_forward(x, w, b, off, mask, 3, 3, 1, 1, 1, 1, 1, 1, 8)
+    if epi == "lrelu":
+        ref = O.lrelu(ref)
+    om = np.zeros((B, H, W, 216), np.float32)
+    o = off.reshape(B, 8, 9, 2, H, W).transpose(0, 4, 5, 1, 2, 3)
+    m = mask.reshape(B, 8, 9, H, W).transpose(0, 3, 4, 1, 2)
+    om = np.concatenate([o, m[..., None]], -1).reshape(B, H, W, 216)
+    out = torch.empty(B, H, W, 64, device="cuda")
+    ops.dcn([dict(layer=ops.pack_conv(w, b), inp=nhwc(x), offmask=torch.from_numpy(np.ascontiguousarray(om)).cuda(),
+                  out=out)], epi=L.EPI_LRELU if epi == "lrelu" else L.EPI_NONE)
+    assert relmax(to_nchw(out), ref) < RTOL
+
+
+@pytest.mark.parametrize("cfg", [
+    dict(B=2, C=64, Co=64, H=9, W=11, k=3, s=1, p=1, d=1, g=8),
+    dict(B=1, C=16, Co=24, H=10, W=7, k=3, s=2, p=1, d=1, g=2),
+    dict(B=2, C=6, Co=5, H=8, W=9, k=3, s=1, p=2, d=2, g=3),
+    dict(B=1, C=4, Co=70, H=6, W=6, k=1, s=1, p=0, d=1, g=1),
+])
+def test_dcn_v2_forward_dropin(ops, cfg):
+    c = cfg
+    K = c["k"] * c["k"]
+    ho = (c["H"] + 2 * c["p"] - (c["d"] * (c["k"] - 1) + 1)) // c["s"] + 1
+    wo = (c["W"] + 2 * c["p"] - (c["d"] * (c["k"] - 1) + 1)) // c["s"] + 1
+    x = rnd(c["B"], c["C"], c["H"], c["W"], seed=40)
+    w = rnd(c["Co"], c["C"], c["k"], c["k"], seed=41, scale=0.1)
+    b = rnd(c["Co"], seed=42)
+    rng = np.random.default_rng(43)
+    off = (rng.standard_normal((c["B"], c["g"] * 2 * K, ho, wo)) * 1.5).astype(np.float32)
+    mask = rng.random((c["B"], c["g"] * K, ho, wo)).astype(np.float32)
+    ref = O.dcn_v2_forward(x, w, b, off, mask, c["k"], c["k"], c["s"], c["s"], c["p"], c["p"], c["d"], c["d"], c["g"])
+    T = lambda a: torch.from_numpy(a).cuda()
+    out = ops.dcn_v2_forward(T(x), T(w), T(b), T(off), T(mask), c["k"], c["k"], c["s"], c["s"], c["p"], c["p"],
+                             c["d"], c["d"], c["g"])
+    assert tuple(out.shape) == ref.shape
+    assert relmax(out, ref) < RTOL
+
+
+def test_dcn_zero_offset_kat_gpu(ops, golden):
+    """The reference's own known-answer test (DCNv2/test.py:32-67) through the drop-in op."""
+    x = golden["ops"]["kat_input"]
+    N, C, H, W = x.shape
+    w = np.zeros((C, C, 3, 3), np.float32)
+    for p in range(C):
+        w[p, p, 1, 1] = 1.0
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).cuda()
+    out = ops.dcn_v2_forward(T(x), T(w), T(np.zeros(C)), T(np.zeros((N, 18, H, W))), T(np.full((N, 9, H, W), 0.5)),
+                             3, 3, 1, 1, 1, 1, 1, 1, 1)
+    assert float((T(x) - 2 * out).abs().max()) < 1e-6
+
+
+def test_dcn_dropin_rejects_bad_args(ops):
+    x = torch.zeros(1, 4, 5, 5, device="cuda")
+    with pytest.raises(RuntimeError, match="kernel channels"):
+        ops.dcn_v2_forward(x, torch.zeros(2, 3, 3, 3, device="cuda"), torch.zeros(2, device="cuda"),
+                           torch.zeros(1, 18, 5, 5, device="cuda"), torch.zeros(1, 9, 5, 5, device="cuda"),
+                           3, 3, 1, 1, 1, 1, 1, 1, 1)
