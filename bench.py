@@ -69,22 +69,24 @@ def synth_frames(first, count, H, W, device):
     return out.to(device)
 
 
-def cpu_baseline(stif, sd, frames_cpu, times, scale):
-    """The numpy oracle (fp32) on ONE pair of the same window, all host BLAS threads."""
+def cpu_baseline(stif, sd, frames_cpu, times, scale, crop=128):
+    """The numpy oracle (fp32) on a bounded sample of the same workload: one pair of the
+    window, cropped to crop x crop LR pixels (FLOP per output pixel does not depend on the
+    frame size), on all host BLAS threads."""
     from oracle import stif_oracle as O
     try:
         from threadpoolctl import threadpool_info
         threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
     except Exception:
         threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    x = frames_cpu[0:2].numpy()[None]
+    x = np.ascontiguousarray(frames_cpu[0:2, :, :crop, :crop].numpy()[None])
     t0 = time.perf_counter()
     O.forward(x, times, sd, dtype=np.float32)
     dt = time.perf_counter() - t0
     H, W = x.shape[-2:]
     mpix = len(times) * H * scale * W * scale / 1e6
     return {"value": mpix / dt, "unit": "Mpix/s", "cores": threads, "kind": "port",
-            "sample": f"1 pair (frames 0-1) of the same window, {H}x{W} -> {H * scale}x{W * scale}, "
+            "sample": f"1 pair (frames 0-1) of the same window cropped to {H}x{W} -> {H * scale}x{W * scale}, "
                       f"t={times}, numpy fp32 restatement (oracle/stif_oracle.py), {dt:.1f} s"}
 
 

@@ -21,24 +21,36 @@ module run on that restatement.
 from __future__ import annotations
 
 import numpy as np
-from numpy.lib.stride_tricks import sliding_window_view
 
 F32 = np.float32
 
 
 # ----------------------------------------------------------------------------- basic ops
 def conv2d(x, w, b, stride=1, pad=None, dtype=np.float64):
-    """nn.Conv2d forward (NCHW).  x [N,C,H,W], w [Co,C,kh,kw]."""
+    """nn.Conv2d forward (NCHW).  x [N,C,H,W], w [Co,C,kh,kw].
+
+    Computed as a sum over taps of contiguous row-slices of the zero-padded image
+    flattened to [(H+2p)*(W+2p), C] (output evaluated on the padded-width grid, the
+    2p junk columns dropped): one BLAS GEMM per tap and no im2col copy."""
     Co, C, kh, kw = w.shape
     if pad is None:
         pad = kh // 2
-    x = np.asarray(x, dtype)
-    if pad:
-        x = np.pad(x, ((0, 0), (0, 0), (pad, pad), (pad, pad)))
-    win = sliding_window_view(x, (kh, kw), axis=(2, 3))[:, :, ::stride, ::stride]
-    out = np.tensordot(win, np.asarray(w, dtype), axes=([1, 4, 5], [1, 2, 3]))  # [N,Ho,Wo,Co]
-    out = out.transpose(0, 3, 1, 2) + np.asarray(b, dtype)[None, :, None, None]
-    return np.ascontiguousarray(out)
+    N, _, H, W = x.shape
+    Hp, Wp = H + 2 * pad, W + 2 * pad
+    xp = np.zeros((N, Hp + 1, Wp, C), dtype)            # +1 row: the last tap's slice stays in bounds
+    xp[:, pad:pad + H, pad:pad + W, :] = np.asarray(x, dtype).transpose(0, 2, 3, 1)
+    flat = xp.reshape(N, (Hp + 1) * Wp, C)
+    Hf = Hp - kh + 1                                      # stride-1 output rows
+    wt = np.asarray(w, dtype).transpose(2, 3, 1, 0)      # [kh,kw,C,Co]
+    out = np.zeros((N, Hf * Wp, Co), dtype)
+    for n in range(N):
+        for i in range(kh):
+            for j in range(kw):
+                off = i * Wp + j
+                out[n] += np.dot(flat[n, off:off + Hf * Wp], wt[i, j])   # 2-D contiguous -> BLAS
+    out = out.reshape(N, Hf, Wp, Co)[:, ::stride, :Wp - kw + 1:stride]
+    out = out + np.asarray(b, dtype)
+    return np.ascontiguousarray(out.transpose(0, 3, 1, 2))
 
 
 def lrelu(x):
@@ -94,15 +106,15 @@ def dcn_v2_forward(inp, weight, bias, offset, mask, kh, kw, sh, sw, ph, pw, dh, 
     Wo = (W + 2 * pw - (dw * (kw - 1) + 1)) // sw + 1
     K = kh * kw
     cpg = C // dg
-    off = np.asarray(offset, F32).reshape(B, dg, K, 2, Ho, Wo)
-    msk = np.asarray(mask, dtype).reshape(B, dg, K, Ho, Wo)
-    h_in = (np.arange(Ho) * sh - ph).reshape(1, 1, Ho, 1)
-    w_in = (np.arange(Wo) * sw - pw).reshape(1, 1, 1, Wo)
-    img = inp.reshape(B, dg, cpg, H * W)
-    cols = np.zeros((B, dg, cpg, K, Ho, Wo), dtype)
-    bidx = np.arange(B)[:, None, None, None, None]
-    gidx = np.arange(dg)[None, :, None, None, None]
-    cidx = np.arange(cpg)[None, None, :, None, None]
+    P = Ho * Wo
+    off = np.asarray(offset, F32).reshape(B, dg, K, 2, P)
+    msk = np.asarray(mask, dtype).reshape(B, dg, K, P)
+    h_in = np.repeat(np.arange(Ho) * sh - ph, Wo)[None, None]          # [1,1,P]
+    w_in = np.tile(np.arange(Wo) * sw - pw, Ho)[None, None]
+    img = np.ascontiguousarray(inp.transpose(0, 2, 3, 1)).reshape(B, H * W, dg, cpg)
+    bi = np.arange(B)[:, None, None]
+    gi = np.arange(dg)[None, :, None]
+    cols = np.empty((B, P, K, dg, cpg), dtype)
     for i in range(kh):
         for j in range(kw):
             k = i * kw + j
@@ -117,24 +129,22 @@ def dcn_v2_forward(inp, weight, bias, offset, mask, kh, kw, sh, sw, ph, pw, dh, 
             h_low = h_low.astype(np.int64)
             w_low = w_low.astype(np.int64)
             h_high, w_high = h_low + 1, w_low + 1
-
-            def corner(hc, wc, ok):
-                idx = (np.clip(hc, 0, H - 1) * W + np.clip(wc, 0, W - 1))[:, :, None]
-                v = img[bidx, gidx, cidx, idx]                      # [B,dg,cpg,Ho,Wo]
-                return np.where(ok[:, :, None], v, 0)
-
-            v1 = corner(h_low, w_low, (h_low >= 0) & (w_low >= 0))
-            v2 = corner(h_low, w_high, (h_low >= 0) & (w_high <= W - 1))
-            v3 = corner(h_high, w_low, (h_high <= H - 1) & (w_low >= 0))
-            v4 = corner(h_high, w_high, (h_high <= H - 1) & (w_high <= W - 1))
-            e = lambda t: t[:, :, None]
-            val = e(hh * hw) * v1 + e(hh * lw) * v2 + e(lh * hw) * v3 + e(lh * lw) * v4
-            val = np.where(e(inside), val, 0)
-            cols[:, :, :, k] = val * e(msk[:, :, k])
-    cols = cols.reshape(B, C * K, Ho * Wo)
-    out = np.einsum("ok,bkn->bon", np.asarray(weight, dtype).reshape(Co, C * K), cols, optimize=True)
-    out = out + np.asarray(bias, dtype)[None, :, None]
-    return out.reshape(B, Co, Ho, Wo)
+            val = 0
+            for hc, wc, ok, wt in ((h_low, w_low, (h_low >= 0) & (w_low >= 0), hh * hw),
+                                   (h_low, w_high, (h_low >= 0) & (w_high <= W - 1), hh * lw),
+                                   (h_high, w_low, (h_high <= H - 1) & (w_low >= 0), lh * hw),
+                                   (h_high, w_high, (h_high <= H - 1) & (w_high <= W - 1), lh * lw)):
+                idx = np.clip(hc, 0, H - 1) * W + np.clip(wc, 0, W - 1)   # [B,dg,P]
+                v = img[bi, idx, gi]                                        # [B,dg,P,cpg]
+                val = val + v * np.where(ok, wt, 0)[..., None]
+            val = val * np.where(inside, msk[:, :, k], 0)[..., None]
+            cols[:, :, k] = val.transpose(0, 2, 1, 3)
+    wr = np.asarray(weight, dtype).transpose(2, 3, 1, 0).reshape(K * C, Co)  # [(tap, c), Co]
+    out = np.empty((B, P, Co), dtype)
+    for b in range(B):
+        out[b] = cols[b].reshape(P, K * C) @ wr
+    out = out + np.asarray(bias, dtype)
+    return np.ascontiguousarray(out.transpose(0, 2, 1)).reshape(B, Co, Ho, Wo)
 
 
 def dcn_sep(inp, fea, sd, name, groups=8, dtype=np.float64):
