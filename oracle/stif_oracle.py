@@ -253,13 +253,10 @@ def frame_features(frames, sd, front_RBs=5, dtype=np.float64):
     return L1, L2, L3
 
 
-def gen_feat(x, sd, front_RBs=5, back_RBs=40, dtype=np.float64, capture=None):
-    """LunaTokis.gen_feat (Sakuya_arch_test.py:313-362) for N=2 frames: x [B,2,3,H,W] -> [B,3,64,H,W]."""
-    B, N, C, H, W = x.shape
-    L1, L2, L3 = frame_features(np.asarray(x, dtype).reshape(B * N, C, H, W), sd, front_RBs, dtype)
-    lv = [t.reshape(B, N, *t.shape[1:]) for t in (L1, L2, L3)]
-    fea1 = [t[:, 0] for t in lv]
-    fea2 = [t[:, 1] for t in lv]
+def gen_feat_levels(fea1, fea2, sd, back_RBs=40, dtype=np.float64, capture=None):
+    """gen_feat after the per-frame features (Sakuya_arch_test.py:337-362): pyramids of the first
+    and second frame of each pair ([B,64,..] lists of 3 levels) -> latent [B,3,64,H,W]."""
+    B, _, H, W = fea1[0].shape
     aligned = pcd_align(fea1, fea2, sd, "pcd_align.", dtype)
     fused = conv2d(aligned, sd["fusion.weight"], sd["fusion.bias"], dtype=dtype)
     if capture is not None:
@@ -274,6 +271,14 @@ def gen_feat(x, sd, front_RBs=5, back_RBs=40, dtype=np.float64, capture=None):
         out = resblock(out, sd, f"recon_trunk.{i}", dtype)
     out = out.reshape(3, B, 64, H, W).transpose(1, 0, 2, 3, 4)
     return np.ascontiguousarray(out)
+
+
+def gen_feat(x, sd, front_RBs=5, back_RBs=40, dtype=np.float64, capture=None):
+    """LunaTokis.gen_feat (Sakuya_arch_test.py:313-362) for N=2 frames: x [B,2,3,H,W] -> [B,3,64,H,W]."""
+    B, N, C, H, W = x.shape
+    L1, L2, L3 = frame_features(np.asarray(x, dtype).reshape(B * N, C, H, W), sd, front_RBs, dtype)
+    lv = [t.reshape(B, N, *t.shape[1:]) for t in (L1, L2, L3)]
+    return gen_feat_levels([t[:, 0] for t in lv], [t[:, 1] for t in lv], sd, back_RBs, dtype, capture)
 
 
 # ----------------------------------------------------------------------------- decoder

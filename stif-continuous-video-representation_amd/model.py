@@ -353,16 +353,26 @@ class LunaTokis:
         self._feat = self._gen_feat_core(fea1, fea2)
         return None
 
-    def gen_feat_window(self, frames):
+    def frame_features(self, frames):
+        """Per-frame encoder (conv_first + feature_extraction + pyramid, :318-325) of frames
+        [F,3,H,W] -> NHWC (L1, L2, L3); used for sliding windows and halo exchange."""
+        frames = frames.to(self.device, torch.float32).contiguous()
+        return self._frame_features(frames)
+
+    def gen_feat_window(self, frames, last_frame_feats=None):
         """Sliding-window gen_feat: frames [F,3,H,W] -> latents of the F-1 adjacent pairs, with the
         per-frame encoder run once per frame (the reference harness runs it twice per inner frame,
-        custom_video_test.py:81-97)."""
+        custom_video_test.py:81-97).  ``last_frame_feats`` = (L1, L2, L3) of the last frame computed
+        elsewhere (parallel.halo_exchange); its encoder is then not recomputed here."""
         frames = frames.to(self.device, torch.float32).contiguous()
-        F_, C, H, Wd = frames.shape
         x = torch.stack([frames[:-1], frames[1:]], dim=1).contiguous()
         self._check_input(x)
         self.inp = x
-        l1, l2, l3 = self._frame_features(frames)
+        if last_frame_feats is None:
+            l1, l2, l3 = self._frame_features(frames)
+        else:
+            a1, a2, a3 = self._frame_features(frames[:-1].contiguous())
+            l1, l2, l3 = (torch.cat([a, b.reshape(1, *a.shape[1:])]) for a, b in zip((a1, a2, a3), last_frame_feats))
         self._feat = self._gen_feat_core([l1[:-1], l2[:-1], l3[:-1]], [l1[1:], l2[1:], l3[1:]])
         return None
 

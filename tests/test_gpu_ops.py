@@ -224,3 +224,17 @@ def test_dcn_dropin_rejects_bad_args(ops):
         ops.dcn_v2_forward(x, torch.zeros(2, 3, 3, 3, device="cuda"), torch.zeros(2, device="cuda"),
                            torch.zeros(1, 18, 5, 5, device="cuda"), torch.zeros(1, 9, 5, 5, device="cuda"),
                            3, 3, 1, 1, 1, 1, 1, 1, 1)
+
+
+def test_dcn_sep_plugin_module_matches_reference(stif, sd, golden):
+    """The reference plugin API (dcn_v2.py:110-140) on the drop-in op vs the reference's own DCN_sep run."""
+    g = golden["ops"]
+    m = stif.dcn_v2.DCN_sep(64, 64, 3, stride=1, padding=1, dilation=1, deformable_groups=8).cuda()
+    p = "pcd_align.L2_dcnpack_1"
+    with torch.no_grad():
+        m.weight.copy_(torch.from_numpy(sd[p + ".weight"]))
+        m.bias.copy_(torch.from_numpy(sd[p + ".bias"]))
+        m.conv_offset_mask.weight.copy_(torch.from_numpy(sd[p + ".conv_offset_mask.weight"]))
+        m.conv_offset_mask.bias.copy_(torch.from_numpy(sd[p + ".conv_offset_mask.bias"]))
+        out = m(torch.from_numpy(g["dcnsep_in"]).cuda(), torch.from_numpy(g["dcnsep_fea"]).cuda())
+    assert relmax(out, g["dcnsep_out"]) < 1e-4

@@ -1,0 +1,66 @@
+"""Multi-process (gloo, world_size 2, CPU) coverage of the frame-pair sharding and the
+optional boundary-frame halo exchange (stif_amd.parallel), with the oracle as compute."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import stif_oracle as O
+
+
+def test_pair_shards_cover_every_pair_once(stif):
+    P = stif.parallel
+    for F in (2, 3, 7, 9, 64, 65):
+        for world in (1, 2, 3, 8):
+            shards = P.pair_shards(F, world)
+            pairs = [p for (a, b) in shards for p in range(a, max(a, b - 1))]
+            assert pairs == list(range(F - 1)), (F, world, shards)
+            for (a, b), (c, d) in zip(shards, shards[1:]):
+                if b > a and d > c:
+                    assert c == b - 1          # one shared boundary frame
+    assert P.pair_shards(64, 8)[0] == (0, 9)    # C3: 63 pairs over 8 ranks = 8,8,...,7
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, frames, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import stif_pkg
+    stif = stif_pkg.load()
+    sd = stif.weights.make_state_dict(0)
+    a, b = stif.parallel.shard_for_rank(frames.shape[0], world, rank)
+    mine = frames[a:b]
+    own = O.frame_features(mine[:-1] if rank + 1 < world else mine, sd)
+    first = [torch.from_numpy(np.ascontiguousarray(t[:1])) for t in own]
+    halo = stif.parallel.halo_exchange(first, rank, world)
+    if halo is not None:
+        own = [np.concatenate([t, h.numpy()]) for t, h in zip(own, halo)]
+    fea1 = [t[:-1] for t in own]
+    fea2 = [t[1:] for t in own]
+    feat = O.gen_feat_levels(fea1, fea2, sd, back_RBs=40)
+    x = np.stack([mine[:-1], mine[1:]], axis=1)
+    out = O.decoding(feat, x, [0.5], sd)[0]
+    np.save(os.path.join(outdir, f"r{rank}.npy"), out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_window_equals_single_process(sd):
+    rng = np.random.default_rng(5)
+    frames = rng.random((5, 3, 8, 8))
+    ref = O.forward(np.stack([frames[:-1], frames[1:]], 1), [0.5], sd)[0]
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(2, _free_port(), frames, d), nprocs=2, join=True)
+        got = np.concatenate([np.load(os.path.join(d, f"r{r}.npy")) for r in range(2)])
+    assert got.shape == ref.shape
+    assert np.abs(got - ref).max() <= 1e-9 * np.abs(ref).max()
