@@ -145,11 +145,15 @@ int stif_dec_stage2(const float* proj, const float* mlp, const float* hrfeat, co
 /* ---- host-side weight packing (pure CPU, callable without a GPU) ---- */
 enum { STIF_PACK_PLAIN = 0, STIF_PACK_OFFMASK = 1, STIF_PACK_LSTM = 2 };
 
-/* Size in floats of a packed conv weight / bias. */
-size_t stif_conv_weight_floats(int cout, int cin, int ks);
-size_t stif_conv_bias_floats(int cout);
-/* w_oihw: [cout][cin][ks][ks] (nn.Conv2d layout).  dst layout: [cin/8][cout_pad][ks*ks][8],
- * cout_pad = cout rounded up to 32, rows permuted per `mode`. */
+/* Size in floats of a packed conv weight / bias for a packing mode. */
+size_t stif_conv_weight_floats(int cout, int cin, int ks, int mode);
+size_t stif_conv_bias_floats(int cout, int mode);
+/* w_oihw: [cout][cin][ks][ks] (nn.Conv2d layout).  dst layout:
+ * [slice][cin/8][ks*ks][nt][lane 64][4] -- the MFMA B fragments of one (slice, 8-channel chunk),
+ * contiguous so the kernel copies them to LDS with LDS-DMA; a slice is 32*NT output channels
+ * (NT = 7 for OFFMASK, 4 for LSTM, 2 otherwise), cout padded to a whole slice with zeros, and
+ * output rows permuted per `mode` (OFFMASK: [group][tap][dy, dx, mask]; LSTM: gates i,f,o,g
+ * of 32 hidden channels per slice). */
 int stif_pack_conv_weight(const float* w_oihw, const float* b, int cout, int cin, int ks, int mode,
                           float* w_dst, float* b_dst);
 

@@ -54,8 +54,8 @@ EXPORTS = {
     "stif_dec_pack_lr": (C.c_int, [_P, _P, _P, _P, _P, C.c_int, C.c_int, C.c_int, _P]),
     "stif_dec_stage1": (C.c_int, [_P, _P, C.POINTER(DecTables), _P, _P, _P] + [C.c_int] * 5 + [_P]),
     "stif_dec_stage2": (C.c_int, [_P, _P, _P, _P, C.POINTER(DecTables), _P, _P] + [C.c_int] * 5 + [_P]),
-    "stif_conv_weight_floats": (C.c_size_t, [C.c_int, C.c_int, C.c_int]),
-    "stif_conv_bias_floats": (C.c_size_t, [C.c_int]),
+    "stif_conv_weight_floats": (C.c_size_t, [C.c_int, C.c_int, C.c_int, C.c_int]),
+    "stif_conv_bias_floats": (C.c_size_t, [C.c_int, C.c_int]),
     "stif_pack_conv_weight": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P]),
     "stif_dec_proj_floats": (C.c_size_t, []),
     "stif_pack_dec_proj": (C.c_int, [_P] * 6),

@@ -21,19 +21,26 @@
 
 namespace {
 
-template <int KS, int S, int MT, int NT, int IN1, int EPI>
-__global__ __launch_bounds__(256) void k_conv(stif_conv_args a) {
-  constexpr int TH = 4 * MT;               // output rows per workgroup
+template <int KS, int S, int MT, int NT, int NW, int IN1, int EPI>
+__global__ __launch_bounds__(NW * 64) void k_conv(stif_conv_args a) {
+  constexpr int TH = NW * MT;              // output rows per workgroup
   constexpr int HR = (TH - 1) * S + KS;    // halo rows
   constexpr int HC = 31 * S + KS;          // halo cols
-  constexpr int PS = 12;                   // floats per staged pixel (8 + 4 pad: conflict-free b128)
   constexpr int T2 = KS * KS;
-  constexpr int WS = T2 * 8 + 4;           // floats per staged weight row
   constexpr int NJ = NT * 32;              // couts per workgroup
   constexpr int PAD = KS / 2;
-  __shared__ __attribute__((aligned(16))) float smem[HR * HC * PS + NJ * WS];
-  float* s_in = smem;
-  float* s_w = smem + HR * HC * PS;
+  constexpr int NTH = NW * 64;
+  // input halo image [row][h][col][4 floats] (h = channel half of the 8-channel chunk): lane-linear,
+  // so the LDS-DMA fills it directly and a wave's A-operand read is 32 consecutive 16-B slots
+  constexpr int IN_EL = HR * 2 * HC;
+  constexpr int IN_INST = (IN_EL + 63) / 64;
+  constexpr int IN_F = IN_INST * 256;
+  constexpr int W_EL = T2 * NT * 64;       // weight fragments per chunk: [tap][nt][lane][4]
+  constexpr int W_F = W_EL * 4;
+  constexpr int BUF_F = IN_F + W_F;
+  constexpr int SM_F = (2 * BUF_F > NW * 1024) ? 2 * BUF_F : NW * 1024;
+  constexpr int EPT = (IN_EL + NTH - 1) / NTH;   // register-staged (upsampled) elements per thread
+  __shared__ __attribute__((aligned(16))) float smem[SM_F];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -47,17 +54,83 @@ __global__ __launch_bounds__(256) void k_conv(stif_conv_args a) {
   const int g = blockIdx.z / a.nitems;
   const int n = blockIdx.z - g * a.nitems;
 
+  const int H = a.H, W = a.W, C0 = a.C0, C1 = a.C1;
   const float* in0 = a.in0[g] + (size_t)n * a.in0_item;
   const float* in1 = IN1 ? a.in1[g] + (size_t)n * a.in1_item : nullptr;
-  const int H = a.H, W = a.W, C0 = a.C0, C1 = a.C1;
+  const int H1 = (IN1 == 2) ? (H >> 1) : H, W1 = (IN1 == 2) ? (W >> 1) : W;
+  const __amdgpu_buffer_rsrc_t r0 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)in0, (short)0, (int)((size_t)H * W * C0 * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(IN1 == 1 ? in1 : in0), (short)0, (int)((size_t)H * W * (IN1 == 1 ? C1 : C0) * 4), 0x00020000);
   const int oy0 = ty * TH, ox0 = tx * 32;
   const int iy0 = oy0 * S - PAD, ix0 = ox0 * S - PAD;
   const int NC0 = C0 >> 3;
   const int NC = NC0 + (IN1 ? (C1 >> 3) : 0);
-  const int cout_pad = (a.cout + 31) & ~31;
-  const float* wbase = a.w[g] + (size_t)slice * NJ * T2 * 8;
-  const size_t wchunk = (size_t)cout_pad * T2 * 8;
-  const int H1 = H >> 1, W1 = W >> 1;
+  const float* wsl = a.w[g] + (size_t)slice * NC * W_F;   // packed [slice][chunk][tap][nt][lane][4]
+
+  // ---- staging: LDS-DMA for plain inputs and weights; registers for the x2-upsampled input
+  auto stage_dma = [&](int c, int buf) {
+    float* si = smem + buf * BUF_F;
+    float* sw = si + IN_F;
+    if (!(IN1 == 2 && c >= NC0)) {
+      const bool second = c >= NC0;
+      const int cc = second ? c - NC0 : c;
+      const int Cs = second ? C1 : C0;
+      for (int i = wv; i < IN_INST; i += NW) {
+        const int e = i * 64 + lane;
+        const int col = e % HC, rh = e / HC, h = rh & 1, row = rh >> 1;
+        const int y = iy0 + row, x = ix0 + col;
+        const bool ok = e < IN_EL && y >= 0 && y < H && x >= 0 && x < W;
+        const unsigned voff = ok ? (unsigned)((((size_t)y * W + x) * Cs + cc * 8 + h * 4) * 4) : 0x80000000u;
+        if (second)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(r1, si + i * 256, 16, voff, 0, 0, 0);
+        else
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(r0, si + i * 256, 16, voff, 0, 0, 0);
+      }
+    }
+    const float* wc = wsl + (size_t)c * W_F;
+    for (int i = wv; i < W_EL / 64; i += NW)
+      __builtin_amdgcn_global_load_lds(wc + (i * 64 + lane) * 4, sw + i * 256, 16, 0, 0);
+  };
+  f32x4 ur[EPT][4];
+  float uw[EPT][4];
+  auto up_issue = [&](int c) {   // F.interpolate(x2, bilinear, align_corners=False) corner loads
+    const int co = (c - NC0) * 8;
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+      const int e = tid + k * NTH;
+      const int col = e % HC, rh = e / HC, h = rh & 1, row = rh >> 1;
+      const int y = iy0 + row, x = ix0 + col;
+      const bool ok = e < IN_EL && y >= 0 && y < H && x >= 0 && x < W;
+      const float sy = fmaxf(0.5f * ((float)y + 0.5f) - 0.5f, 0.f);
+      const float sx = fmaxf(0.5f * ((float)x + 0.5f) - 0.5f, 0.f);
+      const int y0 = min((int)sy, H1 - 1), x0 = min((int)sx, W1 - 1);
+      const int y1 = y0 + (y0 < H1 - 1 ? 1 : 0), x1 = x0 + (x0 < W1 - 1 ? 1 : 0);
+      const float ly1 = sy - (float)y0, lx1 = sx - (float)x0;
+      uw[k][0] = ok ? 1.f - ly1 : 0.f;
+      uw[k][1] = ok ? ly1 : 0.f;
+      uw[k][2] = 1.f - lx1;
+      uw[k][3] = lx1;
+      const int c4 = co + h * 4;
+      const int yy0 = ok ? y0 : 0, yy1 = ok ? y1 : 0, xx0 = ok ? x0 : 0, xx1 = ok ? x1 : 0;
+      ur[k][0] = ld4(in1 + ((size_t)yy0 * W1 + xx0) * C1 + c4);
+      ur[k][1] = ld4(in1 + ((size_t)yy0 * W1 + xx1) * C1 + c4);
+      ur[k][2] = ld4(in1 + ((size_t)yy1 * W1 + xx0) * C1 + c4);
+      ur[k][3] = ld4(in1 + ((size_t)yy1 * W1 + xx1) * C1 + c4);
+    }
+  };
+  auto up_commit = [&](int buf) {
+    float* si = smem + buf * BUF_F;
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+      const int e = tid + k * NTH;
+      if (e < IN_EL) {
+        const f32x4 v = (uw[k][0] * (uw[k][2] * ur[k][0] + uw[k][3] * ur[k][1]) +
+                         uw[k][1] * (uw[k][2] * ur[k][2] + uw[k][3] * ur[k][3])) * a.in1_scale;
+        st4(si + e * 4, v);
+      }
+    }
+  };
 
   f32x16 acc[MT][NT];
 #pragma unroll
@@ -65,49 +138,19 @@ __global__ __launch_bounds__(256) void k_conv(stif_conv_args a) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x16{0};
 
+  stage_dma(0, 0);
+  if (IN1 == 2 && NC0 == 0) { up_issue(0); up_commit(0); }
+  __syncthreads();
   for (int c = 0; c < NC; ++c) {
-    // ---- stage the input halo of this 8-channel chunk
-    for (int e = tid; e < HR * HC * 2; e += 256) {
-      const int half = e & 1;
-      const int pix = e >> 1;
-      const int r = pix / HC;
-      const int cc = pix - r * HC;
-      const int y = iy0 + r, x = ix0 + cc;
-      f32x4 v = f32x4{0};
-      const bool inside = (y >= 0) & (y < H) & (x >= 0) & (x < W);
-      if (inside) {
-        if (c < NC0) {
-          v = ld4(in0 + ((size_t)y * W + x) * C0 + c * 8 + half * 4);
-        } else if (IN1 == 1) {
-          v = ld4(in1 + ((size_t)y * W + x) * C1 + (c - NC0) * 8 + half * 4);
-        } else if (IN1 == 2) {
-          // upsample_bilinear2d, align_corners=False, scale 2 (PyTorch area_pixel_compute_source_index)
-          const float sy = fmaxf(0.5f * ((float)y + 0.5f) - 0.5f, 0.f);
-          const float sx = fmaxf(0.5f * ((float)x + 0.5f) - 0.5f, 0.f);
-          const int y0 = (int)sy, x0 = (int)sx;
-          const int y1 = y0 + (y0 < H1 - 1 ? 1 : 0);
-          const int x1 = x0 + (x0 < W1 - 1 ? 1 : 0);
-          const float ly1 = sy - (float)y0, lx1 = sx - (float)x0;
-          const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
-          const int co = (c - NC0) * 8 + half * 4;
-          const f32x4 v00 = ld4(in1 + ((size_t)y0 * W1 + x0) * C1 + co);
-          const f32x4 v01 = ld4(in1 + ((size_t)y0 * W1 + x1) * C1 + co);
-          const f32x4 v10 = ld4(in1 + ((size_t)y1 * W1 + x0) * C1 + co);
-          const f32x4 v11 = ld4(in1 + ((size_t)y1 * W1 + x1) * C1 + co);
-          v = (ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11)) * a.in1_scale;
-        }
-      }
-      st4(s_in + pix * PS + half * 4, v);
+    const int nb = (c + 1) & 1;
+    const bool more = c + 1 < NC;
+    const bool up_next = IN1 == 2 && more && c + 1 >= NC0;
+    if (more) {
+      stage_dma(c + 1, nb);
+      if (up_next) up_issue(c + 1);
     }
-    // ---- stage the weight slice of this chunk: NJ rows x (T2*8) contiguous floats
-    const float* wc = wbase + (size_t)c * wchunk;
-    for (int e = tid; e < NJ * T2 * 2; e += 256) {
-      const int j = e / (T2 * 2);
-      const int q = e - j * (T2 * 2);
-      const f32x4 v = (slice * NJ + j < cout_pad) ? ld4(wc + (size_t)j * T2 * 8 + q * 4) : f32x4{0};
-      st4(s_w + j * WS + q * 4, v);
-    }
-    __syncthreads();
+    const float* si = smem + (c & 1) * BUF_F;
+    const float* sw = si + IN_F;
 #pragma unroll
     for (int tap = 0; tap < T2; ++tap) {
       const int ky = tap / KS, kx = tap % KS;
@@ -115,10 +158,10 @@ __global__ __launch_bounds__(256) void k_conv(stif_conv_args a) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const int oy = wv * MT + mt;
-        av[mt] = ld4(s_in + ((oy * S + ky) * HC + l32 * S + kx) * PS + hf * 4);
+        av[mt] = ld4(si + (((oy * S + ky) * 2 + hf) * HC + l32 * S + kx) * 4);
       }
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) bv[nt] = ld4(s_w + (nt * 32 + l32) * WS + tap * 8 + hf * 4);
+      for (int nt = 0; nt < NT; ++nt) bv[nt] = ld4(sw + ((tap * NT + nt) * 64 + lane) * 4);
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -126,75 +169,103 @@ __global__ __launch_bounds__(256) void k_conv(stif_conv_args a) {
 #pragma unroll
           for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma32(av[mt][q], bv[nt][q], acc[mt][nt]);
     }
+    if (up_next) up_commit(nb);
     __syncthreads();
   }
 
-  // ---- epilogue: lane holds cout l32 of tile nt for pixels x = mfma_row(r, lane)
+  // ---- epilogue (smem is free after the final barrier): one 4-KB block per wave
+  float* blk = smem + wv * 1024;
   const float* bias = a.bias[g] + slice * NJ;
+  const int rpx = lane >> 3, c4 = lane & 7;   // read-back mapping: px = 8i + rpx, channels 4*c4..
   if constexpr (EPI == STIF_EPI_LSTM) {
     static_assert(NT == 4, "LSTM epilogue needs the i,f,o,g tiles of one hidden channel in one lane");
     float* hout = a.out[g] + (size_t)n * a.out_item;
     float* cout_ = a.out2[g] + (size_t)n * a.out2_item;
     const float* ccur = a.res[g] + (size_t)n * a.res_item;
-    const int hc = slice * 32 + l32;   // hidden channel (weights packed with STIF_PACK_LSTM)
+    const int hc0 = slice * 32;           // hidden channels of this slice (STIF_PACK_LSTM)
     const float bi = bias[l32], bff = bias[32 + l32], bo = bias[64 + l32], bg = bias[96 + l32];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const int y = oy0 + wv * MT + mt;
+      const int yc = min(y, a.Ho - 1);
+      f32x16 hv, cv;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int x = ox0 + mfma_row(r, lane);
-        if (y < a.Ho && x < a.Wo) {
-          const size_t p = ((size_t)y * a.Wo + x) * 64 + hc;
-          const float i_ = sigmoidf_(acc[mt][0][r] + bi);
-          const float f_ = sigmoidf_(acc[mt][1][r] + bff);
-          const float o_ = sigmoidf_(acc[mt][2][r] + bo);
-          const float g_ = tanhf(acc[mt][3][r] + bg);
-          const float cn = f_ * ccur[p] + i_ * g_;
-          cout_[p] = cn;
-          hout[p] = o_ * tanhf(cn);
+        const int x = min(ox0 + mfma_row(r, lane), a.Wo - 1);
+        const float cc = ccur[((size_t)yc * a.Wo + x) * 64 + hc0 + l32];
+        const float i_ = sigmoidf_(acc[mt][0][r] + bi);
+        const float f_ = sigmoidf_(acc[mt][1][r] + bff);
+        const float o_ = sigmoidf_(acc[mt][2][r] + bo);
+        const float g_ = tanhf(acc[mt][3][r] + bg);
+        const float cn = f_ * cc + i_ * g_;
+        cv[r] = cn;
+        hv[r] = o_ * tanhf(cn);
+      }
+#pragma unroll
+      for (int which = 0; which < 2; ++which) {
+        tile_to_lds(blk, which ? cv : hv, lane);
+        float* dst = which ? cout_ : hout;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int px = i * 8 + rpx, x = ox0 + px;
+          const f32x4 v = lds_row4(blk, px, c4);
+          if (y < a.Ho && x < a.Wo) st4(dst + ((size_t)y * a.Wo + x) * 64 + hc0 + c4 * 4, v);
         }
       }
     }
   } else {
     float* out = a.out[g] + (size_t)n * a.out_item;
     const float* res = (EPI == STIF_EPI_RES) ? a.res[g] + (size_t)n * a.res_item : nullptr;
-    const int cstride = a.cout;
+    const int cs = a.cout;   // pixel stride of the output
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
-      const int co = slice * NJ + nt * 32 + l32;
-      if (co >= a.cout) continue;
+      const int cob = slice * NJ + nt * 32;   // first cout of this tile
+      if (cob >= a.cout) break;
       const float bv = bias[nt * 32 + l32];
+      const int co = cob + l32;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const int y = oy0 + wv * MT + mt;
-        if (y >= a.Ho) continue;
+        f32x16 v;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int x = ox0 + mfma_row(r, lane);
-          if (x >= a.Wo) continue;
-          const size_t p = ((size_t)y * a.Wo + x) * cstride + co;
-          float v = acc[mt][nt][r] + bv;
-          if (EPI == STIF_EPI_LRELU) v = lrelu01(v);
-          if (EPI == STIF_EPI_RELU) v = fmaxf(v, 0.f);
-          if (EPI == STIF_EPI_RES) v = res[p] + v;
+          float t = acc[mt][nt][r] + bv;
+          if (EPI == STIF_EPI_LRELU) t = lrelu01(t);
+          if (EPI == STIF_EPI_RELU) t = fmaxf(t, 0.f);
           if (EPI == STIF_EPI_OFFMASK) {
-            if (co < 216 && (co % 3) == 2) v = sigmoidf_(v);
+            if (co < 216 && (co % 3) == 2) t = sigmoidf_(t);
           }
-          out[p] = v;
+          v[r] = t;
+        }
+        tile_to_lds(blk, v, lane);
+        f32x4 rv[4];
+        if (EPI == STIF_EPI_RES) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int x = min(ox0 + i * 8 + rpx, a.Wo - 1);
+            rv[i] = ld4(res + ((size_t)min(y, a.Ho - 1) * a.Wo + x) * cs + cob + c4 * 4);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int px = i * 8 + rpx, x = ox0 + px;
+          f32x4 o = lds_row4(blk, px, c4);
+          if (EPI == STIF_EPI_RES) o = rv[i] + o;
+          if (y < a.Ho && x < a.Wo && cob + c4 * 4 < a.cout)
+            st4(out + ((size_t)y * a.Wo + x) * cs + cob + c4 * 4, o);
         }
       }
     }
   }
 }
 
-template <int KS, int S, int MT, int NT, int IN1, int EPI>
+template <int KS, int S, int MT, int NT, int NW, int IN1, int EPI>
 int launch(const stif_conv_args& a, hipStream_t st) {
-  constexpr int TH = 4 * MT;
+  constexpr int TH = NW * MT;
   const int tiles = ((a.Wo + 31) / 32) * ((a.Ho + TH - 1) / TH);
   const int slices = ((a.cout + 31) / 32 + NT - 1) / NT;
   dim3 grid(tiles, slices, a.ngroups * a.nitems);
-  hipLaunchKernelGGL((k_conv<KS, S, MT, NT, IN1, EPI>), grid, dim3(256), 0, st, a);
+  hipLaunchKernelGGL((k_conv<KS, S, MT, NT, NW, IN1, EPI>), grid, dim3(NW * 64), 0, st, a);
   return stif_check_launch("stif_conv2d_nhwc");
 }
 
@@ -268,34 +339,34 @@ extern "C" int stif_conv2d_nhwc(const stif_conv_args* pa, void* stream) {
   // dispatch on the shapes the STIF graph uses
   if (a.ks == 3 && a.stride == 1 && a.epi == STIF_EPI_LSTM) {
     if (a.cout != 256 || a.in1_mode != 1) return stif_fail(STIF_E_INVALID, "LSTM conv must be 128->256");
-    return launch<3, 1, 1, 4, 1, STIF_EPI_LSTM>(a, st);
+    return launch<3, 1, 1, 4, 8, 1, STIF_EPI_LSTM>(a, st);
   }
   if (a.ks == 3 && a.stride == 1 && a.epi == STIF_EPI_OFFMASK) {
     if (a.in1_mode != 0 || a.cout > 224) return stif_fail(STIF_E_INVALID, "offset conv must be 64->216");
-    return launch<3, 1, 1, 7, 0, STIF_EPI_OFFMASK>(a, st);
+    return launch<3, 1, 1, 7, 8, 0, STIF_EPI_OFFMASK>(a, st);
   }
   if (a.ks == 3 && a.stride == 2) {
     if (a.in1_mode != 0) return stif_fail(STIF_E_INVALID, "strided conv takes one input");
     switch (a.epi) {
-      case STIF_EPI_LRELU: return launch<3, 2, 1, 2, 0, STIF_EPI_LRELU>(a, st);
-      case STIF_EPI_NONE: return launch<3, 2, 1, 2, 0, STIF_EPI_NONE>(a, st);
+      case STIF_EPI_LRELU: return launch<3, 2, 1, 2, 4, 0, STIF_EPI_LRELU>(a, st);
+      case STIF_EPI_NONE: return launch<3, 2, 1, 2, 4, 0, STIF_EPI_NONE>(a, st);
       default: break;
     }
     return stif_fail(STIF_E_INVALID, "strided conv: unsupported epilogue");
   }
   if (a.ks == 1) {
     if (a.epi != STIF_EPI_NONE) return stif_fail(STIF_E_INVALID, "1x1 conv: unsupported epilogue");
-    if (a.in1_mode == 0) return launch<1, 1, 2, 2, 0, STIF_EPI_NONE>(a, st);
-    if (a.in1_mode == 1) return launch<1, 1, 2, 2, 1, STIF_EPI_NONE>(a, st);
+    if (a.in1_mode == 0) return launch<1, 1, 2, 2, 4, 0, STIF_EPI_NONE>(a, st);
+    if (a.in1_mode == 1) return launch<1, 1, 2, 2, 4, 1, STIF_EPI_NONE>(a, st);
     return stif_fail(STIF_E_INVALID, "1x1 conv: unsupported in1 mode");
   }
   // 3x3 stride 1
 #define STIF_CONV_CASE(IN1)                                                   \
   switch (a.epi) {                                                            \
-    case STIF_EPI_NONE: return launch<3, 1, 2, 2, IN1, STIF_EPI_NONE>(a, st); \
-    case STIF_EPI_LRELU: return launch<3, 1, 2, 2, IN1, STIF_EPI_LRELU>(a, st); \
-    case STIF_EPI_RELU: return launch<3, 1, 2, 2, IN1, STIF_EPI_RELU>(a, st); \
-    case STIF_EPI_RES: return launch<3, 1, 2, 2, IN1, STIF_EPI_RES>(a, st);   \
+    case STIF_EPI_NONE: return launch<3, 1, 2, 2, 4, IN1, STIF_EPI_NONE>(a, st); \
+    case STIF_EPI_LRELU: return launch<3, 1, 2, 2, 4, IN1, STIF_EPI_LRELU>(a, st); \
+    case STIF_EPI_RELU: return launch<3, 1, 2, 2, 4, IN1, STIF_EPI_RELU>(a, st); \
+    case STIF_EPI_RES: return launch<3, 1, 2, 2, 4, IN1, STIF_EPI_RES>(a, st);   \
     default: break;                                                           \
   }
   if (a.in1_mode == 0) { STIF_CONV_CASE(0) }

@@ -39,9 +39,8 @@ template <int EPI>
 __global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
   constexpr int NPX = 128;        // 4 rows x 32 cols
   constexpr int AS = 9 * 8 + 4;   // floats per staged pixel row of the A tile
-  constexpr int WS = 9 * 8 + 4;
-  constexpr int NJ = 64;
-  __shared__ __attribute__((aligned(16))) float smem[NPX * AS + NJ * WS];
+  constexpr int W_F = 9 * 2 * 64 * 4;   // one chunk of packed B fragments: [tap][nt][lane][4]
+  __shared__ __attribute__((aligned(16))) float smem[NPX * AS + W_F];
   float* s_a = smem;
   float* s_w = smem + NPX * AS;
 
@@ -72,17 +71,15 @@ __global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
       }
       st4(s_a + px * AS + tap * 8 + half * 4, v);
     }
-    const float* wc = wt + (size_t)dg * NJ * 72;
-    for (int e = tid; e < NJ * 18; e += 256) {
-      const int j = e / 18, q = e - j * 18;
-      st4(s_w + j * WS + q * 4, ld4(wc + j * 72 + q * 4));
-    }
+    const float* wc = wt + (size_t)dg * W_F;     // packed [chunk][tap][nt][lane][4] (stif_pack_conv_weight)
+    for (int i = wv; i < W_F / 256; i += 4)
+      __builtin_amdgcn_global_load_lds(wc + (i * 64 + lane) * 4, s_w + i * 256, 16, 0, 0);
     __syncthreads();
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const f32x4 av = ld4(s_a + (wv * 32 + l32) * AS + tap * 8 + hf * 4);
-      const f32x4 b0 = ld4(s_w + l32 * WS + tap * 8 + hf * 4);
-      const f32x4 b1 = ld4(s_w + (32 + l32) * WS + tap * 8 + hf * 4);
+      const f32x4 b0 = ld4(s_w + ((tap * 2 + 0) * 64 + lane) * 4);
+      const f32x4 b1 = ld4(s_w + ((tap * 2 + 1) * 64 + lane) * 4);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         acc0 = mfma32(av[q], b0[q], acc0);
@@ -91,21 +88,28 @@ __global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
     }
     __syncthreads();
   }
+  // epilogue through a per-wave LDS block -> coalesced 16-B stores (see tile_to_lds)
   float* out = a.out[g] + (size_t)n * a.out_item;
   const float* bias = a.bias[g];
   const int y = oy0 + wv;
-  if (y >= H) return;
+  float* blk = smem + wv * 1024;
+  const int rpx = lane >> 3, c4 = lane & 7;
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt) {
-    const int co = nt * 32 + l32;
-    const float bv = bias[co];
+    const float bv = bias[nt * 32 + l32];
+    f32x16 v;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int x = ox0 + mfma_row(r, lane);
-      if (x >= W) continue;
-      float v = (nt ? acc1[r] : acc0[r]) + bv;
-      if (EPI == STIF_EPI_LRELU) v = lrelu01(v);
-      out[((size_t)y * W + x) * 64 + co] = v;
+      float t = (nt ? acc1[r] : acc0[r]) + bv;
+      if (EPI == STIF_EPI_LRELU) t = lrelu01(t);
+      v[r] = t;
+    }
+    tile_to_lds(blk, v, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int px = i * 8 + rpx, x = ox0 + px;
+      const f32x4 o = lds_row4(blk, px, c4);
+      if (y < H && x < W) st4(out + ((size_t)y * W + x) * 64 + nt * 32 + c4 * 4, o);
     }
   }
 }

@@ -14,6 +14,13 @@ namespace {
 
 int round32(int x) { return (x + 31) & ~31; }
 
+// 32-wide N-tiles per workgroup slice of stif_conv2d_nhwc for a packing mode (conv.hip dispatch)
+int slice_tiles(int mode) { return mode == STIF_PACK_OFFMASK ? 7 : (mode == STIF_PACK_LSTM ? 4 : 2); }
+int cout_padded(int cout, int mode) {
+  const int nj = 32 * slice_tiles(mode);
+  return (cout + nj - 1) / nj * nj;
+}
+
 // source row of packed output channel j
 int src_row(int j, int cout, int mode) {
   if (j >= cout) return -1;
@@ -63,11 +70,11 @@ void column(float* dst, const float* W, int ld, int rows, int col) {
 
 }  // namespace
 
-extern "C" size_t stif_conv_weight_floats(int cout, int cin, int ks) {
-  return (size_t)round32(cout) * cin * ks * ks;
+extern "C" size_t stif_conv_weight_floats(int cout, int cin, int ks, int mode) {
+  return (size_t)cout_padded(cout, mode) * cin * ks * ks;
 }
 
-extern "C" size_t stif_conv_bias_floats(int cout) { return (size_t)round32(cout); }
+extern "C" size_t stif_conv_bias_floats(int cout, int mode) { return (size_t)cout_padded(cout, mode); }
 
 extern "C" int stif_pack_conv_weight(const float* w, const float* b, int cout, int cin, int ks, int mode,
                                      float* w_dst, float* b_dst) {
@@ -75,15 +82,24 @@ extern "C" int stif_pack_conv_weight(const float* w, const float* b, int cout, i
     return stif_fail(STIF_E_INVALID, "stif_pack_conv_weight: bad arguments");
   if (mode == STIF_PACK_OFFMASK && cout != 216) return stif_fail(STIF_E_INVALID, "offmask pack needs cout=216");
   if (mode == STIF_PACK_LSTM && cout != 256) return stif_fail(STIF_E_INVALID, "lstm pack needs cout=256");
-  const int cp = round32(cout), T2 = ks * ks, NC = cin / 8;
-  for (int c = 0; c < NC; ++c)
-    for (int j = 0; j < cp; ++j) {
-      const int sr = src_row(j, cout, mode);
+  // layout [slice][chunk][tap][nt][lane][4]: the B fragments of one (slice, chunk) are one
+  // contiguous block, copied to LDS by LDS-DMA; lane l of N-tile nt holds cout
+  // slice*NJ + nt*32 + (l & 31), input channels chunk*8 + 4*(l >> 5) + e.
+  const int NT = slice_tiles(mode), NJ = 32 * NT, cp = cout_padded(cout, mode), T2 = ks * ks, NC = cin / 8;
+  const int NS = cp / NJ;
+  for (int s = 0; s < NS; ++s)
+    for (int c = 0; c < NC; ++c)
       for (int t = 0; t < T2; ++t)
-        for (int ci = 0; ci < 8; ++ci)
-          w_dst[(((size_t)c * cp + j) * T2 + t) * 8 + ci] =
-              sr < 0 ? 0.f : w[((size_t)sr * cin + c * 8 + ci) * T2 + t];
-    }
+        for (int nt = 0; nt < NT; ++nt)
+          for (int l = 0; l < 64; ++l) {
+            const int j = s * NJ + nt * 32 + (l & 31);
+            const int sr = src_row(j, cout, mode);
+            for (int e = 0; e < 4; ++e) {
+              const int ci = c * 8 + 4 * (l >> 5) + e;
+              w_dst[(((((size_t)s * NC + c) * T2 + t) * NT + nt) * 64 + l) * 4 + e] =
+                  sr < 0 ? 0.f : w[((size_t)sr * cin + ci) * T2 + t];
+            }
+          }
   if (b_dst)
     for (int j = 0; j < cp; ++j) {
       const int sr = src_row(j, cout, mode);
@@ -92,7 +108,7 @@ extern "C" int stif_pack_conv_weight(const float* w, const float* b, int cout, i
   return STIF_OK;
 }
 
-extern "C" size_t stif_dec_proj_floats(void) { return stif_conv_weight_floats(256, stif_dec::SRC_C, 1); }
+extern "C" size_t stif_dec_proj_floats(void) { return stif_conv_weight_floats(256, stif_dec::SRC_C, 1, STIF_PACK_PLAIN); }
 
 extern "C" int stif_pack_dec_proj(const float* feat_w0, const float* feat_b0, const float* flow_w0,
                                   const float* enc_w0, float* w_dst, float* b_dst) {

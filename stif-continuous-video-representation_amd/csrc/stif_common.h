@@ -44,3 +44,17 @@ STIF_DEV float stif_sin(float x) {
   const float res = (qi & 1) ? c : s;
   return (qi & 2) ? -res : res;
 }
+
+// Epilogue helper: write one 32 px x 32 cout accumulator tile (lane = cout, regs = px) into the
+// wave's private 4-KB LDS block as [px][co] with the 16-B slot XOR-swizzled by px & 3 (bank-conflict
+// free for both the b32 writes and the b128 row reads), so the global stores become coalesced
+// 16-B accesses (8 pixels x 128 B per wave instruction).
+STIF_DEV void tile_to_lds(float* blk, const f32x16& v, int lane) {
+  const int l32 = lane & 31, hf = lane >> 5;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int px = (r & 3) + 8 * (r >> 2) + 4 * hf;
+    blk[px * 32 + (((l32 >> 2) ^ (px & 3)) << 2) + (l32 & 3)] = v[r];
+  }
+}
+STIF_DEV f32x4 lds_row4(const float* blk, int px, int c4) { return ld4(blk + px * 32 + ((c4 ^ (px & 3)) << 2)); }

@@ -148,7 +148,7 @@ class LunaTokis:
         # decoder
         lib = L.lib()
         wd = np.empty(lib.stif_dec_proj_floats(), np.float32)
-        bd = np.empty(lib.stif_conv_bias_floats(256), np.float32)
+        bd = np.empty(lib.stif_conv_bias_floats(256, L.PACK_PLAIN), np.float32)
         f0 = h["feat_imnet.net.0.linear.weight"]
         L.check(lib.stif_pack_dec_proj(f0.ctypes.data, h["feat_imnet.net.0.linear.bias"].ctypes.data,
                                        h["flow_imnet.net.0.linear.weight"].ctypes.data,

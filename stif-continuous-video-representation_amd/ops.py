@@ -60,8 +60,8 @@ def pack_conv(weight: np.ndarray, bias: np.ndarray, mode: int = L.PACK_PLAIN, de
     bias = np.ascontiguousarray(bias, np.float32)
     cout, cin, ks, _ = weight.shape
     lib = L.lib()
-    wd = np.empty(lib.stif_conv_weight_floats(cout, cin, ks), np.float32)
-    bd = np.empty(lib.stif_conv_bias_floats(cout), np.float32)
+    wd = np.empty(lib.stif_conv_weight_floats(cout, cin, ks, mode), np.float32)
+    bd = np.empty(lib.stif_conv_bias_floats(cout, mode), np.float32)
     L.check(lib.stif_pack_conv_weight(weight.ctypes.data, bias.ctypes.data, cout, cin, ks, mode,
                                       wd.ctypes.data, bd.ctypes.data), "stif_pack_conv_weight")
     return PackedConv(torch.from_numpy(wd).to(device), torch.from_numpy(bd).to(device), cout, cin, ks, mode)

@@ -35,36 +35,39 @@ def test_library_exports_every_header_symbol(stif):
     assert set(stif._lib.EXPORTS) >= names
 
 
-def _unpack_conv(wd, cout, cin, ks):
-    cp = (cout + 31) // 32 * 32
-    a = wd.reshape(cin // 8, cp, ks * ks, 8)            # [chunk][cout_pad][tap][ci]
-    return a.transpose(1, 0, 3, 2).reshape(cp, cin, ks, ks)
+def _unpack_conv(wd, cout_pad, cin, ks, nt):
+    """inverse of the [slice][chunk][tap][nt][lane][4] packing -> [cout_pad][cin][ks][ks]"""
+    ns = cout_pad // (32 * nt)
+    a = wd.reshape(ns, cin // 8, ks * ks, nt, 2, 32, 4)      # lane = h*32 + j
+    a = a.transpose(0, 3, 5, 1, 4, 6, 2)                      # [s][nt][j][chunk][h][e][tap]
+    return a.reshape(cout_pad, cin, ks, ks)
 
 
-@pytest.mark.parametrize("mode", ["plain", "offmask", "lstm"])
+@pytest.mark.parametrize("mode", ["plain", "offmask", "lstm", "plain1x1"])
 def test_pack_conv_layout(stif, mode):
     L = stif._lib
     rng = np.random.default_rng(0)
-    cout, cin, m = {"plain": (64, 128, L.PACK_PLAIN), "offmask": (216, 64, L.PACK_OFFMASK),
-                    "lstm": (256, 128, L.PACK_LSTM)}[mode][0], {"plain": 128, "offmask": 64, "lstm": 128}[mode], \
-        {"plain": L.PACK_PLAIN, "offmask": L.PACK_OFFMASK, "lstm": L.PACK_LSTM}[mode]
-    w = rng.standard_normal((cout, cin, 3, 3)).astype(np.float32)
+    cout, cin, ks, m, nt = {"plain": (64, 128, 3, L.PACK_PLAIN, 2), "offmask": (216, 64, 3, L.PACK_OFFMASK, 7),
+                            "lstm": (256, 128, 3, L.PACK_LSTM, 4), "plain1x1": (256, 200, 1, L.PACK_PLAIN, 2)}[mode]
+    w = rng.standard_normal((cout, cin, ks, ks)).astype(np.float32)
     b = rng.standard_normal(cout).astype(np.float32)
     lib = L.lib()
-    wd = np.empty(lib.stif_conv_weight_floats(cout, cin, 3), np.float32)
-    bd = np.empty(lib.stif_conv_bias_floats(cout), np.float32)
-    assert lib.stif_pack_conv_weight(w.ctypes.data, b.ctypes.data, cout, cin, 3, m, wd.ctypes.data, bd.ctypes.data) == 0
-    up = _unpack_conv(wd, cout, cin, 3)
-    if mode == "plain":
-        perm = np.arange(cout)
-    elif mode == "offmask":
+    wd = np.empty(lib.stif_conv_weight_floats(cout, cin, ks, m), np.float32)
+    bd = np.empty(lib.stif_conv_bias_floats(cout, m), np.float32)
+    assert lib.stif_pack_conv_weight(w.ctypes.data, b.ctypes.data, cout, cin, ks, m, wd.ctypes.data, bd.ctypes.data) == 0
+    cp = bd.size
+    assert cp % (32 * nt) == 0 and cp >= cout
+    up = _unpack_conv(wd, cp, cin, ks, nt)
+    if mode == "offmask":
         perm = []
         for g in range(8):
             for k in range(9):
                 perm += [g * 18 + 2 * k, g * 18 + 2 * k + 1, 144 + g * 9 + k]
         perm = np.array(perm)
-    else:
+    elif mode == "lstm":
         perm = np.array([gate * 64 + s * 32 + j for s in range(2) for gate in range(4) for j in range(32)])
+    else:
+        perm = np.arange(cout)
     assert np.array_equal(up[:cout], w[perm])
     assert np.array_equal(bd[:cout], b[perm])
     assert not up[cout:].any() and not bd[cout:].any()
