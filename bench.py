@@ -34,15 +34,22 @@ FP32_PEAK_TFLOPS = 157.3   # MI355X dense fp32 MFMA (MI355X_MICROARCH.md, chip-l
 
 
 class KernelTimer:
-    """HIP-event timing of every launch of one kernel variant, on the launch stream."""
+    """HIP-event timing of every launch of one kernel variant (or of all, kind=None), on the
+    launch stream."""
 
     def __init__(self, kind):
         self.kind = kind
         self.rec = []
+        self.all = []
         self._cur = None
 
+    kinds = None
+
     def begin(self, kind, flops):
-        if kind == self.kind:
+        if self.kind is None or kind == self.kind:
+            if self.kinds is None:
+                self.kinds = []
+            self.kinds.append(kind)
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -53,6 +60,18 @@ class KernelTimer:
             self._cur[1].record()
             self.rec.append(self._cur)
             self._cur = None
+
+    def report(self):
+        """per-kind launches / avg us / TFLOP/s (all-kinds mode)"""
+        agg = {}
+        for (a, b, f), k in zip(self.rec, self.kinds):
+            d = agg.setdefault(k, [0, 0.0, 0.0])
+            d[0] += 1
+            d[1] += a.elapsed_time(b)
+            d[2] += f
+        for k, (nl, ms, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+            print(f"  {str(k):40s} {nl:5d} launches {ms / nl * 1e3:9.1f} us avg {fl / (ms * 1e-3) / 1e12:7.1f} TFLOP/s"
+                  f"  {ms:8.2f} ms total", file=sys.stderr)
 
     def summary(self):
         ms = [a.elapsed_time(b) for a, b, _ in self.rec]
@@ -98,6 +117,7 @@ def main():
     ap.add_argument("--config", default="c1", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_r01.json"))
+    ap.add_argument("--kernel-report", action="store_true", help="time every conv launch kind (stderr)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -148,6 +168,15 @@ def main():
         td.all_reduce(t, op=td.ReduceOp.MAX)
         elapsed = float(t.item())
     n_launch, avg_ms, avg_flops = timer.summary()
+    if args.kernel_report and rank == 0:
+        with torch.no_grad():
+            rep = KernelTimer(None)
+            stif.ops.TRACE = rep
+            step()
+            torch.cuda.synchronize()
+            stif.ops.TRACE = None
+        print("conv launch report (one extra step, not timed):", file=sys.stderr)
+        rep.report()
 
     out_pix = pairs * len(times) * (H * scale) * (W * scale)
     value = world * out_pix * args.steps / elapsed / 1e6

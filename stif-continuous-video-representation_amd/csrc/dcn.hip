@@ -35,14 +35,23 @@ STIF_DEV f32x4 dcn_sample4(const float* __restrict__ img, int H, int W, float h,
   return w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4;
 }
 
+// Workgroup: 4 waves, 4 output rows x 32 px, all 64 output channels.  Per deformable group
+// (= 8 input channels = one K chunk): the group's input tile with an M-pixel margin around the
+// 3x3 footprint ([row][channel half][col][4], zero-filled outside the frame) and the group's
+// weight fragments are LDS-DMA'd one chunk ahead (double-buffered).  Each lane then bilinearly
+// samples its own MFMA A-fragment (pixel = lane & 31, channels 4h..4h+3) tap by tap from the
+// tile -- falling back to global loads only when an offset leaves the margin -- so sampling
+// (VALU + LDS) interleaves with the MFMAs and no sampled A tile ever round-trips memory.
 template <int EPI>
 __global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
-  constexpr int NPX = 128;        // 4 rows x 32 cols
-  constexpr int AS = 9 * 8 + 4;   // floats per staged pixel row of the A tile
-  constexpr int W_F = 9 * 2 * 64 * 4;   // one chunk of packed B fragments: [tap][nt][lane][4]
-  __shared__ __attribute__((aligned(16))) float smem[NPX * AS + W_F];
-  float* s_a = smem;
-  float* s_w = smem + NPX * AS;
+  constexpr int NW = 4, TH = 4, M = 4;
+  constexpr int TR = TH + 2 + 2 * M, TC = 32 + 2 + 2 * M;   // tile rows / cols
+  constexpr int T_EL = TR * 2 * TC;                          // 16-B elements
+  constexpr int T_INST = (T_EL + 63) / 64;
+  constexpr int T_F = T_INST * 256;
+  constexpr int W_F = 9 * 2 * 64 * 4;                        // packed B fragments: [tap][nt][lane][4]
+  constexpr int BUF_F = T_F + W_F;
+  __shared__ __attribute__((aligned(16))) float smem[2 * BUF_F];
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l32 = lane & 31, hf = lane >> 5;
   const int H = a.H, W = a.W;
@@ -52,39 +61,83 @@ __global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
   const float* in = a.in[g] + (size_t)n * a.in_item;
   const float* om = a.offmask[g] + (size_t)n * a.om_item;
   const float* wt = a.w[g];
-  const int oy0 = ty * 4, ox0 = tx * 32;
+  const int oy0 = ty * TH, ox0 = tx * 32;
+  const int ty0 = oy0 - 1 - M, tx0 = ox0 - 1 - M;           // tile origin (frame coords)
+  const int oy = oy0 + wv, ox = ox0 + l32;                   // this lane's output pixel
+  const bool pix_ok = oy < H && ox < W;
+  const float* omp = om + ((size_t)min(oy, H - 1) * W + min(ox, W - 1)) * OMC;
+  const __amdgpu_buffer_rsrc_t rin =
+      __builtin_amdgcn_make_buffer_rsrc((void*)in, (short)0, (int)((size_t)H * W * 64 * 4), 0x00020000);
+
+  auto stage = [&](int dg, int buf) {
+    float* st = smem + buf * BUF_F;
+    float* sw = st + T_F;
+    for (int i = wv; i < T_INST; i += NW) {
+      const int e = i * 64 + lane;
+      const int col = e % TC, rh = e / TC, h = rh & 1, row = rh >> 1;
+      const int y = ty0 + row, x = tx0 + col;
+      const bool ok = e < T_EL && y >= 0 && y < H && x >= 0 && x < W;
+      const unsigned voff = ok ? (unsigned)((((size_t)y * W + x) * 64 + dg * 8 + h * 4) * 4) : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, st + i * 256, 16, voff, 0, 0, 0);
+    }
+    const float* wc = wt + (size_t)dg * W_F;   // packed [chunk][tap][nt][lane][4]
+    for (int i = wv; i < W_F / 256; i += NW)
+      __builtin_amdgcn_global_load_lds(wc + (i * 64 + lane) * 4, sw + i * 256, 16, 0, 0);
+  };
+  float omc[27], omn[27];
+#pragma unroll
+  for (int k = 0; k < 27; ++k) omc[k] = omp[k];
 
   f32x16 acc0 = f32x16{0}, acc1 = f32x16{0};
+  stage(0, 0);
+  __syncthreads();
   for (int dg = 0; dg < 8; ++dg) {
-    for (int e = tid; e < NPX * 9 * 2; e += 256) {
-      const int half = e & 1;
-      const int it = e >> 1;
-      const int px = it / 9, tap = it - px * 9;
-      const int oy = oy0 + (px >> 5), ox = ox0 + (px & 31);
-      f32x4 v = f32x4{0};
-      if (oy < H && ox < W) {
-        const float* o = om + ((size_t)oy * W + ox) * OMC + dg * 27 + tap * 3;
-        const float h_im = (float)(oy - 1 + tap / 3) + o[0];
-        const float w_im = (float)(ox - 1 + tap % 3) + o[1];
-        if (h_im > -1.f && w_im > -1.f && h_im < (float)H && w_im < (float)W)
-          v = dcn_sample4(in, H, W, h_im, w_im, dg * 8 + half * 4) * o[2];
-      }
-      st4(s_a + px * AS + tap * 8 + half * 4, v);
+    if (dg + 1 < 8) {
+      stage(dg + 1, (dg + 1) & 1);
+#pragma unroll
+      for (int k = 0; k < 27; ++k) omn[k] = omp[(dg + 1) * 27 + k];
     }
-    const float* wc = wt + (size_t)dg * W_F;     // packed [chunk][tap][nt][lane][4] (stif_pack_conv_weight)
-    for (int i = wv; i < W_F / 256; i += 4)
-      __builtin_amdgcn_global_load_lds(wc + (i * 64 + lane) * 4, s_w + i * 256, 16, 0, 0);
-    __syncthreads();
+    const float* st = smem + (dg & 1) * BUF_F;
+    const float* sw = st + T_F;
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
-      const f32x4 av = ld4(s_a + (wv * 32 + l32) * AS + tap * 8 + hf * 4);
-      const f32x4 b0 = ld4(s_w + ((tap * 2 + 0) * 64 + lane) * 4);
-      const f32x4 b1 = ld4(s_w + ((tap * 2 + 1) * 64 + lane) * 4);
+      // modulated_deformable_im2col (dcn_v2_im2col_cuda.cu:158-192) for this lane's pixel / tap
+      const float h_im = (float)(oy - 1 + tap / 3) + omc[tap * 3];
+      const float w_im = (float)(ox - 1 + tap % 3) + omc[tap * 3 + 1];
+      f32x4 av = f32x4{0};
+      if (pix_ok && h_im > -1.f && w_im > -1.f && h_im < (float)H && w_im < (float)W) {
+        const float fh = floorf(h_im), fw = floorf(w_im);
+        const int h_low = (int)fh, w_low = (int)fw;
+        const float lh = h_im - fh, lw = w_im - fw, hh = 1.f - lh, hw = 1.f - lw;
+        const int r0 = h_low - ty0, c0 = w_low - tx0;
+        f32x4 v1, v2, v3, v4;
+        if (r0 >= 0 && r0 + 1 < TR && c0 >= 0 && c0 + 1 < TC) {
+          // in the staged tile (zero outside the frame = dmcn_im2col_bilinear's corner checks)
+          const float* p0 = st + ((r0 * 2 + hf) * TC + c0) * 4;
+          const float* p1 = p0 + 2 * TC * 4;
+          v1 = ld4(p0); v2 = ld4(p0 + 4); v3 = ld4(p1); v4 = ld4(p1 + 4);
+        } else {
+          const int h_high = h_low + 1, w_high = w_low + 1, co = dg * 8 + hf * 4;
+          v1 = (h_low >= 0 && w_low >= 0) ? ld4(in + ((size_t)h_low * W + w_low) * 64 + co) : f32x4{0};
+          v2 = (h_low >= 0 && w_high <= W - 1) ? ld4(in + ((size_t)h_low * W + w_high) * 64 + co) : f32x4{0};
+          v3 = (h_high <= H - 1 && w_low >= 0) ? ld4(in + ((size_t)h_high * W + w_low) * 64 + co) : f32x4{0};
+          v4 = (h_high <= H - 1 && w_high <= W - 1) ? ld4(in + ((size_t)h_high * W + w_high) * 64 + co)
+                                                     : f32x4{0};
+        }
+        const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
+        av = (w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4) * omc[tap * 3 + 2];
+      }
+      const f32x4 b0 = ld4(sw + ((tap * 2 + 0) * 64 + lane) * 4);
+      const f32x4 b1 = ld4(sw + ((tap * 2 + 1) * 64 + lane) * 4);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         acc0 = mfma32(av[q], b0[q], acc0);
         acc1 = mfma32(av[q], b1[q], acc1);
       }
+    }
+    if (dg + 1 < 8) {
+#pragma unroll
+      for (int k = 0; k < 27; ++k) omc[k] = omn[k];
     }
     __syncthreads();
   }

@@ -136,7 +136,12 @@ def dcn(groups, *, epi=L.EPI_NONE):
     a.om_item = _item_stride([g["offmask"] for g in groups], "dcn offmask")
     a.out_item = _item_stride([g["out"] for g in groups], "dcn out")
     a.ngroups, a.nitems, a.H, a.W, a.epi = len(groups), nitems, H, W, epi
+    tr = TRACE
+    if tr is not None:
+        tr.begin(("dcn", epi), 2.0 * 64 * 576 * H * W * nitems * len(groups))
     L.check(L.lib().stif_dcn_nhwc(C.byref(a), _stream()), "stif_dcn_nhwc")
+    if tr is not None:
+        tr.end()
 
 
 def dcn_v2_forward(input, weight, bias, offset, mask, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w,
@@ -184,12 +189,22 @@ def dec_pack_lr(f0, f1, f2, x, out):
 def dec_stage1(proj, mlp, tables: DecTablesDev, t, hrfeat, flow):
     n, h, w, _ = proj.shape
     HH, WW = hrfeat.shape[1:3]
+    tr = TRACE
+    if tr is not None:   # executed MFMA work: 1,088 v_mfma_f32_32x32x2_f32 per 32 HR pixels
+        tr.begin(("dec1",), 1088 / 32 * 4096.0 * n * HH * WW)
     L.check(L.lib().stif_dec_stage1(_vp(proj), _vp(mlp), C.byref(tables.c), _vp(t), _vp(hrfeat), _vp(flow), n, h, w,
                                     HH, WW, _stream()), "stif_dec_stage1")
+    if tr is not None:
+        tr.end()
 
 
 def dec_stage2(proj, mlp, hrfeat, flow, tables: DecTablesDev, t, out):
     n, h, w, _ = proj.shape
     HH, WW = hrfeat.shape[1:3]
+    tr = TRACE
+    if tr is not None:   # executed MFMA work: 1,600 v_mfma_f32_32x32x2_f32 per 32 HR pixels
+        tr.begin(("dec2",), 1600 / 32 * 4096.0 * n * HH * WW)
     L.check(L.lib().stif_dec_stage2(_vp(proj), _vp(mlp), _vp(hrfeat), _vp(flow), C.byref(tables.c), _vp(t),
                                     _vp(out), n, h, w, HH, WW, _stream()), "stif_dec_stage2")
+    if tr is not None:
+        tr.end()
