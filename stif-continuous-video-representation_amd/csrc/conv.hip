@@ -140,7 +140,7 @@ __global__ __launch_bounds__(NW * 64) void k_conv(stif_conv_args a) {
 
   stage_dma(0, 0);
   if (IN1 == 2 && NC0 == 0) { up_issue(0); up_commit(0); }
-  __syncthreads();
+  lds_dma_barrier();
   for (int c = 0; c < NC; ++c) {
     const int nb = (c + 1) & 1;
     const bool more = c + 1 < NC;
@@ -170,7 +170,7 @@ __global__ __launch_bounds__(NW * 64) void k_conv(stif_conv_args a) {
           for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma32(av[mt][q], bv[nt][q], acc[mt][nt]);
     }
     if (up_next) up_commit(nb);
-    __syncthreads();
+    lds_dma_barrier();
   }
 
   // ---- epilogue (smem is free after the final barrier): one 4-KB block per wave

@@ -90,7 +90,7 @@ __global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
 
   f32x16 acc0 = f32x16{0}, acc1 = f32x16{0};
   stage(0, 0);
-  __syncthreads();
+  lds_dma_barrier();
   for (int dg = 0; dg < 8; ++dg) {
     if (dg + 1 < 8) {
       stage(dg + 1, (dg + 1) & 1);
@@ -139,7 +139,7 @@ __global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
 #pragma unroll
       for (int k = 0; k < 27; ++k) omc[k] = omn[k];
     }
-    __syncthreads();
+    lds_dma_barrier();
   }
   // epilogue through a per-wave LDS block -> coalesced 16-B stores (see tile_to_lds)
   float* out = a.out[g] + (size_t)n * a.out_item;

@@ -24,24 +24,6 @@ namespace {
 
 using namespace stif_dec;
 
-// acc += W_tile(ot) . X  over KT K-tiles; wt points at tile (ot, kt=0); x = KT register tiles
-template <int KT>
-STIF_DEV void mlp_acc(f32x16& acc, const float* __restrict__ wt, const f32x16* x, int lane) {
-#pragma unroll
-  for (int kt = 0; kt < KT; ++kt) {
-    const float* b = wt + kt * T + lane * 4;
-    const f32x4 w0 = ld4(b), w1 = ld4(b + 256), w2 = ld4(b + 512), w3 = ld4(b + 768);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) acc = mfma32(w0[e], x[kt][e], acc);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) acc = mfma32(w1[e], x[kt][4 + e], acc);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) acc = mfma32(w2[e], x[kt][8 + e], acc);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) acc = mfma32(w3[e], x[kt][12 + e], acc);
-  }
-}
-
 // SineLayer: sin(30 * (z + b))  (SIREN.py:44-45, omega_0 = 30)
 STIF_DEV f32x16 bias_sin(f32x16 z, const float* __restrict__ b, int hf) {
 #pragma unroll
@@ -98,20 +80,66 @@ STIF_DEV void gather64(f32x16* dst, const float* __restrict__ base, int stride, 
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const int c = c0 + ot * 32 + 8 * v + 4 * hf;
-      const f32x4 s = b.w00 * ld4(base + (size_t)b.o00 * stride + c) + b.w01 * ld4(base + (size_t)b.o01 * stride + c) +
+      f32x4 s = b.w00 * ld4(base + (size_t)b.o00 * stride + c) + b.w01 * ld4(base + (size_t)b.o01 * stride + c) +
                       b.w10 * ld4(base + (size_t)b.o10 * stride + c) + b.w11 * ld4(base + (size_t)b.o11 * stride + c);
+      // combine the corners here: otherwise the blend is sunk to the first use (past a barrier)
+      // and all four corners of every channel stay live
+      asm volatile("" : "+v"(s));
 #pragma unroll
       for (int e = 0; e < 4; ++e) dst[ot][4 * v + e] = s[e];
     }
 }
 
-__global__ __launch_bounds__(256) void k_dec1(const float* __restrict__ proj, const float* __restrict__ mlp,
-                                              stif_dec_tables tb, const float* __restrict__ tq,
-                                              float* __restrict__ hrfeat, float* __restrict__ flow, int n, int h,
-                                              int w, int HH, int WW) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, hf = lane >> 5;
+// ---- weight streaming: a workgroup consumes its MLP weight tiles segment by segment; each segment
+// (a few 4-KB tiles: one layer, or one output tile's K-tiles) is LDS-DMA'd while the previous one
+// is being consumed (double-buffered, one barrier per segment), and every wave reads its A
+// operands from LDS -- one tile feeds 16 MFMAs in each wave of the workgroup.
+constexpr int DEC_NW = 8;    // waves per workgroup of k_dec1 (178 VGPRs: 2 waves/SIMD)
+constexpr int DEC2_NW = 4;   // k_dec2 keeps 8 layer-2 tiles (128 VGPRs) live: 1 wave/SIMD
+constexpr int SEG = 10;      // max tiles per segment
+
+// Buffer loads with the tile offset in SGPRs: the per-lane operand is the same lane*16 for every
+// tile (flat global_load_lds would keep a 64-bit VGPR address per hoisted tile live).
+template <int NW>
+STIF_DEV void dma_tiles(float* dst, __amdgpu_buffer_rsrc_t rm, int src, int ntiles, int wv, int lane) {
+  for (int k = wv; k < ntiles * 4; k += NW)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rm, dst + k * 256, 16, lane * 16, (src + k * 256) * 4, 0, 0);
+}
+
+STIF_DEV __amdgpu_buffer_rsrc_t mlp_rsrc(const float* mlp) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)mlp, (short)0, (int)(MLP_FLOATS * 4), 0x00020000);
+}
+
+// acc += W_tile . x, tile in LDS ([v][lane][4]), x = one 32-feature register tile
+STIF_DEV void tile_mma(f32x16& acc, const float* t, const f32x16& x, int lane) {
+  const float* b = t + lane * 4;
+  const f32x4 w0 = ld4(b), w1 = ld4(b + 256), w2 = ld4(b + 512), w3 = ld4(b + 768);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) acc = mfma32(w0[e], x[e], acc);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) acc = mfma32(w1[e], x[4 + e], acc);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) acc = mfma32(w2[e], x[8 + e], acc);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) acc = mfma32(w3[e], x[12 + e], acc);
+  // keep the compiler from hoisting the LDS reads of many tiles ahead (VGPR budget)
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+__global__ __launch_bounds__(DEC_NW * 64) void k_dec1(const float* __restrict__ proj, const float* __restrict__ mlp,
+                                                     stif_dec_tables tb, const float* __restrict__ tq,
+                                                     float* __restrict__ hrfeat, float* __restrict__ flow, int n,
+                                                     int h, int w, int HH, int WW) {
+  __shared__ __attribute__((aligned(16))) float wbuf[2 * SEG * T];
+  const int lane = threadIdx.x & 63, hf = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
+  float* const B0 = wbuf;
+  float* const B1 = wbuf + SEG * T;
+  const __amdgpu_buffer_rsrc_t rm = mlp_rsrc(mlp);
+  // segment 0: feat layer 1 (4 tiles); segments 1..8: feat layer 2 tile kt + layer 3 (0, kt), (1, kt)
+  dma_tiles<DEC_NW>(B0, rm, F_W1, 4, wv, lane);
   const long long total = (long long)n * HH * WW;
-  const long long p = ((long long)blockIdx.x * 4 + wv) * 32 + (lane & 31);
+  const long long p = ((long long)blockIdx.x * DEC_NW + wv) * 32 + (lane & 31);
   const bool valid = p < total;
   const long long pc = valid ? p : total - 1;
   const int item = (int)(pc / ((long long)HH * WW));
@@ -135,23 +163,40 @@ __global__ __launch_bounds__(256) void k_dec1(const float* __restrict__ proj, co
         for (int e = 0; e < 4; ++e) x0[ot][4 * v + e] = stif_sin(30.0f * z[e]);
       }
   }
+  auto seg_feat23 = [&](float* dst, int kt) {   // W2 rows kt (2 tiles), W3 (0, kt), (1, kt)
+    dma_tiles<DEC_NW>(dst, rm, F_W2 + kt * 2 * T, 2, wv, lane);
+    dma_tiles<DEC_NW>(dst + 2 * T, rm, F_W3 + kt * T, 1, wv, lane);
+    dma_tiles<DEC_NW>(dst + 3 * T, rm, F_W3 + (8 + kt) * T, 1, wv, lane);
+  };
+  lds_dma_barrier();
+  seg_feat23(B1, 0);
   // ---- layer 1: 64 -> 64
   f32x16 x1[2];
 #pragma unroll
   for (int ot = 0; ot < 2; ++ot) {
     f32x16 acc = f32x16{0};
-    mlp_acc<2>(acc, mlp + F_W1 + ot * 2 * T, x0, lane);
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) tile_mma(acc, B0 + (ot * 2 + kt) * T, x0[kt], lane);
     x1[ot] = bias_sin(acc, mlp + F_B1 + ot * 32, hf);
   }
   // ---- layer 2 (64 -> 256, sine) streamed into layer 3 (256 -> 64, linear)
   f32x16 hr[2] = {f32x16{0}, f32x16{0}};
 #pragma unroll 1
   for (int kt = 0; kt < 8; ++kt) {
+    lds_dma_barrier();
+    float* cur = (kt & 1) ? B0 : B1;
+    float* nxt = (kt & 1) ? B1 : B0;
+    if (kt < 7) seg_feat23(nxt, kt + 1);
+    else {   // prefetch flow layer 0 (4 tiles) + layer 1 (4 tiles)
+      dma_tiles<DEC_NW>(nxt, rm, L_W0, 4, wv, lane);
+      dma_tiles<DEC_NW>(nxt + 4 * T, rm, L_W1, 4, wv, lane);
+    }
     f32x16 acc = f32x16{0};
-    mlp_acc<2>(acc, mlp + F_W2 + kt * 2 * T, x1, lane);
-    f32x16 h2[1] = {bias_sin(acc, mlp + F_B2 + kt * 32, hf)};
-#pragma unroll
-    for (int ot = 0; ot < 2; ++ot) mlp_acc<1>(hr[ot], mlp + F_W3 + (ot * 8 + kt) * T, h2, lane);
+    tile_mma(acc, cur, x1[0], lane);
+    tile_mma(acc, cur + T, x1[1], lane);
+    const f32x16 h2 = bias_sin(acc, mlp + F_B2 + kt * 32, hf);
+    tile_mma(hr[0], cur + 2 * T, h2, lane);
+    tile_mma(hr[1], cur + 3 * T, h2, lane);
   }
 #pragma unroll
   for (int ot = 0; ot < 2; ++ot) hr[ot] = bias_add(hr[ot], mlp + F_B3 + ot * 32, hf);
@@ -187,42 +232,64 @@ __global__ __launch_bounds__(256) void k_dec1(const float* __restrict__ proj, co
         for (int e = 0; e < 4; ++e) z[ot][4 * v + e] += wt[e] * t + bb[e];
       }
   }
+  // flow layers 0/1 live in B1 (prefetched during the last feat segment)
+  lds_dma_barrier();
+  auto seg_flow23 = [&](float* dst, int kt) {   // W2 rows kt (2 tiles), W3 (kt)
+    dma_tiles<DEC_NW>(dst, rm, L_W2 + kt * 2 * T, 2, wv, lane);
+    dma_tiles<DEC_NW>(dst + 2 * T, rm, L_W3 + kt * T, 1, wv, lane);
+  };
+  seg_flow23(B0, 0);
 #pragma unroll
   for (int ot = 0; ot < 2; ++ot) {
-    mlp_acc<2>(z[ot], mlp + L_W0 + ot * 2 * T, hr, lane);
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) tile_mma(z[ot], B1 + (ot * 2 + kt) * T, hr[kt], lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r) z[ot][r] = stif_sin(30.0f * z[ot][r]);
   }
 #pragma unroll
   for (int ot = 0; ot < 2; ++ot) {
     f32x16 acc = f32x16{0};
-    mlp_acc<2>(acc, mlp + L_W1 + ot * 2 * T, z, lane);
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) tile_mma(acc, B1 + (4 + ot * 2 + kt) * T, z[kt], lane);
     x1[ot] = bias_sin(acc, mlp + L_B1 + ot * 32, hf);
   }
-  f32x16 fl[1] = {f32x16{0}};
+  f32x16 fl = f32x16{0};
 #pragma unroll 1
   for (int kt = 0; kt < 8; ++kt) {
+    lds_dma_barrier();
+    float* cur = (kt & 1) ? B1 : B0;
+    float* nxt = (kt & 1) ? B0 : B1;
+    if (kt < 7) seg_flow23(nxt, kt + 1);
     f32x16 acc = f32x16{0};
-    mlp_acc<2>(acc, mlp + L_W2 + kt * 2 * T, x1, lane);
-    f32x16 h2[1] = {bias_sin(acc, mlp + L_B2 + kt * 32, hf)};
-    mlp_acc<1>(fl[0], mlp + L_W3 + kt * T, h2, lane);
+    tile_mma(acc, cur, x1[0], lane);
+    tile_mma(acc, cur + T, x1[1], lane);
+    const f32x16 h2 = bias_sin(acc, mlp + L_B2 + kt * 32, hf);
+    tile_mma(fl, cur + 2 * T, h2, lane);
   }
   if (valid && hf == 0) {
     const f32x4 bb = ld4(mlp + L_B3);
     f32x4 s;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) s[e] = fl[0][e] + bb[e];
+    for (int e = 0; e < 4; ++e) s[e] = fl[e] + bb[e];
     st4(flow + (size_t)pc * 4, s);
   }
 }
 
-__global__ __launch_bounds__(256) void k_dec2(const float* __restrict__ proj, const float* __restrict__ mlp,
-                                              const float* __restrict__ hrfeat, const float* __restrict__ flow,
-                                              stif_dec_tables tb, const float* __restrict__ tq,
-                                              float* __restrict__ out, int n, int h, int w, int HH, int WW) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, hf = lane >> 5;
+__global__ __launch_bounds__(DEC2_NW * 64) void k_dec2(const float* __restrict__ proj, const float* __restrict__ mlp,
+                                                     const float* __restrict__ hrfeat, const float* __restrict__ flow,
+                                                     stif_dec_tables tb, const float* __restrict__ tq,
+                                                     float* __restrict__ out, int n, int h, int w, int HH, int WW) {
+  __shared__ __attribute__((aligned(16))) float wbuf[2 * SEG * T];
+  const int lane = threadIdx.x & 63, hf = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
+  float* const B0 = wbuf;
+  float* const B1 = wbuf + SEG * T;
+  const __amdgpu_buffer_rsrc_t rm = mlp_rsrc(mlp);
+  // segments: [L0: 8 tiles] [L1: 4] then per layer-2 tile kt: [W2 rows kt (2) + W3 column kt (8)],
+  // then [W4: 8]
+  dma_tiles<DEC2_NW>(B0, rm, E_W0, 8, wv, lane);
   const long long total = (long long)n * HH * WW;
-  const long long p = ((long long)blockIdx.x * 4 + wv) * 32 + (lane & 31);
+  const long long p = ((long long)blockIdx.x * DEC2_NW + wv) * 32 + (lane & 31);
   const bool valid = p < total;
   const long long pc = valid ? p : total - 1;
   const int item = (int)(pc / ((long long)HH * WW));
@@ -242,58 +309,90 @@ __global__ __launch_bounds__(256) void k_dec2(const float* __restrict__ proj, co
   const float g2x = fminf(fmaxf(bx + fv[2] / dx, lo), hi), g2y = fminf(fmaxf(by + fv[3] / dy, lo), hi);
 
   // ---- encode_imnet layer 0: W[:, :128] . [q_feat1 | q_feat2] + P3(grid1) + P4(grid2) + w_t t + b
-  f32x16 q[4];
-  gather64(q, HRF, 64, 0, bilin(g1x, g1y, WW, HH), hf);
-  gather64(q + 2, HRF, 64, 0, bilin(g2x, g2y, WW, HH), hf);
-  f32x16 z[2], z2[2];
-  gather64(z, P, PROJ_C, 128, bilin(g1x, g1y, w, h), hf);
-  gather64(z2, P, PROJ_C, 192, bilin(g2x, g2y, w, h), hf);
+  f32x16 x0[2];
+  {
+    // four 64-channel bilinear gathers (32 x 16-B loads per lane each); the compiler barriers
+    // keep it from hoisting all 128 loads at once (VGPR budget)
+    f32x16 q[4];
+    gather64(q, HRF, 64, 0, bilin(g1x, g1y, WW, HH), hf);
+    asm volatile("" ::: "memory");
+    gather64(q + 2, HRF, 64, 0, bilin(g2x, g2y, WW, HH), hf);
+    asm volatile("" ::: "memory");
+    f32x16 z[2], z2[2];
+    gather64(z, P, PROJ_C, 128, bilin(g1x, g1y, w, h), hf);
+    asm volatile("" ::: "memory");
+    gather64(z2, P, PROJ_C, 192, bilin(g2x, g2y, w, h), hf);
 #pragma unroll
-  for (int ot = 0; ot < 2; ++ot)
+    for (int ot = 0; ot < 2; ++ot)
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int f = ot * 32 + 8 * v + 4 * hf;
-      const f32x4 wt = ld4(mlp + E_WT + f), bb = ld4(mlp + E_B0 + f);
+      for (int v = 0; v < 4; ++v) {
+        const int f = ot * 32 + 8 * v + 4 * hf;
+        const f32x4 wt = ld4(mlp + E_WT + f), bb = ld4(mlp + E_B0 + f);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) z[ot][4 * v + e] += z2[ot][4 * v + e] + wt[e] * t + bb[e];
+        for (int e = 0; e < 4; ++e) z[ot][4 * v + e] += z2[ot][4 * v + e] + wt[e] * t + bb[e];
+      }
+    lds_dma_barrier();
+    dma_tiles<DEC2_NW>(B1, rm, E_W1, 4, wv, lane);
+#pragma unroll
+    for (int ot = 0; ot < 2; ++ot) {
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) tile_mma(z[ot], B0 + (ot * 4 + kt) * T, q[kt], lane);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) x0[ot][r] = stif_sin(30.0f * z[ot][r]);
     }
-#pragma unroll
-  for (int ot = 0; ot < 2; ++ot) {
-    mlp_acc<4>(z[ot], mlp + E_W0 + ot * 4 * T, q, lane);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) z[ot][r] = stif_sin(30.0f * z[ot][r]);
   }
+  lds_dma_barrier();
+  auto seg_l23_first = [&](float* dst) {
+    dma_tiles<DEC2_NW>(dst, rm, E_W2, 2, wv, lane);
+#pragma unroll
+    for (int ot = 0; ot < 8; ++ot) dma_tiles<DEC2_NW>(dst + (2 + ot) * T, rm, E_W3 + ot * 8 * T, 1, wv, lane);
+  };
+  seg_l23_first(B0);
   f32x16 x1[2];
 #pragma unroll
   for (int ot = 0; ot < 2; ++ot) {
     f32x16 acc = f32x16{0};
-    mlp_acc<2>(acc, mlp + E_W1 + ot * 2 * T, z, lane);
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) tile_mma(acc, B1 + (ot * 2 + kt) * T, x0[kt], lane);
     x1[ot] = bias_sin(acc, mlp + E_B1 + ot * 32, hf);
   }
-  // layer 2 (64 -> 256, sine) streamed into layer 3 (256 -> 256) accumulators
+  // layer 2 (64 -> 256, sine) streamed tile by tile into the 8 accumulators of layer 3 (256 -> 256):
+  // segment kt = W2 rows of tile kt (2 tiles) + column kt of W3 (8 tiles)
+  auto seg_l23 = [&](float* dst, int kt) {
+    dma_tiles<DEC2_NW>(dst, rm, E_W2 + kt * 2 * T, 2, wv, lane);
+#pragma unroll
+    for (int ot = 0; ot < 8; ++ot) dma_tiles<DEC2_NW>(dst + (2 + ot) * T, rm, E_W3 + (ot * 8 + kt) * T, 1, wv, lane);
+  };
   f32x16 a3[8];
 #pragma unroll
   for (int ot = 0; ot < 8; ++ot) a3[ot] = f32x16{0};
 #pragma unroll 1
   for (int kt = 0; kt < 8; ++kt) {
+    lds_dma_barrier();
+    float* cur = (kt & 1) ? B1 : B0;
+    float* nxt = (kt & 1) ? B0 : B1;
+    if (kt < 7) seg_l23(nxt, kt + 1);
+    else dma_tiles<DEC2_NW>(nxt, rm, E_W4, 8, wv, lane);
     f32x16 acc = f32x16{0};
-    mlp_acc<2>(acc, mlp + E_W2 + kt * 2 * T, x1, lane);
-    f32x16 h2[1] = {bias_sin(acc, mlp + E_B2 + kt * 32, hf)};
+    tile_mma(acc, cur, x1[0], lane);
+    tile_mma(acc, cur + T, x1[1], lane);
+    const f32x16 h2 = bias_sin(acc, mlp + E_B2 + kt * 32, hf);
 #pragma unroll
-    for (int ot = 0; ot < 8; ++ot) mlp_acc<1>(a3[ot], mlp + E_W3 + (ot * 8 + kt) * T, h2, lane);
+    for (int ot = 0; ot < 8; ++ot) tile_mma(a3[ot], cur + (2 + ot) * T, h2, lane);
   }
-  // layer 3 sine streamed into layer 4 (256 -> 3, linear)
-  f32x16 o4[1] = {f32x16{0}};
+  // layer 3 sine streamed into layer 4 (256 -> 3, linear); W4 sits in B0 (kt = 7 prefetch)
+  lds_dma_barrier();
+  f32x16 o4 = f32x16{0};
 #pragma unroll
   for (int kt = 0; kt < 8; ++kt) {
-    f32x16 h3[1] = {bias_sin(a3[kt], mlp + E_B3 + kt * 32, hf)};
-    mlp_acc<1>(o4[0], mlp + E_W4 + kt * T, h3, lane);
+    const f32x16 h3 = bias_sin(a3[kt], mlp + E_B3 + kt * 32, hf);
+    tile_mma(o4, B0 + kt * T, h3, lane);
   }
   if (valid && hf == 0) {
     const size_t plane = (size_t)HH * WW;
     float* o = out + (size_t)item * 3 * plane + (size_t)py * WW + px;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) o[c * plane] = o4[0][c] + mlp[E_B4 + c];
+    for (int c = 0; c < 3; ++c) o[c * plane] = o4[c] + mlp[E_B4 + c];
   }
 }
 
@@ -344,8 +443,8 @@ extern "C" int stif_dec_stage1(const float* proj, const float* mlp, const stif_d
   if (!proj || !mlp || !tables_ok(tab) || !t || !hrfeat || !flow || n < 1 || h < 1 || w < 1 || HH < 2 || WW < 2)
     return stif_fail(STIF_E_INVALID, "stif_dec_stage1: bad arguments");
   const long long total = (long long)n * HH * WW;
-  const long long blocks = (total + 127) / 128;
-  hipLaunchKernelGGL(k_dec1, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, proj, mlp, *tab, t, hrfeat,
+  const long long blocks = (total + DEC_NW * 32 - 1) / (DEC_NW * 32);
+  hipLaunchKernelGGL(k_dec1, dim3((unsigned)blocks), dim3(DEC_NW * 64), 0, (hipStream_t)stream, proj, mlp, *tab, t, hrfeat,
                      flow, n, h, w, HH, WW);
   return stif_check_launch("stif_dec_stage1");
 }
@@ -357,8 +456,8 @@ extern "C" int stif_dec_stage2(const float* proj, const float* mlp, const float*
       WW < 2)
     return stif_fail(STIF_E_INVALID, "stif_dec_stage2: bad arguments");
   const long long total = (long long)n * HH * WW;
-  const long long blocks = (total + 127) / 128;
-  hipLaunchKernelGGL(k_dec2, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, proj, mlp, hrfeat, flow,
+  const long long blocks = (total + DEC2_NW * 32 - 1) / (DEC2_NW * 32);
+  hipLaunchKernelGGL(k_dec2, dim3((unsigned)blocks), dim3(DEC2_NW * 64), 0, (hipStream_t)stream, proj, mlp, hrfeat, flow,
                      *tab, t, out, n, h, w, HH, WW);
   return stif_check_launch("stif_dec_stage2");
 }

@@ -58,3 +58,11 @@ STIF_DEV void tile_to_lds(float* blk, const f32x16& v, int lane) {
   }
 }
 STIF_DEV f32x4 lds_row4(const float* blk, int px, int c4) { return ld4(blk + px * 32 + ((c4 ^ (px & 3)) << 2)); }
+
+// Barrier for LDS filled by LDS-DMA (buffer_load/global_load ... lds): the DMA completes
+// asynchronously on each wave's vmcnt and gfx950's back-off barrier does not drain it, so every
+// wave waits for its own transfers before the workgroup barrier that publishes them.
+STIF_DEV void lds_dma_barrier() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
