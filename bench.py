@@ -183,7 +183,8 @@ def main():
     if rank == 0:
         achieved = avg_flops / (avg_ms * 1e-3) / 1e12 if avg_ms else 0.0
         traffic = None
-        if os.path.exists(args.traffic):
+        # the committed PMC summary was measured at C1 (per-launch bytes of that configuration)
+        if args.config == "c1" and os.path.exists(args.traffic):
             try:
                 traffic = json.load(open(args.traffic)).get("hbm_bytes_per_launch")
             except Exception:
