@@ -31,6 +31,24 @@ CONFIGS = {
     "c2": (7, 540, 960, 4, [0.25, 0.5, 0.75]),
 }
 FP32_PEAK_TFLOPS = 157.3   # MI355X dense fp32 MFMA (MI355X_MICROARCH.md, chip-level parameters)
+WINO_GAIN = 36.0 / 16.0    # F(2x2,3x3): 16 transformed-domain MACs per 36 direct MACs
+EPI_NAMES = {0: "NONE", 1: "LRELU", 2: "RELU", 3: "RES", 4: "OFFMASK", 5: "LSTM"}
+
+
+def kernel_desc(kind):
+    """(kernel name as rocprof shows it, description, peak in algorithmic TFLOP/s) of a launch kind."""
+    if kind[0] == "wino":
+        _, ks, s, epi, in1, cout = kind
+        return (f"k_wino<{in1}, {epi}>", f"3x3 {64 * (2 if in1 else 1)}->{cout} conv, EPI_{EPI_NAMES[epi]}, "
+                f"Winograd F(2x2,3x3) on fp32 MFMA; algorithmic = direct-conv FLOPs, peak = fp32 MFMA peak x 36/16",
+                FP32_PEAK_TFLOPS * WINO_GAIN)
+    if kind[0] == "conv":
+        _, ks, s, epi, in1, cout = kind
+        return (f"k_conv<{ks}, {s}, ...>", f"{ks}x{ks}/s{s} conv -> {cout}, in1 mode {in1}, EPI_{EPI_NAMES[epi]}, "
+                "direct implicit GEMM on fp32 MFMA", FP32_PEAK_TFLOPS)
+    if kind[0] == "dcn":
+        return ("k_dcn", "fused modulated deformable conv", FP32_PEAK_TFLOPS)
+    return (f"k_{kind[0]}", "SIREN decoder stage", FP32_PEAK_TFLOPS)
 
 
 class KernelTimer:
@@ -61,14 +79,22 @@ class KernelTimer:
             self.rec.append(self._cur)
             self._cur = None
 
-    def report(self):
-        """per-kind launches / avg us / TFLOP/s (all-kinds mode)"""
+    def per_kind(self):
         agg = {}
         for (a, b, f), k in zip(self.rec, self.kinds):
             d = agg.setdefault(k, [0, 0.0, 0.0])
             d[0] += 1
             d[1] += a.elapsed_time(b)
             d[2] += f
+        return agg
+
+    def dominant(self):
+        """the launch kind with the largest total time"""
+        return max(self.per_kind().items(), key=lambda kv: kv[1][1])[0]
+
+    def report(self):
+        """per-kind launches / avg us / TFLOP/s (all-kinds mode)"""
+        agg = self.per_kind()
         for k, (nl, ms, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
             print(f"  {str(k):40s} {nl:5d} launches {ms / nl * 1e3:9.1f} us avg {fl / (ms * 1e-3) / 1e12:7.1f} TFLOP/s"
                   f"  {ms:8.2f} ms total", file=sys.stderr)
@@ -147,10 +173,15 @@ def main():
         return model.decoding(tq)
 
     with torch.no_grad():
-        for _ in range(args.warmup):
+        # warm-up; the last warm-up step times every launch to find the dominant kernel
+        probe = KernelTimer(None)
+        for i in range(max(1, args.warmup)):
+            stif.ops.TRACE = probe if i == max(1, args.warmup) - 1 else None
             step()
+        stif.ops.TRACE = None
         torch.cuda.synchronize()
-        timer = KernelTimer(("conv", 3, 1, stif._lib.EPI_RES, 0, 64))
+        dom = probe.dominant()
+        timer = KernelTimer(dom)
         stif.ops.TRACE = timer
         if dist:
             td.barrier()
@@ -182,11 +213,14 @@ def main():
     value = world * out_pix * args.steps / elapsed / 1e6
     if rank == 0:
         achieved = avg_flops / (avg_ms * 1e-3) / 1e12 if avg_ms else 0.0
+        kname, kdesc, peak = kernel_desc(dom)
         traffic = None
         # the committed PMC summary was measured at C1 (per-launch bytes of that configuration)
         if args.config == "c1" and os.path.exists(args.traffic):
             try:
-                traffic = json.load(open(args.traffic)).get("hbm_bytes_per_launch")
+                pmc = json.load(open(args.traffic))
+                if kname.split("<")[0] in pmc.get("kernel", "") and pmc.get("kind") == list(dom):
+                    traffic = pmc.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
         res = {
@@ -205,9 +239,9 @@ def main():
             "config": {"workload": f"{nframes}x3x{H}x{W} window ({pairs} pairs), {scale}x spatial, t={times}",
                        "frames_per_gpu": nframes, "lr_hw": [H, W], "scale": scale, "times": times,
                        "parallelism": f"pair-sharded x{world} (1-frame halo, no collective)"},
-            "roofline": {"bound": "mfma", "kernel": "k_conv<3,1,2,2,0,EPI_RES> (3x3 64->64 conv + residual)",
-                         "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+            "roofline": {"bound": "mfma", "kernel": f"{kname} ({kdesc})", "kind": list(dom),
+                         "achieved": round(achieved, 3), "peak": round(peak, 2), "unit": "TFLOP/s",
+                         "frac": round(achieved / peak, 4), "traffic": traffic,
                          "launches": n_launch, "avg_launch_us": round(avg_ms * 1e3, 2),
                          "flops_per_launch": avg_flops},
         }

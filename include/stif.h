@@ -73,6 +73,11 @@ typedef struct {
 
 int stif_conv2d_nhwc(const stif_conv_args* args, void* stream);
 
+/* The same operator for 3x3 / stride 1 / 'same' shapes by Winograd F(2x2,3x3) on fp32 MFMA
+ * (2.25x fewer multiply-adds; all arithmetic fp32): weights packed with STIF_PACK_WINO,
+ * cout a multiple of 64, in1_mode 0 or 1, epi NONE / LRELU / RELU / RES. */
+int stif_conv3x3_wino(const stif_conv_args* args, void* stream);
+
 /* conv_first (3 -> 64, 3x3) + LeakyReLU, reading NCHW RGB frames [n,3,h,w]
  * (Sakuya_arch_test.py:318) and writing NHWC [n,h,w,64]. w: [64,3,3,3] as in the state dict. */
 int stif_conv_first(const float* x_nchw, const float* w, const float* b, float* out,
@@ -143,7 +148,7 @@ int stif_dec_stage2(const float* proj, const float* mlp, const float* hrfeat, co
                     int n, int h, int w, int HH, int WW, void* stream);
 
 /* ---- host-side weight packing (pure CPU, callable without a GPU) ---- */
-enum { STIF_PACK_PLAIN = 0, STIF_PACK_OFFMASK = 1, STIF_PACK_LSTM = 2 };
+enum { STIF_PACK_PLAIN = 0, STIF_PACK_OFFMASK = 1, STIF_PACK_LSTM = 2, STIF_PACK_WINO = 3 };
 
 /* Size in floats of a packed conv weight / bias for a packing mode. */
 size_t stif_conv_weight_floats(int cout, int cin, int ks, int mode);
@@ -153,7 +158,11 @@ size_t stif_conv_bias_floats(int cout, int mode);
  * contiguous so the kernel copies them to LDS with LDS-DMA; a slice is 32*NT output channels
  * (NT = 7 for OFFMASK, 4 for LSTM, 2 otherwise), cout padded to a whole slice with zeros, and
  * output rows permuted per `mode` (OFFMASK: [group][tap][dy, dx, mask]; LSTM: gates i,f,o,g
- * of 32 hidden channels per slice). */
+ * of 32 hidden channels per slice).
+ * STIF_PACK_WINO (3x3 only, for stif_conv3x3_wino): the Winograd-domain weights U = G g G^T
+ * (F(2x2,3x3), computed in double) as [cout/64][cin/8][i 4][j 4][nt 2][lane 64][4], lane l of
+ * (i, j, nt) holding U[i][j] of cout slice*64 + nt*32 + (l & 31), input channel
+ * chunk*8 + 4(l >> 5) + e; cout padded to a multiple of 64. */
 int stif_pack_conv_weight(const float* w_oihw, const float* b, int cout, int cin, int ks, int mode,
                           float* w_dst, float* b_dst);
 

@@ -12,7 +12,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libstif_hip
 
 MAXG = 8
 EPI_NONE, EPI_LRELU, EPI_RELU, EPI_RES, EPI_OFFMASK, EPI_LSTM = range(6)
-PACK_PLAIN, PACK_OFFMASK, PACK_LSTM = range(3)
+PACK_PLAIN, PACK_OFFMASK, PACK_LSTM, PACK_WINO = range(4)
 
 _P = C.c_void_p
 _PA = _P * MAXG
@@ -47,6 +47,7 @@ class DecTables(C.Structure):
 EXPORTS = {
     # name: (restype, argtypes)
     "stif_conv2d_nhwc": (C.c_int, [C.POINTER(ConvArgs), _P]),
+    "stif_conv3x3_wino": (C.c_int, [C.POINTER(ConvArgs), _P]),
     "stif_conv_first": (C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, C.c_int, _P]),
     "stif_dcn_nhwc": (C.c_int, [C.POINTER(DcnArgs), _P]),
     "stif_dcn_v2_workspace_size": (C.c_size_t, [C.c_int] * 14),

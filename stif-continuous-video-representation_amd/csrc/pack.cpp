@@ -13,6 +13,17 @@ extern int stif_fail(int code, const char* msg);
 namespace {
 
 int round32(int x) { return (x + 31) & ~31; }
+int round64(int x) { return (x + 63) & ~63; }
+
+// Winograd F(2x2, 3x3) weight transform U = G g G^T (wino.hip), in double
+void wino_u(const float* g, double u[4][4]) {
+  static const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+  double t[4][3];
+  for (int a = 0; a < 4; ++a)
+    for (int q = 0; q < 3; ++q) t[a][q] = G[a][0] * g[q] + G[a][1] * g[3 + q] + G[a][2] * g[6 + q];
+  for (int a = 0; a < 4; ++a)
+    for (int b = 0; b < 4; ++b) u[a][b] = t[a][0] * G[b][0] + t[a][1] * G[b][1] + t[a][2] * G[b][2];
+}
 
 // 32-wide N-tiles per workgroup slice of stif_conv2d_nhwc for a packing mode (conv.hip dispatch)
 int slice_tiles(int mode) { return mode == STIF_PACK_OFFMASK ? 7 : (mode == STIF_PACK_LSTM ? 4 : 2); }
@@ -71,10 +82,38 @@ void column(float* dst, const float* W, int ld, int rows, int col) {
 }  // namespace
 
 extern "C" size_t stif_conv_weight_floats(int cout, int cin, int ks, int mode) {
+  if (mode == STIF_PACK_WINO) return (size_t)round64(cout) * cin * 16;
   return (size_t)cout_padded(cout, mode) * cin * ks * ks;
 }
 
-extern "C" size_t stif_conv_bias_floats(int cout, int mode) { return (size_t)cout_padded(cout, mode); }
+extern "C" size_t stif_conv_bias_floats(int cout, int mode) {
+  return mode == STIF_PACK_WINO ? (size_t)round64(cout) : (size_t)cout_padded(cout, mode);
+}
+
+namespace {
+// [slice][chunk][i][j][nt][lane][4]: U[4i+j] of cout slice*64 + nt*32 + (lane & 31), input channel
+// chunk*8 + 4*(lane >> 5) + e -- the B fragments wave i of stif_conv3x3_wino loads per 8-channel chunk
+int pack_wino(const float* w, const float* b, int cout, int cin, float* w_dst, float* b_dst) {
+  const int cp = round64(cout), NS = cp / 64, NC = cin / 8;
+  for (int s = 0; s < NS; ++s)
+    for (int nt = 0; nt < 2; ++nt)
+      for (int l = 0; l < 64; ++l) {
+        const int co = s * 64 + nt * 32 + (l & 31);
+        for (int c = 0; c < NC; ++c)
+          for (int e = 0; e < 4; ++e) {
+            const int ci = c * 8 + 4 * (l >> 5) + e;
+            double u[4][4] = {{0}};
+            if (co < cout) wino_u(w + ((size_t)co * cin + ci) * 9, u);
+            for (int i = 0; i < 4; ++i)
+              for (int j = 0; j < 4; ++j)
+                w_dst[((((((size_t)s * NC + c) * 4 + i) * 4 + j) * 2 + nt) * 64 + l) * 4 + e] = (float)u[i][j];
+          }
+      }
+  if (b_dst)
+    for (int j = 0; j < cp; ++j) b_dst[j] = (j < cout && b) ? b[j] : 0.f;
+  return STIF_OK;
+}
+}  // namespace
 
 extern "C" int stif_pack_conv_weight(const float* w, const float* b, int cout, int cin, int ks, int mode,
                                      float* w_dst, float* b_dst) {
@@ -82,6 +121,10 @@ extern "C" int stif_pack_conv_weight(const float* w, const float* b, int cout, i
     return stif_fail(STIF_E_INVALID, "stif_pack_conv_weight: bad arguments");
   if (mode == STIF_PACK_OFFMASK && cout != 216) return stif_fail(STIF_E_INVALID, "offmask pack needs cout=216");
   if (mode == STIF_PACK_LSTM && cout != 256) return stif_fail(STIF_E_INVALID, "lstm pack needs cout=256");
+  if (mode == STIF_PACK_WINO) {
+    if (ks != 3) return stif_fail(STIF_E_INVALID, "winograd pack needs a 3x3 kernel");
+    return pack_wino(w, b, cout, cin, w_dst, b_dst);
+  }
   // layout [slice][chunk][tap][nt][lane][4]: the B fragments of one (slice, chunk) are one
   // contiguous block, copied to LDS by LDS-DMA; lane l of N-tile nt holds cout
   // slice*NJ + nt*32 + (l & 31), input channels chunk*8 + 4*(l >> 5) + e.

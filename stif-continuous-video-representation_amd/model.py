@@ -35,7 +35,7 @@ def _np(v):
 class LunaTokis:
     """STIF LunaTokis (Sakuya_arch_test.py:268) on MI355X."""
 
-    def __init__(self, nf=64, nframes=3, groups=8, front_RBs=5, back_RBs=10, device="cuda"):
+    def __init__(self, nf=64, nframes=3, groups=8, front_RBs=5, back_RBs=10, device="cuda", winograd=True):
         if nf != 64 or groups != 8:
             raise ValueError("the gfx950 kernels implement nf=64, groups=8 (the shipped STIF configuration)")
         self.nf, self.groups = nf, groups
@@ -50,6 +50,8 @@ class LunaTokis:
         self.inp = None
         self._tables = {}
         self.training = False
+        # 3x3 convs by Winograd F(2x2,3x3) where the shape allows (fp32 throughout); False = direct
+        self.winograd = bool(winograd)
 
     # ------------------------------------------------------------------ nn.Module-like API
     def eval(self):
@@ -116,13 +118,20 @@ class LunaTokis:
         def conv(name, mode=L.PACK_PLAIN):
             lay[name] = ops.pack_conv(h[name + ".weight"], h[name + ".bias"], mode, dev)
 
+        # 3x3 / stride-1 / 64-cout convs whose second input (if any) is at full resolution run by
+        # Winograd F(2x2,3x3) (stif_conv3x3_wino); the x2-upsampled-input, strided, 1x1,
+        # offset/mask and ConvLSTM convs keep the direct kernel.
+        wino = L.PACK_WINO if self.winograd else L.PACK_PLAIN
+
         lay["conv_first.w"] = torch.from_numpy(h["conv_first.weight"]).to(dev)
         lay["conv_first.b"] = torch.from_numpy(h["conv_first.bias"]).to(dev)
         for i in range(self.front_RBs):
-            conv(f"feature_extraction.{i}.conv1")
-            conv(f"feature_extraction.{i}.conv2")
-        for n in ("fea_L2_conv1", "fea_L2_conv2", "fea_L3_conv1", "fea_L3_conv2"):
+            conv(f"feature_extraction.{i}.conv1", wino)
+            conv(f"feature_extraction.{i}.conv2", wino)
+        for n in ("fea_L2_conv1", "fea_L3_conv1"):
             conv(n)
+        for n in ("fea_L2_conv2", "fea_L3_conv2"):
+            conv(n, wino)
 
         def pcd(prefix):
             for d in (1, 2):
@@ -131,20 +140,24 @@ class LunaTokis:
                     if cin is None:
                         conv(n)
                         conv(n + ".conv_offset_mask", L.PACK_OFFMASK)
+                    elif ln in ("L2_offset_conv2", "L2_fea_conv", "L1_offset_conv2", "L1_fea_conv"):
+                        conv(n)                       # second input is x2-upsampled
                     else:
-                        conv(n)
+                        conv(n, wino)
 
         pcd("pcd_align.")
         conv("fusion")
         conv("ConvBLSTM.forward_net.cell_list.0.conv", L.PACK_LSTM)
         for p in ("ConvBLSTM.forward_net.pcd_h.", "ConvBLSTM.forward_net.pcd_c."):
-            for n in ("fea_L2_conv1", "fea_L2_conv2", "fea_L3_conv1", "fea_L3_conv2", "fusion"):
+            for n in ("fea_L2_conv1", "fea_L3_conv1", "fusion"):
                 conv(p + n)
+            for n in ("fea_L2_conv2", "fea_L3_conv2"):
+                conv(p + n, wino)
             pcd(p + "pcd_align.")
         conv("ConvBLSTM.conv_1x1")
         for i in range(self.back_RBs):
-            conv(f"recon_trunk.{i}.conv1")
-            conv(f"recon_trunk.{i}.conv2")
+            conv(f"recon_trunk.{i}.conv1", wino)
+            conv(f"recon_trunk.{i}.conv2", wino)
         # decoder
         lib = L.lib()
         wd = np.empty(lib.stif_dec_proj_floats(), np.float32)

@@ -105,11 +105,18 @@ def conv2d(groups, *, epi=L.EPI_NONE, in1_mode=0, in1_scale=1.0, stride=None):
     a.H, a.W, a.C0, a.C1 = H, W, C0, C1
     a.in1_mode, a.in1_scale = in1_mode, in1_scale
     a.Ho, a.Wo, a.cout, a.ks, a.stride, a.epi = Ho, Wo, lay.cout, ks, stride, epi
+    wino = lay.mode == L.PACK_WINO
+    if any((g["layer"].mode == L.PACK_WINO) != wino for g in groups):
+        raise ValueError("conv2d: groups mix Winograd and direct packings")
     tr = TRACE
     if tr is not None:
-        tr.begin(("conv", ks, stride, epi, in1_mode, lay.cout),
+        # algorithmic (direct-convolution) FLOPs, whichever algorithm runs
+        tr.begin(("wino" if wino else "conv", ks, stride, epi, in1_mode, lay.cout),
                  2.0 * lay.cout * (C0 + C1) * ks * ks * Ho * Wo * nitems * len(groups))
-    L.check(L.lib().stif_conv2d_nhwc(C.byref(a), _stream()), "stif_conv2d_nhwc")
+    if wino:
+        L.check(L.lib().stif_conv3x3_wino(C.byref(a), _stream()), "stif_conv3x3_wino")
+    else:
+        L.check(L.lib().stif_conv2d_nhwc(C.byref(a), _stream()), "stif_conv2d_nhwc")
     if tr is not None:
         tr.end()
 

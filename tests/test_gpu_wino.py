@@ -1,0 +1,113 @@
+"""Winograd F(2x2,3x3) conv path (stif_conv3x3_wino) against the CPU oracle's direct conv."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import stif_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5   # relative to max |ref|, same bar as the direct conv kernels
+
+
+def relmax(a, b):
+    return float(np.abs(np.asarray(a, np.float64) - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def nhwc(x):
+    return torch.from_numpy(np.ascontiguousarray(np.asarray(x, np.float32).transpose(0, 2, 3, 1))).cuda()
+
+
+def to_nchw(t):
+    return t.detach().cpu().numpy().transpose(0, 3, 1, 2)
+
+
+def rnd(*shape, seed=0, scale=1.0):
+    return (np.random.default_rng(seed).standard_normal(shape) * scale).astype(np.float32)
+
+
+@pytest.mark.parametrize("epi", ["none", "lrelu", "relu", "res"])
+@pytest.mark.parametrize("hw", [(13, 37), (8, 32), (33, 70), (4, 4)])
+def test_wino_conv3x3(stif, epi, hw):
+    L, ops = stif._lib, stif.ops
+    H, W = hw
+    x = rnd(3, 64, H, W, seed=1)
+    w = rnd(64, 64, 3, 3, seed=2, scale=0.05)
+    b = rnd(64, seed=3)
+    r = rnd(3, 64, H, W, seed=4)
+    ref = O.conv2d(x, w, b)
+    e = dict(none=L.EPI_NONE, lrelu=L.EPI_LRELU, relu=L.EPI_RELU, res=L.EPI_RES)[epi]
+    ref = {"lrelu": O.lrelu, "relu": O.relu}.get(epi, lambda v: v)(ref)
+    if epi == "res":
+        ref = ref + r
+    out = torch.empty(3, H, W, 64, device="cuda")
+    layer = ops.pack_conv(w, b, L.PACK_WINO)
+    ops.conv2d([dict(layer=layer, in0=nhwc(x), out=out, res=nhwc(r) if epi == "res" else None)], epi=e)
+    assert relmax(to_nchw(out), ref) < RTOL
+
+
+def test_wino_residual_in_place(stif):
+    """out == res (the ResidualBlock_noBN in-place update the model uses)."""
+    L, ops = stif._lib, stif.ops
+    x = rnd(2, 64, 16, 64, seed=5)
+    t = rnd(2, 64, 16, 64, seed=6)
+    w = rnd(64, 64, 3, 3, seed=7, scale=0.05)
+    b = rnd(64, seed=8)
+    xd = nhwc(x)
+    ops.conv2d([dict(layer=ops.pack_conv(w, b, L.PACK_WINO), in0=nhwc(t), out=xd, res=xd)], epi=L.EPI_RES)
+    assert relmax(to_nchw(xd), x + O.conv2d(t, w, b)) < RTOL
+
+
+@pytest.mark.parametrize("cin1", [64, 32])
+def test_wino_two_inputs_groups(stif, cin1):
+    """cat(in0, in1) input (PCD offset convs) in two weight groups over strided item views."""
+    L, ops = stif._lib, stif.ops
+    H, W = 12, 40
+    fr = rnd(4, 64, H, W, seed=9)
+    f1n = fr[0::2]
+    f2n = fr[1::2, :cin1]
+    wa, wb = rnd(64, 64 + cin1, 3, 3, seed=10, scale=0.04), rnd(64, 64 + cin1, 3, 3, seed=11, scale=0.04)
+    ba, bb = rnd(64, seed=12), rnd(64, seed=13)
+    t = nhwc(fr)
+    in1 = t[1::2, :, :, :cin1].contiguous() if cin1 != 64 else t[1::2]
+    out = torch.empty(2, 2, H, W, 64, device="cuda")
+    ops.conv2d([dict(layer=ops.pack_conv(wa, ba, L.PACK_WINO), in0=t[0::2], in1=in1, out=out[0]),
+                dict(layer=ops.pack_conv(wb, bb, L.PACK_WINO), in0=t[0::2], in1=in1, out=out[1])],
+               epi=L.EPI_LRELU, in1_mode=1)
+    cat = np.concatenate([f1n, f2n], 1)
+    assert relmax(to_nchw(out[0]), O.lrelu(O.conv2d(cat, wa, ba))) < RTOL
+    assert relmax(to_nchw(out[1]), O.lrelu(O.conv2d(cat, wb, bb))) < RTOL
+
+
+def test_wino_multi_slice(stif):
+    L, ops = stif._lib, stif.ops
+    x = rnd(1, 128, 10, 36, seed=14)
+    w = rnd(128, 128, 3, 3, seed=15, scale=0.03)
+    b = rnd(128, seed=16)
+    out = torch.empty(1, 10, 36, 128, device="cuda")
+    ops.conv2d([dict(layer=ops.pack_conv(w, b, L.PACK_WINO), in0=nhwc(x), out=out)])
+    assert relmax(to_nchw(out), O.conv2d(x, w, b)) < RTOL
+
+
+def test_wino_matches_direct_kernel(stif):
+    """Winograd vs the direct implicit-GEMM kernel on the trunk shape: both fp32, both ~1e-7."""
+    L, ops = stif._lib, stif.ops
+    x = rnd(2, 64, 32, 64, seed=17)
+    w = rnd(64, 64, 3, 3, seed=18, scale=0.05)
+    b = rnd(64, seed=19)
+    o1 = torch.empty(2, 32, 64, 64, device="cuda")
+    o2 = torch.empty_like(o1)
+    ops.conv2d([dict(layer=ops.pack_conv(w, b, L.PACK_WINO), in0=nhwc(x), out=o1)], epi=L.EPI_RELU)
+    ops.conv2d([dict(layer=ops.pack_conv(w, b), in0=nhwc(x), out=o2)], epi=L.EPI_RELU)
+    ref = O.relu(O.conv2d(x, w, b))
+    e1, e2 = relmax(to_nchw(o1), ref), relmax(to_nchw(o2), ref)
+    assert e1 < RTOL and e2 < RTOL, (e1, e2)
+
+
+def test_wino_rejects_bad_shapes(stif):
+    L, ops = stif._lib, stif.ops
+    w = rnd(64, 64, 3, 3)
+    lay = ops.pack_conv(w, rnd(64), L.PACK_WINO)
+    x = torch.zeros(1, 8, 8, 64, device="cuda")
+    with pytest.raises(Exception):
+        ops.conv2d([dict(layer=lay, in0=x, out=torch.empty(1, 4, 4, 64, device="cuda"))], stride=2)

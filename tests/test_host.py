@@ -145,3 +145,26 @@ def test_load_state_dict_contract(stif, sd):
     back = m.state_dict()
     assert list(back.keys()) == list(sd.keys())
     assert np.array_equal(back["recon_trunk.39.conv2.weight"].numpy(), sd["recon_trunk.39.conv2.weight"])
+
+
+def test_pack_wino_layout(stif):
+    """STIF_PACK_WINO: [slice][chunk][i][j][nt][lane][4] of U = G g G^T (F(2x2,3x3))."""
+    L = stif._lib
+    lib = L.lib()
+    rng = np.random.default_rng(1)
+    cout, cin = 96, 16          # 96 -> padded to 128 (2 slices)
+    w = rng.standard_normal((cout, cin, 3, 3)).astype(np.float32)
+    b = rng.standard_normal(cout).astype(np.float32)
+    wd = np.empty(lib.stif_conv_weight_floats(cout, cin, 3, L.PACK_WINO), np.float32)
+    bd = np.empty(lib.stif_conv_bias_floats(cout, L.PACK_WINO), np.float32)
+    assert wd.size == 128 * cin * 16 and bd.size == 128
+    assert lib.stif_pack_conv_weight(w.ctypes.data, b.ctypes.data, cout, cin, 3, L.PACK_WINO,
+                                     wd.ctypes.data, bd.ctypes.data) == 0
+    G = np.array([[1, 0, 0], [.5, .5, .5], [.5, -.5, .5], [0, 0, 1]])
+    U = np.einsum("ap,oipq,bq->oiab", G, w.astype(np.float64), G)          # [co][ci][4][4]
+    Up = np.zeros((128, cin, 4, 4))
+    Up[:cout] = U
+    a = wd.reshape(2, cin // 8, 4, 4, 2, 2, 32, 4)        # [s][c][i][j][nt][h][l32][e]
+    got = a.transpose(0, 4, 6, 1, 5, 7, 2, 3).reshape(128, cin, 4, 4)
+    assert np.allclose(got, Up, rtol=1e-6, atol=1e-7)
+    assert np.array_equal(bd[:cout], b) and not bd[cout:].any()
