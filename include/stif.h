@@ -78,6 +78,12 @@ int stif_conv2d_nhwc(const stif_conv_args* args, void* stream);
  * cout a multiple of 64, in1_mode 0 or 1, epi NONE / LRELU / RELU / RES. */
 int stif_conv3x3_wino(const stif_conv_args* args, void* stream);
 
+/* out = scale * F.interpolate(in, scale_factor=2, mode='bilinear', align_corners=False) on NHWC
+ * maps (PCD_Align's coarse-to-fine step, Sakuya_arch_test.py:86-87); in [n][h1][w1][c],
+ * out [n][2h1][2w1][c], items `in_item` / `out_item` floats apart, c % 4 == 0. */
+int stif_upsample2x_nhwc(const float* in, float* out, int n, int h1, int w1, int c, float scale,
+                         long long in_item, long long out_item, void* stream);
+
 /* conv_first (3 -> 64, 3x3) + LeakyReLU, reading NCHW RGB frames [n,3,h,w]
  * (Sakuya_arch_test.py:318) and writing NHWC [n,h,w,64]. w: [64,3,3,3] as in the state dict. */
 int stif_conv_first(const float* x_nchw, const float* w, const float* b, float* out,

@@ -8,7 +8,8 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libstif_hip.so")
+# STIF_HIP_LIB overrides the in-tree library (kernel experiments); the default is the in-tree build
+LIB_PATH = os.environ.get("STIF_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libstif_hip.so")
 
 MAXG = 8
 EPI_NONE, EPI_LRELU, EPI_RELU, EPI_RES, EPI_OFFMASK, EPI_LSTM = range(6)
@@ -48,6 +49,8 @@ EXPORTS = {
     # name: (restype, argtypes)
     "stif_conv2d_nhwc": (C.c_int, [C.POINTER(ConvArgs), _P]),
     "stif_conv3x3_wino": (C.c_int, [C.POINTER(ConvArgs), _P]),
+    "stif_upsample2x_nhwc": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, C.c_longlong,
+                                       C.c_longlong, _P]),
     "stif_conv_first": (C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, C.c_int, _P]),
     "stif_dcn_nhwc": (C.c_int, [C.POINTER(DcnArgs), _P]),
     "stif_dcn_v2_workspace_size": (C.c_size_t, [C.c_int] * 14),

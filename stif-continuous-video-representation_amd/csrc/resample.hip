@@ -1,0 +1,55 @@
+// x2 bilinear upsampling of NHWC fp32 maps, times a scale:
+//   scale * F.interpolate(x, scale_factor=2, mode='bilinear', align_corners=False)
+// as PCD_Align applies it to the coarser level's offsets (x2) and aligned features (x1)
+// (Sakuya_arch_test.py:86-87,90,95-96,99,112,116,121,125).  Materialising the upsampled map
+// (HBM-bound, ~3 bytes moved per byte produced) lets the cat(., up(.)) convolutions run on the
+// Winograd kernel with two full-resolution inputs.
+#include "abi_util.h"
+#include "stif.h"
+#include "stif_common.h"
+
+#include <algorithm>
+
+namespace {
+
+// one thread = 4 channels of one output pixel
+__global__ __launch_bounds__(256) void k_up2(const float* __restrict__ in, float* __restrict__ out, int n, int h1,
+                                             int w1, int c, float scale, long long in_item, long long out_item) {
+  const int c4n = c >> 2;
+  const int H = 2 * h1, W = 2 * w1;
+  const long long total = (long long)n * H * W * c4n;
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const int q = (int)(e % c4n);
+    long long r = e / c4n;
+    const int x = (int)(r % W);
+    r /= W;
+    const int y = (int)(r % H);
+    const int item = (int)(r / H);
+    // align_corners=False source coordinates (clamped at 0 like ATen's area_pixel_compute_source_index)
+    const float sy = fmaxf(0.5f * ((float)y + 0.5f) - 0.5f, 0.f);
+    const float sx = fmaxf(0.5f * ((float)x + 0.5f) - 0.5f, 0.f);
+    const int y0 = min((int)sy, h1 - 1), x0 = min((int)sx, w1 - 1);
+    const int y1 = y0 + (y0 < h1 - 1 ? 1 : 0), x1 = x0 + (x0 < w1 - 1 ? 1 : 0);
+    const float ly1 = sy - (float)y0, lx1 = sx - (float)x0;
+    const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
+    const float* src = in + (size_t)item * in_item + q * 4;
+    const f32x4 v00 = ld4(src + ((size_t)y0 * w1 + x0) * c), v01 = ld4(src + ((size_t)y0 * w1 + x1) * c);
+    const f32x4 v10 = ld4(src + ((size_t)y1 * w1 + x0) * c), v11 = ld4(src + ((size_t)y1 * w1 + x1) * c);
+    const f32x4 v = (ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11)) * scale;
+    st4(out + (size_t)item * out_item + ((size_t)y * W + x) * c + q * 4, v);
+  }
+}
+
+}  // namespace
+
+extern "C" int stif_upsample2x_nhwc(const float* in, float* out, int n, int h1, int w1, int c, float scale,
+                                    long long in_item, long long out_item, void* stream) {
+  if (!in || !out || n < 1 || h1 < 1 || w1 < 1 || c < 4 || c % 4 || in_item < (long long)h1 * w1 * c ||
+      out_item < 4LL * h1 * w1 * c)
+    return stif_fail(STIF_E_INVALID, "stif_upsample2x_nhwc: bad arguments");
+  const long long total = (long long)n * 4 * h1 * w1 * (c / 4);
+  const long long blocks = std::min<long long>((total + 255) / 256, 1 << 20);
+  hipLaunchKernelGGL(k_up2, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, in, out, n, h1, w1, c, scale,
+                     in_item, out_item);
+  return stif_check_launch("stif_upsample2x_nhwc");
+}

@@ -25,24 +25,39 @@
 #include "stif.h"
 #include "stif_common.h"
 
+#include <algorithm>
+
 namespace {
 
-constexpr int WR = 4;      // output rows per workgroup
+constexpr int WR = 4;      // output rows per tile
 constexpr int HR = 6;      // halo rows
 constexpr int HC = 34;     // halo columns
+#ifndef WINO_PSUB
 constexpr int PSUB = 4;    // 8-channel chunks per staging phase
+#else
+constexpr int PSUB = WINO_PSUB;
+#endif
 constexpr int IN_EL = HR * PSUB * 2 * HC;      // 16-B elements per phase buffer
 constexpr int IN_INST = (IN_EL + 63) / 64;     // LDS-DMA instructions per phase
-constexpr int BUF_F = IN_INST * 256;           // floats per phase buffer
-constexpr int EPI_F = 2 * 4 * 2 * 32 * 32;     // epilogue exchange: [nt][i][b][tile][32 co]
-constexpr int SM_F = (2 * BUF_F > EPI_F) ? 2 * BUF_F : EPI_F;
+constexpr int EX_F = 2 * 2 * 2 * 1024;         // epilogue exchange: [wave 1|2][nt][b][32 tiles][32 co]
+constexpr int BUF_F = (IN_INST * 256 > EX_F) ? IN_INST * 256 : EX_F;   // floats per buffer (32 KB)
+constexpr int WG_PER_CU = 2;
 
 // slot of halo column c in its (row, chunk, half) run: even columns first, then odd
 STIF_DEV int col_slot(int c) { return (c & 1) ? 17 + (c >> 1) : (c >> 1); }
 
+struct Tile {
+  int oy0, ox0, slice, g, n;
+};
+
+// Persistent: WG_PER_CU workgroups per CU walk the tiles (tile = 4 output rows x 32 columns x one
+// 64-cout slice of one item), and the last staging phase of a tile already LDS-DMAs the first
+// phase of the next tile and the last chunk prefetches the next tile's first B operands, so a
+// workgroup's MFMA stream only pauses at the per-phase barriers and the short epilogue exchange.
 template <int IN1, int EPI>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_wino(stif_conv_args a) {
-  __shared__ __attribute__((aligned(16))) float smem[SM_F];
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_wino(stif_conv_args a,
+                                                                                      int ntiles) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * BUF_F];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wi = __builtin_amdgcn_readfirstlane(tid >> 6);   // transform row i of this wave
@@ -51,28 +66,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   const int tyl = tl >> 4, txl = tl & 15;
 
   const int tiles_x = (a.Wo + 31) >> 5;
-  const int tx = blockIdx.x % tiles_x;
-  const int ty = blockIdx.x / tiles_x;
-  const int slice = blockIdx.y;
-  const int g = blockIdx.z / a.nitems;
-  const int n = blockIdx.z - g * a.nitems;
+  const int tiles_y = (a.Ho + WR - 1) / WR;
+  const int slices = a.cout >> 6;
   const int H = a.H, W = a.W, C0 = a.C0, C1 = a.C1;
-  const float* in0 = a.in0[g] + (size_t)n * a.in0_item;
-  const float* in1 = IN1 ? a.in1[g] + (size_t)n * a.in1_item : in0;
-  const __amdgpu_buffer_rsrc_t r0 =
-      __builtin_amdgcn_make_buffer_rsrc((void*)in0, (short)0, (int)((size_t)H * W * C0 * 4), 0x00020000);
-  const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)in1, (short)0, (int)((size_t)H * W * (IN1 ? C1 : C0) * 4), 0x00020000);
-  const int oy0 = ty * WR, ox0 = tx * 32;
-  const int iy0 = oy0 - 1, ix0 = ox0 - 1;
   const int NC0 = C0 >> 3;
   const int NC = NC0 + (IN1 ? (C1 >> 3) : 0);
-  const int NP = (NC + PSUB - 1) / PSUB;
-  // packed U: [slice][chunk][i][j][nt][lane][4]
-  const float* wsl = a.w[g] + (size_t)slice * NC * 8192 + wi * 2048 + lane * 4;
+  const int NP = NC / PSUB;   // host guarantees NC % PSUB == 0
 
-  auto stage = [&](int p, int buf) {
+  auto tile_of = [&](int T) {
+    Tile t;
+    const int x = T % tiles_x;
+    int r = T / tiles_x;
+    const int y = r % tiles_y;
+    r /= tiles_y;
+    t.slice = r % slices;
+    r /= slices;
+    t.g = r / a.nitems;
+    t.n = r - t.g * a.nitems;
+    t.oy0 = y * WR;
+    t.ox0 = x * 32;
+    return t;
+  };
+  // packed U: [slice][chunk][i][j][nt][lane][4]
+  auto wbase = [&](const Tile& t) { return a.w[t.g] + (size_t)t.slice * NC * 8192 + wi * 2048 + lane * 4; };
+
+  auto stage = [&](const Tile& t, int p, int buf) {
+    const float* in0 = a.in0[t.g] + (size_t)t.n * a.in0_item;
+    const float* in1 = IN1 ? a.in1[t.g] + (size_t)t.n * a.in1_item : in0;
+    const __amdgpu_buffer_rsrc_t r0 =
+        __builtin_amdgcn_make_buffer_rsrc((void*)in0, (short)0, (int)((size_t)H * W * C0 * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)in1, (short)0, (int)((size_t)H * W * (IN1 ? C1 : C0) * 4), 0x00020000);
     float* dst = smem + buf * BUF_F;
+    const int iy0 = t.oy0 - 1, ix0 = t.ox0 - 1;
+#ifdef WINO_EXP_NOSTAGE
+    if (p < 1000000) return;
+#endif
     for (int q = wi; q < IN_INST; q += 4) {
       const int e = q * 64 + lane;
       const int slot = e % HC;
@@ -81,7 +110,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       const int col = slot < 17 ? 2 * slot : 2 * (slot - 17) + 1;
       const int k = p * PSUB + sub;
       const int y = iy0 + row, x = ix0 + col;
-      const bool ok = e < IN_EL && k < NC && y >= 0 && y < H && x >= 0 && x < W;
+      const bool ok = e < IN_EL && y >= 0 && y < H && x >= 0 && x < W;
       const bool second = IN1 && k >= NC0;
       const int Cs = second ? C1 : C0;
       const int cc = second ? k - NC0 : k;
@@ -99,113 +128,189 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   const float sB = (wi == 1) ? 1.f : -1.f;
   const int s0 = col_slot(0) + txl, s1 = col_slot(1) + txl, s2 = col_slot(2) + txl, s3 = col_slot(3) + txl;
 
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) acc[j][0] = acc[j][1] = f32x16{0};
+  // input transform row i of 8-channel chunk s of the phase in `buf`, for this lane's tile and
+  // channels 4h..4h+3: the wave's MFMA A operands for xi = 4i + j
+  auto transform = [&](const float* buf, int s, f32x4* v) {
+    const float* ra = buf + (((2 * tyl + rA) * PSUB + s) * 2 + hf) * HC * 4;
+    const float* rb = buf + (((2 * tyl + rB) * PSUB + s) * 2 + hf) * HC * 4;
+    const f32x4 t0 = ld4(ra + s0 * 4) + sB * ld4(rb + s0 * 4);
+    const f32x4 t1 = ld4(ra + s1 * 4) + sB * ld4(rb + s1 * 4);
+    const f32x4 t2 = ld4(ra + s2 * 4) + sB * ld4(rb + s2 * 4);
+    const f32x4 t3 = ld4(ra + s3 * 4) + sB * ld4(rb + s3 * 4);
+    v[0] = t0 - t2;
+    v[1] = t1 + t2;
+    v[2] = t2 - t1;
+    v[3] = t1 - t3;
+  };
 
+  int T = blockIdx.x;
+  if (T >= ntiles) return;
+  Tile cur = tile_of(T);
+  const float* wsl = wbase(cur);
   f32x4 bw[4][2];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) bw[j][nt] = ld4(wsl + (j * 2 + nt) * 256);
-
-  stage(0, 0);
+  int gp = 0;                      // phases staged so far: buffer of phase gp = gp & 1
+  stage(cur, 0, 0);
   lds_dma_barrier();
-  for (int p = 0; p < NP; ++p) {
-    if (p + 1 < NP) stage(p + 1, (p + 1) & 1);
-    const float* buf = smem + (p & 1) * BUF_F;
-    const int nsub = min(PSUB, NC - p * PSUB);
-    for (int s = 0; s < nsub; ++s) {
-      const int k = p * PSUB + s;
-      // ---- input transform row i for this lane's tile and 4 channels
-      const float* ra = buf + (((2 * tyl + rA) * PSUB + s) * 2 + hf) * HC * 4;
-      const float* rb = buf + (((2 * tyl + rB) * PSUB + s) * 2 + hf) * HC * 4;
-      const f32x4 t0 = ld4(ra + s0 * 4) + sB * ld4(rb + s0 * 4);
-      const f32x4 t1 = ld4(ra + s1 * 4) + sB * ld4(rb + s1 * 4);
-      const f32x4 t2 = ld4(ra + s2 * 4) + sB * ld4(rb + s2 * 4);
-      const f32x4 t3 = ld4(ra + s3 * 4) + sB * ld4(rb + s3 * 4);
-      f32x4 v[4];
-      v[0] = t0 - t2;
-      v[1] = t1 + t2;
-      v[2] = t2 - t1;
-      v[3] = t1 - t3;
-      const bool more = k + 1 < NC;
-      const float* wn = wsl + (size_t)(k + 1) * 8192;
+
+  for (;;) {
+    const int Tn = T + gridDim.x;
+    const bool has_next = Tn < ntiles;
+    const Tile nxt = tile_of(has_next ? Tn : T);
+    const float* wnx = wbase(nxt);
+
+    f32x16 acc[4][2];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < 4; ++j) acc[j][0] = acc[j][1] = f32x16{0};
+
+    for (int p = 0; p < NP; ++p, ++gp) {
+      if (p + 1 < NP) stage(cur, p + 1, (gp + 1) & 1);
+      else if (has_next) stage(nxt, 0, (gp + 1) & 1);
+      const float* buf = smem + (gp & 1) * BUF_F;
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
+      for (int s = 0; s < PSUB; ++s) {
+        f32x4 v[4];
+#ifdef WINO_EXP_NOXF
+        v[0] = v[1] = v[2] = v[3] = f32x4{1.f * s, 1.f, 1.f, (float)lane};
+#else
+        transform(buf, s, v);
+#endif
+        // B operands of the next chunk (the next tile's first chunk after the last one)
+        const int kn = p * PSUB + s + 1;
+        const float* wn = kn < NC ? wsl + (size_t)kn * 8192 : wnx;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) acc[j][nt] = mfma32(v[j][e], bw[j][nt][e], acc[j][nt]);
+        for (int j = 0; j < 4; ++j) {
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[j][nt] = mfma32(v[j][e], bw[j][nt][e], acc[j][nt]);
+          }
+#ifndef WINO_EXP_NOB
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) bw[j][nt] = ld4(wn + (j * 2 + nt) * 256);
+#else
+          for (int nt = 0; nt < 2; ++nt) bw[j][nt] += 1.f;
+          (void)wn;
+#endif
         }
-        // B operands of the next chunk, issued once this j's are consumed
+      }
+#ifndef WINO_EXP_NOBAR
+      lds_dma_barrier();
+#endif
+    }
+
+    // ---- output transform: P_i[b] = sum_j M[i][j] A[j][b] (registers); Y[0] = P_0 + P_1 + P_2
+    // (wave 0), Y[1] = P_1 - P_2 - P_3 (wave 3); waves 1 and 2 hand P over through the buffer of
+    // the phase just finished (free after the barrier; the other one is receiving the next tile).
+    // The stores go straight from the accumulator layout: per register, lanes 0-31 / 32-63 write
+    // the 32 couts (128 B) of one output pixel each.
+    float* ex = smem + ((gp - 1) & 1) * BUF_F;
+    const bool fin = wi == 0 || wi == 3;
+    const int ar = (wi == 0) ? 0 : 1;
+    f32x16 yv[2][2];   // [nt][b]
+    const float sg = wi == 0 ? 1.f : -1.f;
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      yv[nt][0] = acc[0][nt] + acc[1][nt] + acc[2][nt];
+      yv[nt][1] = acc[1][nt] - acc[2][nt] - acc[3][nt];
+    }
+    if (!fin) {
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          float* dx = ex + (((wi - 1) * 2 + nt) * 2 + b) * 1024;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) dx[mfma_row(r, lane) * 32 + tl] = yv[nt][b][r];
+        }
+    }
+    // output addressing: register r of this lane is pixel (oy0 + 2(r >> 3) + ar,
+    // ox0 + 2((r & 3) + 8((r >> 2) & 1) + 4h) + b), cout slice*64 + nt*32 + (lane & 31)
+    const size_t slab = (size_t)a.Ho * a.Wo * a.cout;
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.out[cur.g] + (size_t)cur.n * a.out_item), (short)0, (int)(slab * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(EPI == STIF_EPI_RES ? a.res[cur.g] + (size_t)cur.n * a.res_item : a.in0[cur.g]), (short)0,
+        (int)(slab * 4), 0x00020000);
+    auto voff = [&](int nt, int b, int r) -> unsigned {
+      const int oy = cur.oy0 + 2 * (r >> 3) + ar;
+      const int ox = cur.ox0 + 2 * ((r & 3) + 8 * ((r >> 2) & 1) + 4 * hf) + b;
+      const int co = cur.slice * 64 + nt * 32 + tl;
+      const bool ok = (oy < a.Ho) & (ox < a.Wo);
+      return ok ? (unsigned)(((oy * a.Wo + ox) * a.cout + co) * 4) : 0x80000000u;
+    };
+    __syncthreads();
+    if (fin) {
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const float* s1p = ex + ((0 * 2 + nt) * 2 + b) * 1024;   // P_1
+          const float* s2p = ex + ((1 * 2 + nt) * 2 + b) * 1024;   // P_2
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int o = mfma_row(r, lane) * 32 + tl;
+            yv[nt][b][r] = fmaf(sg, yv[nt][b][r], s1p[o] + sg * s2p[o]);
+          }
+        }
+    }
+    __syncthreads();   // exchange buffer free for the next tile's staging
+    if (fin) {
+      f32x16 rv[2][2];
+      if (EPI == STIF_EPI_RES) {
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt)
-          if (more) bw[j][nt] = ld4(wn + (j * 2 + nt) * 256);
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) rv[nt][b][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, voff(nt, b, r), 0, 0));
       }
-    }
-    lds_dma_barrier();
-  }
-
-  // ---- output transform: P_i[b] = sum_j M[i][j] A[j][b] in registers, Y = sum_i A^T[a][i] P_i
-  float* ex = smem;
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    f32x16 p0 = acc[0][nt] + acc[1][nt] + acc[2][nt];
-    f32x16 p1 = acc[1][nt] - acc[2][nt] - acc[3][nt];
-    float* d0 = ex + ((nt * 4 + wi) * 2 + 0) * 1024;
-    float* d1 = ex + ((nt * 4 + wi) * 2 + 1) * 1024;
+      for (int nt = 0; nt < 2; ++nt) {
+        const float bv = a.bias[cur.g][cur.slice * 64 + nt * 32 + tl];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int t = mfma_row(r, lane);
-      d0[t * 32 + tl] = p0[r];
-      d1[t * 32 + tl] = p1[r];
-    }
-  }
-  __syncthreads();
-  const int c4 = tid & 7, t = tid >> 3;       // (tile, 4 couts) per thread and 32-cout half
-  const int oyt = oy0 + 2 * (t >> 4), oxt = ox0 + 2 * (t & 15);
-  const float* bias = a.bias[g] + slice * 64;
-  float* out = a.out[g] + (size_t)n * a.out_item;
-  const float* res = (EPI == STIF_EPI_RES) ? a.res[g] + (size_t)n * a.res_item : nullptr;
-  const int cs = a.cout;
+        for (int b = 0; b < 2; ++b)
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    const int co = slice * 64 + nt * 32 + c4 * 4;
-    if (co >= a.cout) break;
-    f32x4 P[4][2];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) P[i][b] = ld4(ex + ((nt * 4 + i) * 2 + b) * 1024 + t * 32 + c4 * 4);
-    const f32x4 bv = ld4(bias + nt * 32 + c4 * 4);
-#pragma unroll
-    for (int ar = 0; ar < 2; ++ar)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        f32x4 y = ar == 0 ? P[0][b] + P[1][b] + P[2][b] : P[1][b] - P[2][b] - P[3][b];
-        y += bv;
-        const int oy = oyt + ar, ox = oxt + b;
-        if (oy < a.Ho && ox < a.Wo) {
-          const size_t o = ((size_t)oy * a.Wo + ox) * cs + co;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            if (EPI == STIF_EPI_LRELU) y[e] = lrelu01(y[e]);
-            if (EPI == STIF_EPI_RELU) y[e] = fmaxf(y[e], 0.f);
+          for (int r = 0; r < 16; ++r) {
+            float y = yv[nt][b][r] + bv;
+            if (EPI == STIF_EPI_LRELU) y = lrelu01(y);
+            if (EPI == STIF_EPI_RELU) y = fmaxf(y, 0.f);
+            if (EPI == STIF_EPI_RES) y += rv[nt][b][r];
+#ifdef WINO_EXP_NOEPI
+            if (y == 12345.f)
+#endif
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ro, voff(nt, b, r), 0, 0);
           }
-          if (EPI == STIF_EPI_RES) y += ld4(res + o);
-          st4(out + o, y);
-        }
       }
+    }
+    if (!has_next) break;
+    T = Tn;
+    cur = nxt;
+    wsl = wnx;
   }
+}
+
+int num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
 }
 
 template <int IN1, int EPI>
 int launch(const stif_conv_args& a, hipStream_t st) {
-  const int tiles = ((a.Wo + 31) / 32) * ((a.Ho + WR - 1) / WR);
-  const int slices = (a.cout + 63) / 64;
-  dim3 grid(tiles, slices, a.ngroups * a.nitems);
-  hipLaunchKernelGGL((k_wino<IN1, EPI>), grid, dim3(256), 0, st, a);
+  const long long tiles = (long long)((a.Wo + 31) / 32) * ((a.Ho + WR - 1) / WR) * (a.cout / 64) * a.ngroups * a.nitems;
+  if (tiles > 0x7fffffff) return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: too many tiles");
+  if ((long long)a.H * a.W * std::max(a.C0, std::max(a.C1, a.cout)) * 4 >= 0x7fffffffLL)
+    return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: item larger than 2 GB (buffer addressing)");
+  const int grid = (int)std::min<long long>(tiles, (long long)WG_PER_CU * num_cus());
+  hipLaunchKernelGGL((k_wino<IN1, EPI>), dim3(grid), dim3(256), 0, st, a, (int)tiles);
   return stif_check_launch("stif_conv3x3_wino");
 }
 
@@ -222,6 +327,8 @@ extern "C" int stif_conv3x3_wino(const stif_conv_args* pa, void* stream) {
   if (a.C0 % 8 || a.C0 <= 0 || (a.in1_mode == 1 && (a.C1 % 8 || a.C1 <= 0)))
     return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: channel counts must be multiples of 8");
   if (a.cout % 64) return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: cout must be a multiple of 64");
+  if ((a.C0 + (a.in1_mode ? a.C1 : 0)) % (8 * PSUB))
+    return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: total input channels must be a multiple of 32");
   if (a.epi == STIF_EPI_RES && !a.res[0]) return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: RES needs res");
 #define STIF_WINO_CASE(IN1)                                              \
   switch (a.epi) {                                                       \

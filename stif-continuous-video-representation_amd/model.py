@@ -118,8 +118,8 @@ class LunaTokis:
         def conv(name, mode=L.PACK_PLAIN):
             lay[name] = ops.pack_conv(h[name + ".weight"], h[name + ".bias"], mode, dev)
 
-        # 3x3 / stride-1 / 64-cout convs whose second input (if any) is at full resolution run by
-        # Winograd F(2x2,3x3) (stif_conv3x3_wino); the x2-upsampled-input, strided, 1x1,
+        # 3x3 / stride-1 / 64-cout convs run by Winograd F(2x2,3x3) (stif_conv3x3_wino; the
+        # cat(., up(.)) ones on a materialised x2-upsampled second input); the strided, 1x1,
         # offset/mask and ConvLSTM convs keep the direct kernel.
         wino = L.PACK_WINO if self.winograd else L.PACK_PLAIN
 
@@ -140,8 +140,6 @@ class LunaTokis:
                     if cin is None:
                         conv(n)
                         conv(n + ".conv_offset_mask", L.PACK_OFFMASK)
-                    elif ln in ("L2_offset_conv2", "L2_fea_conv", "L1_offset_conv2", "L1_fea_conv"):
-                        conv(n)                       # second input is x2-upsampled
                     else:
                         conv(n, wino)
 
@@ -244,6 +242,17 @@ class LunaTokis:
 
         conv, dcn = ops.conv2d, ops.dcn
         E = enumerate
+
+        def conv_up(make, coarse, scale, epi):
+            """conv on cat(x, scale * up2(coarse)) for every unit: fused x2 upsample in the direct
+            kernel, or a materialised upsample + the Winograd kernel"""
+            if not self.winograd:
+                conv([make(i, u, coarse[i]) for i, u in E(units)], epi=epi, in1_mode=2, in1_scale=scale)
+                return
+            g_, n_, h_, w_, c_ = coarse.shape
+            up = self._empty(g_, n_, 2 * h_, 2 * w_, c_)
+            ops.upsample2x(coarse.view(g_ * n_, h_, w_, c_), up.view(g_ * n_, 2 * h_, 2 * w_, c_), scale)
+            conv([make(i, u, up[i]) for i, u in E(units)], epi=epi, in1_mode=1)
         # ---- L3
         o = buf(2)
         conv([dict(layer=L_(u, "L3_offset_conv1"), in0=u[2][2], in1=u[3][2], out=o[i]) for i, u in E(units)],
@@ -260,8 +269,8 @@ class LunaTokis:
         conv([dict(layer=L_(u, "L2_offset_conv1"), in0=u[2][1], in1=u[3][1], out=o1[i]) for i, u in E(units)],
              epi=L.EPI_LRELU, in1_mode=1)
         o2 = buf(1)
-        conv([dict(layer=L_(u, "L2_offset_conv2"), in0=o1[i], in1=l3off[i], out=o2[i]) for i, u in E(units)],
-             epi=L.EPI_LRELU, in1_mode=2, in1_scale=2.0)
+        conv_up(lambda i, u, c: dict(layer=L_(u, "L2_offset_conv2"), in0=o1[i], in1=c, out=o2[i]),
+                l3off, 2.0, L.EPI_LRELU)
         l2off = buf(1)
         conv([dict(layer=L_(u, "L2_offset_conv3"), in0=o2[i], out=l2off[i]) for i, u in E(units)], epi=L.EPI_LRELU)
         om = buf(1, 216)
@@ -269,23 +278,23 @@ class LunaTokis:
         d2 = buf(1)
         dcn([dict(layer=L_(u, "L2_dcnpack"), inp=u[2][1], offmask=om[i], out=d2[i]) for i, u in E(units)])
         l2fea = buf(1)
-        conv([dict(layer=L_(u, "L2_fea_conv"), in0=d2[i], in1=l3fea[i], out=l2fea[i]) for i, u in E(units)],
-             epi=L.EPI_LRELU, in1_mode=2, in1_scale=1.0)
+        conv_up(lambda i, u, c: dict(layer=L_(u, "L2_fea_conv"), in0=d2[i], in1=c, out=l2fea[i]),
+                l3fea, 1.0, L.EPI_LRELU)
         # ---- L1
         o1 = buf(0)
         conv([dict(layer=L_(u, "L1_offset_conv1"), in0=u[2][0], in1=u[3][0], out=o1[i]) for i, u in E(units)],
              epi=L.EPI_LRELU, in1_mode=1)
         o2 = buf(0)
-        conv([dict(layer=L_(u, "L1_offset_conv2"), in0=o1[i], in1=l2off[i], out=o2[i]) for i, u in E(units)],
-             epi=L.EPI_LRELU, in1_mode=2, in1_scale=2.0)
+        conv_up(lambda i, u, c: dict(layer=L_(u, "L1_offset_conv2"), in0=o1[i], in1=c, out=o2[i]),
+                l2off, 2.0, L.EPI_LRELU)
         l1off = buf(0)
         conv([dict(layer=L_(u, "L1_offset_conv3"), in0=o2[i], out=l1off[i]) for i, u in E(units)], epi=L.EPI_LRELU)
         om = buf(0, 216)
         conv([dict(layer=LO(u, "L1_dcnpack"), in0=l1off[i], out=om[i]) for i, u in E(units)], epi=L.EPI_OFFMASK)
         d1 = buf(0)
         dcn([dict(layer=L_(u, "L1_dcnpack"), inp=u[2][0], offmask=om[i], out=d1[i]) for i, u in E(units)])
-        conv([dict(layer=L_(u, "L1_fea_conv"), in0=d1[i], in1=l2fea[i], out=u[4]) for i, u in E(units)],
-             epi=L.EPI_NONE, in1_mode=2, in1_scale=1.0)
+        conv_up(lambda i, u, c: dict(layer=L_(u, "L1_fea_conv"), in0=d1[i], in1=c, out=u[4]),
+                l2fea, 1.0, L.EPI_NONE)
 
     def _bilstm(self, X):
         """BiDeformableConvLSTM.forward (:256-266) with DeformableConvLSTM.forward (:192-242) for

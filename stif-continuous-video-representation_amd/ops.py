@@ -121,6 +121,26 @@ def conv2d(groups, *, epi=L.EPI_NONE, in1_mode=0, in1_scale=1.0, stride=None):
         tr.end()
 
 
+def upsample2x(x: torch.Tensor, out: torch.Tensor, scale: float = 1.0):
+    """out = scale * bilinear x2 upsample (align_corners=False) of NHWC x [n, h, w, c] (items may be
+    strided; pixels contiguous) into out [n, 2h, 2w, c]."""
+    n, h, w, c = x.shape
+    if tuple(out.shape) != (n, 2 * h, 2 * w, c):
+        raise ValueError(f"upsample2x: out shape {tuple(out.shape)} != {(n, 2 * h, 2 * w, c)}")
+    for t in (x, out):
+        if t.stride()[1:] != (t.shape[2] * c, c, 1):
+            raise ValueError("upsample2x: pixels must be contiguous")
+    tr = TRACE
+    if tr is not None:
+        tr.begin(("up2",), 0.0)
+    L.check(L.lib().stif_upsample2x_nhwc(_vp(x), _vp(out), n, h, w, c, float(scale),
+                                         x.stride(0) if n > 1 else h * w * c,
+                                         out.stride(0) if n > 1 else 4 * h * w * c, _stream()),
+            "stif_upsample2x_nhwc")
+    if tr is not None:
+        tr.end()
+
+
 def conv_first(x_nchw: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: torch.Tensor):
     n, c, h, wd = x_nchw.shape
     assert c == 3 and x_nchw.is_contiguous() and out.is_contiguous()

@@ -117,3 +117,17 @@ def test_larger_size_vs_oracle(model, sd):
         out = model(torch.from_numpy(x).cuda(), [0.3])[0]
     ok, err, mx = close(out, ref)
     assert ok, (err, mx)
+
+
+def test_direct_conv_path_matches_reference(stif, sd, golden):
+    """winograd=False (every 3x3 conv on the direct implicit-GEMM kernel) against the fixtures."""
+    g = golden["model_16x20"]
+    m = stif.LunaTokis(64, 6, 8, 5, 40, winograd=False)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    with torch.no_grad():
+        outs = m(torch.from_numpy(g["x"]).cuda(), [torch.tensor([[float(t)]]) for t in g["times"]])
+    ok, err, mx = close(m.feat.detach().cpu().numpy()[0], g["feat"])
+    assert ok, (err, mx)
+    for i, o in enumerate(outs):
+        ok, err, mx = close(o[0], g["out"][i])
+        assert ok, (i, err, mx)

@@ -111,3 +111,34 @@ def test_wino_rejects_bad_shapes(stif):
     x = torch.zeros(1, 8, 8, 64, device="cuda")
     with pytest.raises(Exception):
         ops.conv2d([dict(layer=lay, in0=x, out=torch.empty(1, 4, 4, 64, device="cuda"))], stride=2)
+
+
+@pytest.mark.parametrize("scale", [1.0, 2.0])
+def test_upsample2x(stif, scale):
+    """stif_upsample2x_nhwc against the oracle's F.interpolate restatement, strided items."""
+    x = rnd(4, 64, 7, 9, seed=20)
+    t = nhwc(x)
+    out = torch.empty(2, 14, 18, 64, device="cuda")
+    stif.ops.upsample2x(t[1::2], out, scale)
+    ref = O.upsample2x(x[1::2].astype(np.float64)) * scale
+    assert relmax(to_nchw(out), ref) < 1e-6
+
+
+def test_wino_cat_upsampled_matches_fused_direct(stif):
+    """cat(x, 2*up2(c)) conv: materialised upsample + Winograd == the direct kernel's fused path."""
+    L, ops = stif._lib, stif.ops
+    H, W = 12, 36
+    x0 = rnd(2, 64, H, W, seed=21)
+    c = rnd(2, 64, H // 2, W // 2, seed=22)
+    w = rnd(64, 128, 3, 3, seed=23, scale=0.04)
+    b = rnd(64, seed=24)
+    up = torch.empty(2, H, W, 64, device="cuda")
+    ops.upsample2x(nhwc(c), up, 2.0)
+    o1 = torch.empty(2, H, W, 64, device="cuda")
+    o2 = torch.empty_like(o1)
+    ops.conv2d([dict(layer=ops.pack_conv(w, b, L.PACK_WINO), in0=nhwc(x0), in1=up, out=o1)], epi=L.EPI_LRELU,
+               in1_mode=1)
+    ops.conv2d([dict(layer=ops.pack_conv(w, b), in0=nhwc(x0), in1=nhwc(c), out=o2)], epi=L.EPI_LRELU,
+               in1_mode=2, in1_scale=2.0)
+    ref = O.lrelu(O.conv2d(np.concatenate([x0, O.upsample2x(c.astype(np.float64)) * 2], 1), w, b))
+    assert relmax(to_nchw(o1), ref) < RTOL and relmax(to_nchw(o2), ref) < RTOL

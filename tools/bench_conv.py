@@ -17,7 +17,10 @@ b = rng.standard_normal(64).astype(np.float32)
 x = torch.randn(N, H, W, 64, device="cuda")
 r = torch.randn(N, H, W, 64, device="cuda")
 flop = 2.0 * 64 * 64 * 9 * N * H * W
+ONLY = os.environ.get("ONLY")
 for name, mode in (("direct", L.PACK_PLAIN), ("wino", L.PACK_WINO)):
+    if ONLY and name != ONLY:
+        continue
     lay = ops.pack_conv(w, b, mode)
     out = torch.empty(N, H, W, 64, device="cuda")
     for epi in (L.EPI_RES, L.EPI_RELU):
