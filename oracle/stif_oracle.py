@@ -341,42 +341,77 @@ def siren(x, sd, p, n_sine, dtype):
     return x @ np.asarray(sd[f"{p}net.{n_sine}.weight"], dtype).T + np.asarray(sd[f"{p}net.{n_sine}.bias"], dtype)
 
 
-def decoding(feat, inp, times, sd, scale=None, dtype=np.float64, capture=None):
-    """LunaTokis.decoding (Sakuya_arch_test.py:364-459).
-    feat [B,3,64,H,W], inp [B,2,3,H,W], times: list of floats -> list of [B,3,HH,WW]."""
+def upsample_bilinear(x, s, dtype=np.float64):
+    """F.upsample(x, scale_factor=s, mode='bilinear') (align_corners=False; source index
+    (d + 0.5) / s - 0.5 clamped at 0, ATen upsample_bilinear2d) as decoding_test builds HRinp
+    (Sakuya_arch_test.py:513-514).  x [N,C,H,W] -> [N,C,sH,sW]."""
+    x = np.asarray(x, dtype)
+    N, C, H, W = x.shape
+
+    def idx(n):
+        src = np.maximum((np.arange(s * n, dtype=F32) + F32(0.5)) * F32(1.0 / s) - F32(0.5), F32(0))
+        i0 = src.astype(np.int64)
+        i1 = np.where(i0 < n - 1, i0 + 1, i0)
+        l1 = (src - i0).astype(dtype)
+        return i0, i1, 1 - l1, l1
+
+    h0, h1, lh0, lh1 = idx(H)
+    w0, w1, lw0, lw1 = idx(W)
+    top = x[:, :, h0][:, :, :, w0] * lw0 + x[:, :, h0][:, :, :, w1] * lw1
+    bot = x[:, :, h1][:, :, :, w0] * lw0 + x[:, :, h1][:, :, :, w1] * lw1
+    return top * lh0[:, None] + bot * lh1[:, None]
+
+
+def _decode(feat, inp, times, sd, HH, WW, dtype, capture=None, img=None, shift=None):
+    """The decoder body shared by decoding / decoding_test / decoding_fasttest /
+    decoding_localensemble (Sakuya_arch_test.py:364-459, 461-598, 863-1085).
+    img: the image the flow / encode stages sample bilinearly (LR inp, or decoding_test's x4
+    upsampled HRinp).  shift: (vx, vy) of the local ensemble -- the query coordinates move by
+    (vx/H + 1e-6, vy/W + 1e-6) for every sampling step except rel_coord and the warpgrid base.
+    Returns (list of [B,3,HH,WW], area [HH*WW] or None)."""
     B = feat.shape[0]
     H, W = feat.shape[-2:]
     featc = np.asarray(feat, dtype).reshape(B, 192, H, W)          # cat(feat[:,0..2]) (:365)
     inpc = np.asarray(inp, dtype).reshape(B, 6, H, W)
-    HH, WW = (H * 4, W * 4) if scale is None else (int(scale[0]), int(scale[1]))
+    img = inpc if img is None else np.asarray(img, dtype)
     lo, hi = F32(-1 + 1e-6), F32(1 - 1e-6)
     cy = np.clip(make_coord_1d(HH), lo, hi)                          # coord_highres (:373), row/col
     cx = np.clip(make_coord_1d(WW), lo, hi)
+    sy, sx = cy, cx
+    if shift is not None:                                            # :994-998 (fp32 tensor ops)
+        sy = np.clip((cy + F32(shift[0] * (2 / H / 2) + 1e-6)).astype(F32), lo, hi)
+        sx = np.clip((cx + F32(shift[1] * (2 / W / 2) + 1e-6)).astype(F32), lo, hi)
     ly, lx = make_coord_1d(H), make_coord_1d(W)                      # feat_coord (:375)
-    iy = np.clip(nearest_index(cy, H), 0, H - 1)
-    ix = np.clip(nearest_index(cx, W), 0, W - 1)
+    iy = np.clip(nearest_index(sy, H), 0, H - 1)
+    ix = np.clip(nearest_index(sx, W), 0, W - 1)
     rel_y = ((cy - ly[iy]) * F32(H)).astype(F32)                     # (:394-396)
     rel_x = ((cx - lx[ix]) * F32(W)).astype(F32)
     Q = HH * WW
     qy = np.repeat(np.arange(HH), WW)
     qx = np.tile(np.arange(WW), HH)
-    gy = np.broadcast_to(cy[qy], (B, Q))
-    gx = np.broadcast_to(cx[qx], (B, Q))
+    gy = np.broadcast_to(sy[qy], (B, Q))
+    gx = np.broadcast_to(sx[qx], (B, Q))
     lin = featc.reshape(B, 192, H * W).transpose(0, 2, 1)
     q_feat = lin[:, iy[qy] * W + ix[qx]]                              # nearest (:382-385)
     q_inp = inpc.reshape(B, 6, H * W).transpose(0, 2, 1)[:, iy[qy] * W + ix[qx]]
     rel = np.stack([np.broadcast_to(rel_y[qy], (B, Q)), np.broadcast_to(rel_x[qx], (B, Q))], -1).astype(dtype)
+    area = None
+    if shift is not None:                                            # :1003
+        area = np.abs((rel_y[qy] * rel_x[qx]).astype(F32)).astype(dtype) + 1e-9
+    # nearest HR pixel of the (shifted) query: identity without a shift (:406-409)
+    hy = np.clip(nearest_index(sy, HH), 0, HH - 1)
+    hx = np.clip(nearest_index(sx, WW), 0, WW - 1)
     gxs, gys = linspace_f32(WW), linspace_f32(HH)                     # warpgrid base (warplayer.py:27-31)
     preds = []
     for t in times:
         pe = np.full((B, Q, 1), t, dtype)
         x1 = np.concatenate([q_feat, q_inp, rel, pe], -1)             # 201 (:399)
         hrfeat = siren(x1, sd, "feat_imnet.", 3, dtype)               # [B,Q,64] (:400)
-        # q_feat at the HR centres is HRfeat itself (nearest at its own pixel centres, :406-409)
         hr_img = hrfeat.transpose(0, 2, 1).reshape(B, 64, HH, WW)
-        q_inp2 = bilinear_sample(inpc, gx, gy, dtype)                 # (:410-413)
+        q_hr = hrfeat[:, hy[qy] * WW + hx[qx]]
+        q_inp2 = bilinear_sample(img, gx, gy, dtype)                  # (:410-413)
         q_feat0 = bilinear_sample(featc, gx, gy, dtype)               # (:414-417)
-        flow = siren(np.concatenate([hrfeat, q_feat0, q_inp2, pe], -1), sd, "flow_imnet.", 3, dtype)  # 263
+        flow = siren(np.concatenate([q_hr, q_feat0, q_inp2, pe], -1), sd, "flow_imnet.", 3, dtype)  # 263
         if capture is not None:
             capture.setdefault("hrfeat", []).append(hrfeat)
             capture.setdefault("flow", []).append(flow)
@@ -391,11 +426,56 @@ def decoding(feat, inp, times, sd, scale=None, dtype=np.float64, capture=None):
             g_x = np.clip(bx + fx[..., k] / ((WW - 1.0) / 2.0), lo, hi)
             g_y = np.clip(by + fy[..., k] / ((HH - 1.0) / 2.0), lo, hi)
             feats.append((bilinear_sample(hr_img, g_x, g_y, dtype), bilinear_sample(featc, g_x, g_y, dtype)))
-            imgs.append(bilinear_sample(inpc, g_x, g_y, dtype))
+            imgs.append(bilinear_sample(img, g_x, g_y, dtype))
         x3 = np.concatenate([feats[0][0], feats[1][0], feats[0][1], feats[1][1], imgs[0], imgs[1], pe], -1)  # 525
         pred = siren(x3, sd, "encode_imnet.", 4, dtype)                # (:456)
         preds.append(pred.transpose(0, 2, 1).reshape(B, 3, HH, WW))
-    return preds
+    return preds, area
+
+
+def decoding(feat, inp, times, sd, scale=None, dtype=np.float64, capture=None):
+    """LunaTokis.decoding (Sakuya_arch_test.py:364-459).
+    feat [B,3,64,H,W], inp [B,2,3,H,W], times: list of floats -> list of [B,3,HH,WW]."""
+    H, W = feat.shape[-2:]
+    HH, WW = (H * 4, W * 4) if scale is None else (int(scale[0]), int(scale[1]))
+    return _decode(feat, inp, times, sd, HH, WW, dtype, capture)[0]
+
+
+def decoding_test(feat, inp, times, sd, scale=None, dtype=np.float64):
+    """LunaTokis.decoding_test (Sakuya_arch_test.py:461-598): decoding with the flow and encode
+    stages sampling HRinp = F.upsample(inp, x4, bilinear) instead of the LR frames; HH = H*scale
+    (scale an integer, default 4).  The q/3 chunking only bounds memory."""
+    H, W = feat.shape[-2:]
+    s = 4 if scale is None else int(scale)
+    B = feat.shape[0]
+    hr = upsample_bilinear(np.asarray(inp, dtype).reshape(B, 6, H, W), 4, dtype)
+    return _decode(feat, inp, times, sd, H * s, W * s, dtype, img=hr)[0]
+
+
+def decoding_fasttest(feat, inp, times, sd, scale=None, dtype=np.float64):
+    """LunaTokis.decoding_fasttest (Sakuya_arch_test.py:863-960): every time of `times` (floats)
+    as one batch of a batch-1 latent -> [len(times), 3, HH, WW]."""
+    return np.concatenate(decoding(feat, inp, times, sd, scale, dtype), 0)
+
+
+def decoding_localensemble(feat, inp, times, sd, scale=None, dtype=np.float64):
+    """LunaTokis.decoding_localensemble (Sakuya_arch_test.py:962-1085): four decodes with the
+    query shifted by (+-1/H, +-1/W) (+1e-6), blended by the diagonally opposite |rel_y rel_x|
+    area over the total (batch-1 latent, times as the batch) -> [len(times), 3, HH, WW]."""
+    H, W = feat.shape[-2:]
+    HH, WW = (H * 4, W * 4) if scale is None else (int(scale[0]), int(scale[1]))
+    preds, areas = [], []
+    for vx in (-1, 1):
+        for vy in (-1, 1):
+            p, a = _decode(feat, inp, times, sd, HH, WW, dtype, shift=(vx, vy))
+            preds.append(np.concatenate(p, 0))
+            areas.append(a)
+    tot = areas[0] + areas[1] + areas[2] + areas[3]
+    areas = [areas[3], areas[2], areas[1], areas[0]]                   # :1079-1080
+    ret = 0
+    for p, a in zip(preds, areas):
+        ret = ret + p * (a / tot).reshape(1, 1, HH, WW)
+    return ret
 
 
 def forward(x, times, sd, scale=None, front_RBs=5, back_RBs=40, dtype=np.float64, capture=None):

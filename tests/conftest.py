@@ -27,4 +27,4 @@ def sd(stif):
 def golden():
     import numpy as np
     d = os.path.join(REPO, "tests", "golden")
-    return {n: np.load(os.path.join(d, n + ".npz")) for n in ("model_16x20", "window_7x16x16", "ops")}
+    return {n: np.load(os.path.join(d, n + ".npz")) for n in ("model_16x20", "window_7x16x16", "ops", "decoders_16x20")}

@@ -19,7 +19,8 @@ Three shims make the reference importable without CUDA:
 Weights come from ``stif_amd.weights.make_state_dict(seed=0)`` and are loaded
 with ``load_state_dict(strict=True)``.
 
-Usage:  python tests/golden/make_golden.py
+Usage:  python tests/golden/make_golden.py             (model, window and per-op fixtures)
+        python tests/golden/make_golden.py decoders    (decoding_test / _fasttest / _localensemble)
 """
 import json
 import os
@@ -247,5 +248,46 @@ def main():
     print("ops done:", len(ops))
 
 
+def decoders():
+    """decoding_test / decoding_fasttest / decoding_localensemble (Sakuya_arch_test.py:461-598,
+    863-1085) on the model_16x20 latent -> decoders_16x20.npz"""
+    if not os.path.isdir(REF):
+        print("reference absent; nothing to do")
+        return
+    install_shims()
+    sys.path.insert(0, REPO)
+    import stif_pkg
+    stif = stif_pkg.load()
+    import models.modules.Sakuya_arch_test as S
+
+    torch.set_num_threads(8)
+    sd_np = stif.weights.make_state_dict(seed=0)
+    model = S.LunaTokis(64, 6, 8, 5, 40)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd_np.items()}, strict=True)
+    model.eval()
+    g = torch.Generator().manual_seed(1234)
+    H, W = 16, 20
+    x = torch.rand(1, 2, 3, H, W, generator=g)         # the model_16x20 input
+    res = {"x": f32(x)}
+    with torch.no_grad():
+        t_test = [0.25, 0.5]
+        outs = model(x, [torch.tensor([[t]]) for t in t_test], test=True)      # forward(test=True)
+        res["test_times"] = np.array(t_test, np.float32)
+        res["test_out"] = np.stack([f32(o[0]) for o in outs])
+        o3 = model.decoding_test([torch.tensor([[0.5]])], 3)[0]                 # HH = 3H, HRinp still x4
+        res["test_out_scale3"] = f32(o3[0])
+        t_fast = [0.0, 0.5, 0.75]
+        res["fast_times"] = np.array(t_fast, np.float32)
+        res["fast_out"] = f32(model.decoding_fasttest(t_fast))
+        res["fast_out_40x50"] = f32(model.decoding_fasttest([0.5], (40, 50)))
+        res["ens_out"] = f32(model.decoding_localensemble([0.5]))
+        res["ens_out_40x50"] = f32(model.decoding_localensemble([0.25], (40, 50)))
+    np.savez_compressed(os.path.join(HERE, "decoders_16x20.npz"), **res)
+    print("decoders:", {k: v.shape for k, v in res.items()})
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["decoders"]:
+        decoders()
+        sys.exit(0)
     main()

@@ -142,3 +142,24 @@ def test_wino_cat_upsampled_matches_fused_direct(stif):
                in1_mode=2, in1_scale=2.0)
     ref = O.lrelu(O.conv2d(np.concatenate([x0, O.upsample2x(c.astype(np.float64)) * 2], 1), w, b))
     assert relmax(to_nchw(o1), ref) < RTOL and relmax(to_nchw(o2), ref) < RTOL
+
+
+def test_wino_offmask_matches_direct(stif):
+    """64 -> 216 offset/mask conv (permuted [group][tap][dy,dx,sigmoid(m)] rows, 4 cout slices with
+    the last one partial) on the Winograd kernel == the direct kernel, and == the oracle."""
+    L, ops = stif._lib, stif.ops
+    x = rnd(2, 64, 10, 40, seed=30)
+    w = rnd(216, 64, 3, 3, seed=31, scale=0.05)
+    b = rnd(216, seed=32)
+    o1 = torch.empty(2, 10, 40, 216, device="cuda")
+    o2 = torch.empty_like(o1)
+    ops.conv2d([dict(layer=ops.pack_conv(w, b, L.PACK_WINO_OFFMASK), in0=nhwc(x), out=o1)], epi=L.EPI_OFFMASK)
+    ops.conv2d([dict(layer=ops.pack_conv(w, b, L.PACK_OFFMASK), in0=nhwc(x), out=o2)], epi=L.EPI_OFFMASK)
+    a1, a2 = o1.cpu().numpy(), o2.cpu().numpy()
+    assert np.abs(a1 - a2).max() < 1e-5 * np.abs(a2).max()
+    ref = O.conv2d(x, w, b)                                      # [2,216,10,40] reference order
+    got = a1.reshape(2, 10, 40, 8, 9, 3)
+    off = ref[:, :144].reshape(2, 8, 9, 2, 10, 40).transpose(0, 4, 5, 1, 2, 3)
+    msk = 1 / (1 + np.exp(-ref[:, 144:].reshape(2, 8, 9, 10, 40).transpose(0, 3, 4, 1, 2)))
+    assert relmax(got[..., :2], off) < RTOL
+    assert np.abs(got[..., 2] - msk).max() < 1e-5

@@ -100,3 +100,24 @@ def test_window(golden, sd):
     x = np.stack([fr[:-1], fr[1:]], axis=1)      # 6 pairs batched: pairs are independent
     outs = O.forward(x, [0.5], sd)[0]
     assert relmax(outs, g["out"]) < 1e-5
+
+
+@pytest.mark.parametrize("which", ["test", "test_scale3", "fast", "fast_40x50", "ens", "ens_40x50"])
+def test_oracle_decoder_variants_match_reference(sd, golden, which):
+    """decoding_test / decoding_fasttest / decoding_localensemble restatements against the
+    reference's own outputs (tests/golden/decoders_16x20.npz, same latent as model_16x20)."""
+    g, d = golden["model_16x20"], golden["decoders_16x20"]
+    feat, x = g["feat"][None], g["x"]
+    if which == "test":
+        got, ref = np.stack([o[0] for o in O.decoding_test(feat, x, list(d["test_times"]), sd)]), d["test_out"]
+    elif which == "test_scale3":
+        got, ref = O.decoding_test(feat, x, [0.5], sd, scale=3)[0][0], d["test_out_scale3"]
+    elif which == "fast":
+        got, ref = O.decoding_fasttest(feat, x, list(d["fast_times"]), sd), d["fast_out"]
+    elif which == "fast_40x50":
+        got, ref = O.decoding_fasttest(feat, x, [0.5], sd, (40, 50)), d["fast_out_40x50"]
+    elif which == "ens":
+        got, ref = O.decoding_localensemble(feat, x, [0.5], sd), d["ens_out"]
+    else:
+        got, ref = O.decoding_localensemble(feat, x, [0.25], sd, (40, 50)), d["ens_out_40x50"]
+    assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max()
