@@ -74,8 +74,9 @@ typedef struct {
 int stif_conv2d_nhwc(const stif_conv_args* args, void* stream);
 
 /* The same operator for 3x3 / stride 1 / 'same' shapes by Winograd F(2x2,3x3) on fp32 MFMA
- * (2.25x fewer multiply-adds; all arithmetic fp32): weights packed with STIF_PACK_WINO,
- * cout a multiple of 64, in1_mode 0 or 1, epi NONE / LRELU / RELU / RES. */
+ * (2.25x fewer multiply-adds; all arithmetic fp32): weights packed with STIF_PACK_WINO
+ * (epi NONE / LRELU / RELU / RES) or STIF_PACK_WINO_OFFMASK (epi OFFMASK, cout 216);
+ * in1_mode 0 or 1; total input channels a multiple of 32. */
 int stif_conv3x3_wino(const stif_conv_args* args, void* stream);
 
 /* out = scale * F.interpolate(in, scale_factor=2, mode='bilinear', align_corners=False) on NHWC
@@ -139,22 +140,46 @@ typedef struct {
   const float* lin_y;
   const int* near_x; const float* rel_x; const int* bx0; const int* bx1; const float* wx0; const float* wx1;
   const float* lin_x;
+  /* optional (NULL = identity): HR pixel whose HRfeat the flow stage reads for a query -- the
+   * local ensemble's shifted queries (decoding_localensemble, Sakuya_arch_test.py:1022-1025) */
+  const int* hr_y; const int* hr_x;
 } stif_dec_tables;
+
+/* Optional high-resolution image for the flow / encode stages (decoding_test samples
+ * HRinp = F.upsample(inp, x4, bilinear), Sakuya_arch_test.py:513-514, instead of the LR frames;
+ * pack the projection with stif_pack_dec_proj_ex(..., lr_image = 0) then).  img: [n][ih][iw][8]
+ * (rgb0 rgb1 0 0, stif_upsample_image); by0..wx1: bilinear rows / columns / weights of the
+ * image at every HR query row / column (as in stif_dec_tables). */
+typedef struct {
+  const float* img;
+  int ih, iw;
+  const int* by0; const int* by1; const float* wy0; const float* wy1;
+  const int* bx0; const int* bx1; const float* wx0; const float* wx1;
+} stif_dec_image;
 
 /* Stage 1 (per HR pixel): feat_imnet -> HRfeat [n,HH,WW,64]; flow_imnet -> flow [n,HH,WW,4].
  * proj: [n,h,w,256] LR projections (P1 | P2 | P3 | P4) from stif_conv2d_nhwc (1x1, packed by
  * stif_pack_dec_proj).  mlp: packed by stif_pack_dec_mlp.  t: [n] query time per item. */
-int stif_dec_stage1(const float* proj, const float* mlp, const stif_dec_tables* tab, const float* t,
-                    float* hrfeat, float* flow, int n, int h, int w, int HH, int WW, void* stream);
+int stif_dec_stage1(const float* proj, const float* mlp, const stif_dec_tables* tab, const stif_dec_image* img,
+                    const float* t, float* hrfeat, float* flow, int n, int h, int w, int HH, int WW, void* stream);
 
 /* Stage 2 (per HR pixel): warp grids from flow, bilinear HRfeat / projections, encode_imnet
  * -> RGB, written NCHW [n,3,HH,WW] (LunaTokis output layout, unclamped). */
 int stif_dec_stage2(const float* proj, const float* mlp, const float* hrfeat, const float* flow,
-                    const stif_dec_tables* tab, const float* t, float* out_nchw,
+                    const stif_dec_tables* tab, const stif_dec_image* img, const float* t, float* out_nchw,
                     int n, int h, int w, int HH, int WW, void* stream);
 
+/* out = sum_k pred_k * wgt_k (per HR pixel weights [HH*WW], shared by the n items): the
+ * local ensemble's area blend (Sakuya_arch_test.py:1076-1084). pred_k / out: [n][3][HH][WW]. */
+int stif_dec_blend4(const float* const* pred, const float* const* wgt, float* out, int n, int HH, int WW,
+                    void* stream);
+
+/* HRinp for decoding_test: F.upsample(x, scale_factor=s, mode='bilinear') (align_corners=False)
+ * of the NCHW pair x [n][2][3][h][w] as NHWC [n][s*h][s*w][8] (rgb0 rgb1 0 0). */
+int stif_upsample_image(const float* x_nchw, float* out, int n, int h, int w, int s, void* stream);
+
 /* ---- host-side weight packing (pure CPU, callable without a GPU) ---- */
-enum { STIF_PACK_PLAIN = 0, STIF_PACK_OFFMASK = 1, STIF_PACK_LSTM = 2, STIF_PACK_WINO = 3 };
+enum { STIF_PACK_PLAIN = 0, STIF_PACK_OFFMASK = 1, STIF_PACK_LSTM = 2, STIF_PACK_WINO = 3, STIF_PACK_WINO_OFFMASK = 4 };
 
 /* Size in floats of a packed conv weight / bias for a packing mode. */
 size_t stif_conv_weight_floats(int cout, int cin, int ks, int mode);
@@ -168,13 +193,17 @@ size_t stif_conv_bias_floats(int cout, int mode);
  * STIF_PACK_WINO (3x3 only, for stif_conv3x3_wino): the Winograd-domain weights U = G g G^T
  * (F(2x2,3x3), computed in double) as [cout/64][cin/8][i 4][j 4][nt 2][lane 64][4], lane l of
  * (i, j, nt) holding U[i][j] of cout slice*64 + nt*32 + (l & 31), input channel
- * chunk*8 + 4(l >> 5) + e; cout padded to a multiple of 64. */
+ * chunk*8 + 4(l >> 5) + e; cout padded to a multiple of 64.  STIF_PACK_WINO_OFFMASK: the same
+ * with the OFFMASK row permutation (216 -> 256 rows). */
 int stif_pack_conv_weight(const float* w_oihw, const float* b, int cout, int cin, int ks, int mode,
                           float* w_dst, float* b_dst);
 
 size_t stif_dec_proj_floats(void);   /* packed 1x1 weight of the LR projection: [25][256][1][8] */
 int stif_pack_dec_proj(const float* feat_w0, const float* feat_b0, const float* flow_w0,
                        const float* enc_w0, float* w_dst, float* b_dst);
+/* lr_image = 0: P2..P4 without the image columns (decoding_test samples a high-resolution image) */
+int stif_pack_dec_proj_ex(const float* feat_w0, const float* feat_b0, const float* flow_w0,
+                          const float* enc_w0, int lr_image, float* w_dst, float* b_dst);
 size_t stif_dec_mlp_floats(void);
 /* Packs every remaining feat/flow/encode_imnet weight (state-dict shapes, see stif_amd.weights)
  * in the order stif_dec_stage1/2 consume them. Pointers follow the Siren layer order:

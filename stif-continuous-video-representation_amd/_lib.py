@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("STIF_HIP_LIB") or os.path.join(os.path.dirname(os.pat
 
 MAXG = 8
 EPI_NONE, EPI_LRELU, EPI_RELU, EPI_RES, EPI_OFFMASK, EPI_LSTM = range(6)
-PACK_PLAIN, PACK_OFFMASK, PACK_LSTM, PACK_WINO = range(4)
+PACK_PLAIN, PACK_OFFMASK, PACK_LSTM, PACK_WINO, PACK_WINO_OFFMASK = range(5)
 
 _P = C.c_void_p
 _PA = _P * MAXG
@@ -42,7 +42,12 @@ class DcnArgs(C.Structure):
 
 class DecTables(C.Structure):
     _fields_ = [(n, _P) for n in ("near_y", "rel_y", "by0", "by1", "wy0", "wy1", "lin_y",
-                                  "near_x", "rel_x", "bx0", "bx1", "wx0", "wx1", "lin_x")]
+                                  "near_x", "rel_x", "bx0", "bx1", "wx0", "wx1", "lin_x", "hr_y", "hr_x")]
+
+
+class DecImage(C.Structure):
+    _fields_ = [("img", _P), ("ih", C.c_int), ("iw", C.c_int)] + [
+        (n, _P) for n in ("by0", "by1", "wy0", "wy1", "bx0", "bx1", "wx0", "wx1")]
 
 
 EXPORTS = {
@@ -56,8 +61,13 @@ EXPORTS = {
     "stif_dcn_v2_workspace_size": (C.c_size_t, [C.c_int] * 14),
     "stif_dcn_v2_forward": (C.c_int, [_P] * 6 + [C.c_int] * 14 + [_P, C.c_size_t, _P]),
     "stif_dec_pack_lr": (C.c_int, [_P, _P, _P, _P, _P, C.c_int, C.c_int, C.c_int, _P]),
-    "stif_dec_stage1": (C.c_int, [_P, _P, C.POINTER(DecTables), _P, _P, _P] + [C.c_int] * 5 + [_P]),
-    "stif_dec_stage2": (C.c_int, [_P, _P, _P, _P, C.POINTER(DecTables), _P, _P] + [C.c_int] * 5 + [_P]),
+    "stif_dec_stage1": (C.c_int, [_P, _P, C.POINTER(DecTables), C.POINTER(DecImage), _P, _P, _P] + [C.c_int] * 5
+                        + [_P]),
+    "stif_dec_stage2": (C.c_int, [_P, _P, _P, _P, C.POINTER(DecTables), C.POINTER(DecImage), _P, _P]
+                        + [C.c_int] * 5 + [_P]),
+    "stif_dec_blend4": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_int, _P]),
+    "stif_upsample_image": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P]),
+    "stif_pack_dec_proj_ex": (C.c_int, [_P, _P, _P, _P, C.c_int, _P, _P]),
     "stif_conv_weight_floats": (C.c_size_t, [C.c_int, C.c_int, C.c_int, C.c_int]),
     "stif_conv_bias_floats": (C.c_size_t, [C.c_int, C.c_int]),
     "stif_pack_conv_weight": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P]),

@@ -41,11 +41,15 @@ def _unnorm(c: np.ndarray, size: int) -> np.ndarray:
     return ((c + F32(1)) * F32(size) - F32(1)) / F32(2)
 
 
-def axis_table(n_lr: int, n_hr: int) -> dict:
-    """Per-HR-index sampling data along one axis (rows: n = H, HH; cols: n = W, WW)."""
+def axis_table(n_lr: int, n_hr: int, shift: float = 0.0) -> dict:
+    """Per-HR-index sampling data along one axis (rows: n = H, HH; cols: n = W, WW).
+    shift: the local ensemble's query offset v * (2 / n_lr / 2) + 1e-6 (Sakuya_arch_test.py:
+    994-998), added in fp32 and re-clamped; rel_coord keeps the unshifted query (:1000-1002) and
+    ``hr`` is the HR pixel nearest to the shifted query (grid_sample nearest of HRfeat, :1022)."""
     c = np.clip(make_coord_1d(n_hr), LO, HI)
+    s = c if shift == 0.0 else np.clip((c + F32(shift)).astype(F32), LO, HI)
     lr_c = make_coord_1d(n_lr)
-    src = _unnorm(c, n_lr)
+    src = _unnorm(s, n_lr)
     near = np.clip(np.rint(src), 0, n_lr - 1).astype(np.int32)      # nearest (round half even)
     rel = ((c - lr_c[near]) * F32(n_lr)).astype(F32)                  # rel_coord (:394-396)
     f0 = np.floor(src)
@@ -60,12 +64,15 @@ def axis_table(n_lr: int, n_hr: int) -> dict:
         b0=np.clip(i0, 0, n_lr - 1).astype(np.int32), b1=np.clip(i1, 0, n_lr - 1).astype(np.int32),
         w0=np.where(v0, w0, F32(0)).astype(F32), w1=np.where(v1, w1, F32(0)).astype(F32),
         lin=linspace_f32(n_hr),
+        hr=np.clip(np.rint(_unnorm(s, n_hr)), 0, n_hr - 1).astype(np.int32),
     )
 
 
-def dec_tables(h: int, w: int, HH: int, WW: int) -> dict:
-    ty = axis_table(h, HH)
-    tx = axis_table(w, WW)
+def dec_tables(h: int, w: int, HH: int, WW: int, shift=None) -> dict:
+    """Tables of one decode; shift = (vx, vy) of the local ensemble (rows move by vx/h, cols by vy/w)."""
+    sy, sx = (0.0, 0.0) if shift is None else (shift[0] * (2 / h / 2) + 1e-6, shift[1] * (2 / w / 2) + 1e-6)
+    ty = axis_table(h, HH, sy)
+    tx = axis_table(w, WW, sx)
     out = {}
     for k, v in ty.items():
         out[("near" if k == "near" else k) + "_y"] = v
@@ -76,3 +83,16 @@ def dec_tables(h: int, w: int, HH: int, WW: int) -> dict:
 
 TABLE_ORDER = ["near_y", "rel_y", "b0_y", "b1_y", "w0_y", "w1_y", "lin_y",
                "near_x", "rel_x", "b0_x", "b1_x", "w0_x", "w1_x", "lin_x"]
+
+
+def ensemble_weights(h: int, w: int, HH: int, WW: int) -> list:
+    """Per-HR-pixel blend weights of decoding_localensemble (:1003-1004, 1075-1084), in fp32 and the
+    reference's order: area_k = |rel_y rel_x| + 1e-9 for shifts (vx, vy) in (-1,-1), (-1,1), (1,-1),
+    (1,1); tot = sum of the four; decode k is weighted by the diagonally opposite area / tot."""
+    areas = []
+    for vx in (-1, 1):
+        for vy in (-1, 1):
+            t = dec_tables(h, w, HH, WW, (vx, vy))
+            areas.append((np.abs(np.outer(t["rel_y"], t["rel_x"]).astype(F32)) + F32(1e-9)).astype(F32))
+    tot = (((areas[0] + areas[1]).astype(F32) + areas[2]).astype(F32) + areas[3]).astype(F32)
+    return [(areas[3 - k] / tot).astype(F32) for k in range(4)]

@@ -34,7 +34,16 @@ constexpr int E_W3 = E_B2 + 256, E_B3 = E_W3 + 64 * T;
 constexpr int E_W4 = E_B3 + 256, E_B4 = E_W4 + 8 * T;
 constexpr int E_END = E_B4 + 32;
 
-constexpr int MLP_FLOATS = E_END;
+// image columns of the first layers as packed 32x32 tiles (K = the 6 image channels, zero padded;
+// only used when the flow / encode stages sample a high-resolution image, decoding_test --
+// otherwise the LR image lives in P2..P4): 4 MFMAs per output tile with the channels as B operand
+constexpr int I_L = E_END;             // flow_imnet.net.0 columns 256..261 (q_inp), 2 tiles
+constexpr int I_E1 = I_L + 2 * T;      // encode_imnet.net.0 columns 512..517 (q_img1)
+constexpr int I_E2 = I_E1 + 2 * T;     // encode_imnet.net.0 columns 518..523 (q_img2)
+constexpr int I_END = I_E2 + 2 * T;
+
+constexpr int MLP_FLOATS = I_END;
+constexpr int IMG_C = 8;      // high-resolution image channels: rgb0 rgb1 + 2 zero (16-B aligned pixels)
 constexpr int PROJ_C = 256;   // LR projection channels: P1 | P2 | P3 | P4
 constexpr int SRC_C = 200;    // LR source channels: feat t0|t1|t2 (192) + rgb0 rgb1 (6) + 2 zero
 

@@ -20,6 +20,8 @@
 #include "stif.h"
 #include "abi_util.h"
 
+#include <algorithm>
+
 namespace {
 
 using namespace stif_dec;
@@ -90,6 +92,24 @@ STIF_DEV void gather64(f32x16* dst, const float* __restrict__ base, int stride, 
     }
 }
 
+// z[ot] += W_img . img: the 6 image channels (padded to 8) are one K chunk, so lane half h supplies
+// channels 4h..4h+3 as the B operand of the first 4 MFMAs of a packed tile (features F(e, h), e < 4)
+STIF_DEV void img_mma(f32x16* z, const float* __restrict__ wt, const f32x4 im4, int lane) {
+#pragma unroll
+  for (int ot = 0; ot < 2; ++ot) {
+    const f32x4 w0 = ld4(wt + ot * T + lane * 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) z[ot] = mfma32(w0[e], im4[e], z[ot]);
+  }
+}
+
+// bilinear sample of channels 4h..4h+3 of a [ih][iw][8] high-resolution image
+STIF_DEV f32x4 img_sample(const float* __restrict__ I, const Bilin& b, int hf) {
+  const float* c = I + 4 * hf;
+  return b.w00 * ld4(c + b.o00 * IMG_C) + b.w01 * ld4(c + b.o01 * IMG_C) + b.w10 * ld4(c + b.o10 * IMG_C) +
+         b.w11 * ld4(c + b.o11 * IMG_C);
+}
+
 // ---- weight streaming: a workgroup consumes its MLP weight tiles segment by segment; each segment
 // (a few 4-KB tiles: one layer, or one output tile's K-tiles) is LDS-DMA'd while the previous one
 // is being consumed (double-buffered, one barrier per segment), and every wave reads its A
@@ -126,10 +146,15 @@ STIF_DEV void tile_mma(f32x16& acc, const float* t, const f32x16& x, int lane) {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// MODE 0: feat_imnet + flow_imnet fused (the flow stage reads the pixel's own HRfeat);
+// MODE 1: feat_imnet only; MODE 2: flow_imnet only, reading HRfeat at (hr_y, hr_x) of the query
+// (local ensemble).  HRIMG: the flow stage's image input comes from the high-resolution image.
+template <int MODE, bool HRIMG>
 __global__ __launch_bounds__(DEC_NW * 64) void k_dec1(const float* __restrict__ proj, const float* __restrict__ mlp,
-                                                     stif_dec_tables tb, const float* __restrict__ tq,
-                                                     float* __restrict__ hrfeat, float* __restrict__ flow, int n,
-                                                     int h, int w, int HH, int WW) {
+                                                     stif_dec_tables tb, stif_dec_image im,
+                                                     const float* __restrict__ tq, float* __restrict__ hrfeat,
+                                                     float* __restrict__ flow, int n, int h, int w, int HH,
+                                                     int WW) {
   __shared__ __attribute__((aligned(16))) float wbuf[2 * SEG * T];
   const int lane = threadIdx.x & 63, hf = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
@@ -137,7 +162,11 @@ __global__ __launch_bounds__(DEC_NW * 64) void k_dec1(const float* __restrict__ 
   float* const B1 = wbuf + SEG * T;
   const __amdgpu_buffer_rsrc_t rm = mlp_rsrc(mlp);
   // segment 0: feat layer 1 (4 tiles); segments 1..8: feat layer 2 tile kt + layer 3 (0, kt), (1, kt)
-  dma_tiles<DEC_NW>(B0, rm, F_W1, 4, wv, lane);
+  if (MODE != 2) dma_tiles<DEC_NW>(B0, rm, F_W1, 4, wv, lane);
+  else {   // flow only: flow layers 0 / 1 straight into B1
+    dma_tiles<DEC_NW>(B1, rm, L_W0, 4, wv, lane);
+    dma_tiles<DEC_NW>(B1 + 4 * T, rm, L_W1, 4, wv, lane);
+  }
   const long long total = (long long)n * HH * WW;
   const long long p = ((long long)blockIdx.x * DEC_NW + wv) * 32 + (lane & 31);
   const bool valid = p < total;
@@ -148,6 +177,9 @@ __global__ __launch_bounds__(DEC_NW * 64) void k_dec1(const float* __restrict__ 
   const float t = tq[item];
   const float* P = proj + (size_t)item * h * w * PROJ_C;
 
+  f32x16 hr[2] = {f32x16{0}, f32x16{0}};
+  f32x16 x1[2];
+  if constexpr (MODE != 2) {
   // ---- feat_imnet layer 0: z = P1[nearest] + w_rel . rel + w_t * t  (bias folded into P1)
   f32x16 x0[2];
   {
@@ -171,7 +203,6 @@ __global__ __launch_bounds__(DEC_NW * 64) void k_dec1(const float* __restrict__ 
   lds_dma_barrier();
   seg_feat23(B1, 0);
   // ---- layer 1: 64 -> 64
-  f32x16 x1[2];
 #pragma unroll
   for (int ot = 0; ot < 2; ++ot) {
     f32x16 acc = f32x16{0};
@@ -180,7 +211,6 @@ __global__ __launch_bounds__(DEC_NW * 64) void k_dec1(const float* __restrict__ 
     x1[ot] = bias_sin(acc, mlp + F_B1 + ot * 32, hf);
   }
   // ---- layer 2 (64 -> 256, sine) streamed into layer 3 (256 -> 64, linear)
-  f32x16 hr[2] = {f32x16{0}, f32x16{0}};
 #pragma unroll 1
   for (int kt = 0; kt < 8; ++kt) {
     lds_dma_barrier();
@@ -212,6 +242,17 @@ __global__ __launch_bounds__(DEC_NW * 64) void k_dec1(const float* __restrict__ 
         st4(o + ot * 32 + 8 * v + 4 * hf, s);
       }
   }
+  }   // MODE != 2
+  if constexpr (MODE == 1) return;
+  if constexpr (MODE == 2) {
+    // the query's HRfeat operand: the HR pixel nearest to the shifted query (grid_sample nearest
+    // of HRfeat at coord_, Sakuya_arch_test.py:1022-1025)
+    Bilin b;
+    b.o00 = b.o01 = b.o10 = b.o11 = tb.hr_y[py] * WW + tb.hr_x[px];
+    b.w00 = 1.f;
+    b.w01 = b.w10 = b.w11 = 0.f;
+    gather64(hr, hrfeat + (size_t)item * HH * WW * 64, 64, 0, b, hf);
+  }
 
   // ---- flow_imnet layer 0: W[:, :64] . HRfeat + bilinear(P2 at the HR centre) + w_t * t + b
   f32x16 z[2];
@@ -231,8 +272,16 @@ __global__ __launch_bounds__(DEC_NW * 64) void k_dec1(const float* __restrict__ 
 #pragma unroll
         for (int e = 0; e < 4; ++e) z[ot][4 * v + e] += wt[e] * t + bb[e];
       }
+    if constexpr (HRIMG) {   // q_inp from the high-resolution image (decoding_test :515-518)
+      Bilin bi;
+      const int y0 = im.by0[py], y1 = im.by1[py], x0_ = im.bx0[px], x1_ = im.bx1[px];
+      const float wy0 = im.wy0[py], wy1 = im.wy1[py], wx0 = im.wx0[px], wx1 = im.wx1[px];
+      bi.o00 = y0 * im.iw + x0_; bi.o01 = y0 * im.iw + x1_; bi.o10 = y1 * im.iw + x0_; bi.o11 = y1 * im.iw + x1_;
+      bi.w00 = wx0 * wy0; bi.w01 = wx1 * wy0; bi.w10 = wx0 * wy1; bi.w11 = wx1 * wy1;
+      img_mma(z, mlp + I_L, img_sample(im.img + (size_t)item * im.ih * im.iw * IMG_C, bi, hf), lane);
+    }
   }
-  // flow layers 0/1 live in B1 (prefetched during the last feat segment)
+  // flow layers 0/1 live in B1 (prefetched during the last feat segment, or at the start)
   lds_dma_barrier();
   auto seg_flow23 = [&](float* dst, int kt) {   // W2 rows kt (2 tiles), W3 (kt)
     dma_tiles<DEC_NW>(dst, rm, L_W2 + kt * 2 * T, 2, wv, lane);
@@ -275,10 +324,12 @@ __global__ __launch_bounds__(DEC_NW * 64) void k_dec1(const float* __restrict__ 
   }
 }
 
+template <bool HRIMG>
 __global__ __launch_bounds__(DEC2_NW * 64) void k_dec2(const float* __restrict__ proj, const float* __restrict__ mlp,
                                                      const float* __restrict__ hrfeat, const float* __restrict__ flow,
-                                                     stif_dec_tables tb, const float* __restrict__ tq,
-                                                     float* __restrict__ out, int n, int h, int w, int HH, int WW) {
+                                                     stif_dec_tables tb, stif_dec_image im,
+                                                     const float* __restrict__ tq, float* __restrict__ out, int n,
+                                                     int h, int w, int HH, int WW) {
   __shared__ __attribute__((aligned(16))) float wbuf[2 * SEG * T];
   const int lane = threadIdx.x & 63, hf = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
@@ -331,6 +382,11 @@ __global__ __launch_bounds__(DEC2_NW * 64) void k_dec2(const float* __restrict__
 #pragma unroll
         for (int e = 0; e < 4; ++e) z[ot][4 * v + e] += z2[ot][4 * v + e] + wt[e] * t + bb[e];
       }
+    if constexpr (HRIMG) {   // q_img1 / q_img2 from the high-resolution image (decoding_test :558-583)
+      const float* I = im.img + (size_t)item * im.ih * im.iw * IMG_C;
+      img_mma(z, mlp + I_E1, img_sample(I, bilin(g1x, g1y, im.iw, im.ih), hf), lane);
+      img_mma(z, mlp + I_E2, img_sample(I, bilin(g2x, g2y, im.iw, im.ih), hf), lane);
+    }
     lds_dma_barrier();
     dma_tiles<DEC2_NW>(B1, rm, E_W1, 4, wv, lane);
 #pragma unroll
@@ -419,6 +475,21 @@ __global__ __launch_bounds__(256) void k_pack_lr(const float* __restrict__ f0, c
   }
 }
 
+__global__ __launch_bounds__(256) void k_blend4(const float* __restrict__ p0, const float* __restrict__ p1,
+                                                const float* __restrict__ p2, const float* __restrict__ p3,
+                                                const float* __restrict__ w0, const float* __restrict__ w1,
+                                                const float* __restrict__ w2, const float* __restrict__ w3,
+                                                float* __restrict__ out, long long total, int plane) {
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const int q = (int)(e % plane);
+    float r = p0[e] * w0[q];   // ret = 0 + pred_0 * w_0 + ... in the reference's order (:1082-1084)
+    r += p1[e] * w1[q];
+    r += p2[e] * w2[q];
+    r += p3[e] * w3[q];
+    out[e] = r;
+  }
+}
+
 bool tables_ok(const stif_dec_tables* t) {
   return t && t->near_y && t->rel_y && t->by0 && t->by1 && t->wy0 && t->wy1 && t->lin_y && t->near_x &&
          t->rel_x && t->bx0 && t->bx1 && t->wx0 && t->wx1 && t->lin_x;
@@ -438,26 +509,71 @@ extern "C" int stif_dec_pack_lr(const float* f0, const float* f1, const float* f
   return stif_check_launch("stif_dec_pack_lr");
 }
 
-extern "C" int stif_dec_stage1(const float* proj, const float* mlp, const stif_dec_tables* tab, const float* t,
-                               float* hrfeat, float* flow, int n, int h, int w, int HH, int WW, void* stream) {
-  if (!proj || !mlp || !tables_ok(tab) || !t || !hrfeat || !flow || n < 1 || h < 1 || w < 1 || HH < 2 || WW < 2)
+namespace {
+
+bool image_ok(const stif_dec_image* im) {
+  return !im || (im->img && im->ih > 0 && im->iw > 0 && im->by0 && im->by1 && im->wy0 && im->wy1 && im->bx0 &&
+                 im->bx1 && im->wx0 && im->wx1);
+}
+
+template <int MODE, bool HRIMG>
+void launch_dec1(long long blocks, hipStream_t st, const float* proj, const float* mlp, const stif_dec_tables& tb,
+                 const stif_dec_image& im, const float* t, float* hrfeat, float* flow, int n, int h, int w, int HH,
+                 int WW) {
+  hipLaunchKernelGGL((k_dec1<MODE, HRIMG>), dim3((unsigned)blocks), dim3(DEC_NW * 64), 0, st, proj, mlp, tb, im, t,
+                     hrfeat, flow, n, h, w, HH, WW);
+}
+
+}  // namespace
+
+extern "C" int stif_dec_stage1(const float* proj, const float* mlp, const stif_dec_tables* tab,
+                               const stif_dec_image* img, const float* t, float* hrfeat, float* flow, int n, int h,
+                               int w, int HH, int WW, void* stream) {
+  if (!proj || !mlp || !tables_ok(tab) || !image_ok(img) || !t || !hrfeat || !flow || n < 1 || h < 1 || w < 1 ||
+      HH < 2 || WW < 2 || (!tab->hr_y) != (!tab->hr_x))
     return stif_fail(STIF_E_INVALID, "stif_dec_stage1: bad arguments");
   const long long total = (long long)n * HH * WW;
   const long long blocks = (total + DEC_NW * 32 - 1) / (DEC_NW * 32);
-  hipLaunchKernelGGL(k_dec1, dim3((unsigned)blocks), dim3(DEC_NW * 64), 0, (hipStream_t)stream, proj, mlp, *tab, t, hrfeat,
-                     flow, n, h, w, HH, WW);
+  hipStream_t st = (hipStream_t)stream;
+  const stif_dec_image im = img ? *img : stif_dec_image{};
+  if (tab->hr_y) {   // remapped HRfeat operand: the whole HRfeat map first, then the flow stage
+    launch_dec1<1, false>(blocks, st, proj, mlp, *tab, im, t, hrfeat, flow, n, h, w, HH, WW);
+    if (img) launch_dec1<2, true>(blocks, st, proj, mlp, *tab, im, t, hrfeat, flow, n, h, w, HH, WW);
+    else launch_dec1<2, false>(blocks, st, proj, mlp, *tab, im, t, hrfeat, flow, n, h, w, HH, WW);
+  } else if (img) {
+    launch_dec1<0, true>(blocks, st, proj, mlp, *tab, im, t, hrfeat, flow, n, h, w, HH, WW);
+  } else {
+    launch_dec1<0, false>(blocks, st, proj, mlp, *tab, im, t, hrfeat, flow, n, h, w, HH, WW);
+  }
   return stif_check_launch("stif_dec_stage1");
 }
 
 extern "C" int stif_dec_stage2(const float* proj, const float* mlp, const float* hrfeat, const float* flow,
-                               const stif_dec_tables* tab, const float* t, float* out, int n, int h, int w, int HH,
-                               int WW, void* stream) {
-  if (!proj || !mlp || !hrfeat || !flow || !tables_ok(tab) || !t || !out || n < 1 || h < 1 || w < 1 || HH < 2 ||
-      WW < 2)
+                               const stif_dec_tables* tab, const stif_dec_image* img, const float* t, float* out, int n,
+                               int h, int w, int HH, int WW, void* stream) {
+  if (!proj || !mlp || !hrfeat || !flow || !tables_ok(tab) || !image_ok(img) || !t || !out || n < 1 || h < 1 ||
+      w < 1 || HH < 2 || WW < 2)
     return stif_fail(STIF_E_INVALID, "stif_dec_stage2: bad arguments");
   const long long total = (long long)n * HH * WW;
   const long long blocks = (total + DEC2_NW * 32 - 1) / (DEC2_NW * 32);
-  hipLaunchKernelGGL(k_dec2, dim3((unsigned)blocks), dim3(DEC2_NW * 64), 0, (hipStream_t)stream, proj, mlp, hrfeat, flow,
-                     *tab, t, out, n, h, w, HH, WW);
+  const stif_dec_image im = img ? *img : stif_dec_image{};
+  if (img)
+    hipLaunchKernelGGL((k_dec2<true>), dim3((unsigned)blocks), dim3(DEC2_NW * 64), 0, (hipStream_t)stream, proj, mlp,
+                       hrfeat, flow, *tab, im, t, out, n, h, w, HH, WW);
+  else
+    hipLaunchKernelGGL((k_dec2<false>), dim3((unsigned)blocks), dim3(DEC2_NW * 64), 0, (hipStream_t)stream, proj,
+                       mlp, hrfeat, flow, *tab, im, t, out, n, h, w, HH, WW);
   return stif_check_launch("stif_dec_stage2");
+}
+
+extern "C" int stif_dec_blend4(const float* const* pred, const float* const* wgt, float* out, int n, int HH, int WW,
+                               void* stream) {
+  if (!pred || !wgt || !out || n < 1 || HH < 1 || WW < 1) return stif_fail(STIF_E_INVALID, "stif_dec_blend4: bad arguments");
+  for (int k = 0; k < 4; ++k)
+    if (!pred[k] || !wgt[k]) return stif_fail(STIF_E_INVALID, "stif_dec_blend4: null input");
+  const long long total = (long long)n * 3 * HH * WW;
+  const long long blocks = std::min<long long>((total + 255) / 256, 1 << 16);
+  hipLaunchKernelGGL(k_blend4, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, pred[0], pred[1], pred[2],
+                     pred[3], wgt[0], wgt[1], wgt[2], wgt[3], out, total, HH * WW);
+  return stif_check_launch("stif_dec_blend4");
 }

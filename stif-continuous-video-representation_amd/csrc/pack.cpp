@@ -82,35 +82,41 @@ void column(float* dst, const float* W, int ld, int rows, int col) {
 }  // namespace
 
 extern "C" size_t stif_conv_weight_floats(int cout, int cin, int ks, int mode) {
-  if (mode == STIF_PACK_WINO) return (size_t)round64(cout) * cin * 16;
+  if (mode == STIF_PACK_WINO || mode == STIF_PACK_WINO_OFFMASK) return (size_t)round64(cout) * cin * 16;
   return (size_t)cout_padded(cout, mode) * cin * ks * ks;
 }
 
 extern "C" size_t stif_conv_bias_floats(int cout, int mode) {
-  return mode == STIF_PACK_WINO ? (size_t)round64(cout) : (size_t)cout_padded(cout, mode);
+  return (mode == STIF_PACK_WINO || mode == STIF_PACK_WINO_OFFMASK) ? (size_t)round64(cout)
+                                                                     : (size_t)cout_padded(cout, mode);
 }
 
 namespace {
 // [slice][chunk][i][j][nt][lane][4]: U[4i+j] of cout slice*64 + nt*32 + (lane & 31), input channel
 // chunk*8 + 4*(lane >> 5) + e -- the B fragments wave i of stif_conv3x3_wino loads per 8-channel chunk
-int pack_wino(const float* w, const float* b, int cout, int cin, float* w_dst, float* b_dst) {
+// perm: output-row permutation of the direct packing (STIF_PACK_PLAIN or STIF_PACK_OFFMASK)
+int pack_wino(const float* w, const float* b, int cout, int cin, int perm, float* w_dst, float* b_dst) {
   const int cp = round64(cout), NS = cp / 64, NC = cin / 8;
   for (int s = 0; s < NS; ++s)
     for (int nt = 0; nt < 2; ++nt)
       for (int l = 0; l < 64; ++l) {
         const int co = s * 64 + nt * 32 + (l & 31);
+        const int sr = src_row(co, cout, perm);
         for (int c = 0; c < NC; ++c)
           for (int e = 0; e < 4; ++e) {
             const int ci = c * 8 + 4 * (l >> 5) + e;
             double u[4][4] = {{0}};
-            if (co < cout) wino_u(w + ((size_t)co * cin + ci) * 9, u);
+            if (sr >= 0) wino_u(w + ((size_t)sr * cin + ci) * 9, u);
             for (int i = 0; i < 4; ++i)
               for (int j = 0; j < 4; ++j)
                 w_dst[((((((size_t)s * NC + c) * 4 + i) * 4 + j) * 2 + nt) * 64 + l) * 4 + e] = (float)u[i][j];
           }
       }
   if (b_dst)
-    for (int j = 0; j < cp; ++j) b_dst[j] = (j < cout && b) ? b[j] : 0.f;
+    for (int j = 0; j < cp; ++j) {
+      const int sr = src_row(j, cout, perm);
+      b_dst[j] = (sr >= 0 && b) ? b[sr] : 0.f;
+    }
   return STIF_OK;
 }
 }  // namespace
@@ -119,11 +125,12 @@ extern "C" int stif_pack_conv_weight(const float* w, const float* b, int cout, i
                                      float* w_dst, float* b_dst) {
   if (!w || !w_dst || cout <= 0 || cin <= 0 || cin % 8 || (ks != 1 && ks != 3))
     return stif_fail(STIF_E_INVALID, "stif_pack_conv_weight: bad arguments");
-  if (mode == STIF_PACK_OFFMASK && cout != 216) return stif_fail(STIF_E_INVALID, "offmask pack needs cout=216");
+  if ((mode == STIF_PACK_OFFMASK || mode == STIF_PACK_WINO_OFFMASK) && cout != 216)
+    return stif_fail(STIF_E_INVALID, "offmask pack needs cout=216");
   if (mode == STIF_PACK_LSTM && cout != 256) return stif_fail(STIF_E_INVALID, "lstm pack needs cout=256");
-  if (mode == STIF_PACK_WINO) {
+  if (mode == STIF_PACK_WINO || mode == STIF_PACK_WINO_OFFMASK) {
     if (ks != 3) return stif_fail(STIF_E_INVALID, "winograd pack needs a 3x3 kernel");
-    return pack_wino(w, b, cout, cin, w_dst, b_dst);
+    return pack_wino(w, b, cout, cin, mode == STIF_PACK_WINO ? STIF_PACK_PLAIN : STIF_PACK_OFFMASK, w_dst, b_dst);
   }
   // layout [slice][chunk][tap][nt][lane][4]: the B fragments of one (slice, chunk) are one
   // contiguous block, copied to LDS by LDS-DMA; lane l of N-tile nt holds cout
@@ -153,8 +160,18 @@ extern "C" int stif_pack_conv_weight(const float* w, const float* b, int cout, i
 
 extern "C" size_t stif_dec_proj_floats(void) { return stif_conv_weight_floats(256, stif_dec::SRC_C, 1, STIF_PACK_PLAIN); }
 
+extern "C" int stif_pack_dec_proj_ex(const float* feat_w0, const float* feat_b0, const float* flow_w0,
+                                     const float* enc_w0, int lr_image, float* w_dst, float* b_dst);
+
 extern "C" int stif_pack_dec_proj(const float* feat_w0, const float* feat_b0, const float* flow_w0,
                                   const float* enc_w0, float* w_dst, float* b_dst) {
+  return stif_pack_dec_proj_ex(feat_w0, feat_b0, flow_w0, enc_w0, 1, w_dst, b_dst);
+}
+
+// lr_image = 0 (decoding_test): P2..P4 leave the image columns out -- the flow / encode stages then
+// sample the x4-upsampled frames themselves (stif_dec_image); P1 always folds the nearest LR image.
+extern "C" int stif_pack_dec_proj_ex(const float* feat_w0, const float* feat_b0, const float* flow_w0,
+                                     const float* enc_w0, int lr_image, float* w_dst, float* b_dst) {
   // P1 = feat_imnet.net.0 on [q_feat(192) | q_inp(6)] + bias        (Sakuya_arch_test.py:399)
   // P2 = flow_imnet.net.0 on [q_feat0(192) | q_inp(6)]             (:418, input cols 64..261)
   // P3 = encode_imnet.net.0 on [q_feat3(192) | q_img1(6)]          (:455, cols 128..319, 512..517)
@@ -166,13 +183,13 @@ extern "C" int stif_pack_dec_proj(const float* feat_w0, const float* feat_b0, co
   for (int o = 0; o < 64; ++o) {
     for (int c = 0; c < 198; ++c) {
       W[(size_t)o * C + c] = feat_w0[(size_t)o * 201 + c];
-      W[(size_t)(64 + o) * C + c] = flow_w0[(size_t)o * 263 + 64 + c];
+      if (c < 192 || lr_image) W[(size_t)(64 + o) * C + c] = flow_w0[(size_t)o * 263 + 64 + c];
     }
     for (int c = 0; c < 192; ++c) {
       W[(size_t)(128 + o) * C + c] = enc_w0[(size_t)o * 525 + 128 + c];
       W[(size_t)(192 + o) * C + c] = enc_w0[(size_t)o * 525 + 320 + c];
     }
-    for (int c = 0; c < 6; ++c) {
+    for (int c = 0; c < 6 && lr_image; ++c) {
       W[(size_t)(128 + o) * C + 192 + c] = enc_w0[(size_t)o * 525 + 512 + c];
       W[(size_t)(192 + o) * C + 192 + c] = enc_w0[(size_t)o * 525 + 518 + c];
     }
@@ -224,5 +241,9 @@ extern "C" int stif_pack_dec_mlp(const float* const* f, const float* const* l, c
   copy_vec(d + E_B3, e[7], 256, 256);
   pack_tiles(d + E_W4, e[8], 256, 0, 0, 3, 256);
   copy_vec(d + E_B4, e[9], 3, 32);
+  // image columns for the high-resolution-image decoder (decoding_test)
+  pack_tiles(d + I_L, l[0], 263, 0, 256, 64, 6);
+  pack_tiles(d + I_E1, e[0], 525, 0, 512, 64, 6);
+  pack_tiles(d + I_E2, e[0], 525, 0, 518, 64, 6);
   return STIF_OK;
 }

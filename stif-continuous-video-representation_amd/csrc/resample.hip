@@ -53,3 +53,47 @@ extern "C" int stif_upsample2x_nhwc(const float* in, float* out, int n, int h1, 
                      in_item, out_item);
   return stif_check_launch("stif_upsample2x_nhwc");
 }
+
+namespace {
+
+// one thread = one output pixel of the 8-channel image (rgb0 rgb1 0 0)
+__global__ __launch_bounds__(256) void k_up_img(const float* __restrict__ x, float* __restrict__ out, int n, int h,
+                                                int w, int s) {
+  const int H = s * h, W = s * w;
+  const long long total = (long long)n * H * W;
+  const float inv = 1.0f / (float)s;
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const int X = (int)(e % W);
+    long long r = e / W;
+    const int Y = (int)(r % H);
+    const int item = (int)(r / H);
+    // ATen upsample_bilinear2d, align_corners=False, scale_factor given: src = (d + 0.5) / s - 0.5, >= 0
+    const float sy = fmaxf(((float)Y + 0.5f) * inv - 0.5f, 0.f);
+    const float sx = fmaxf(((float)X + 0.5f) * inv - 0.5f, 0.f);
+    const int y0 = min((int)sy, h - 1), x0 = min((int)sx, w - 1);
+    const int y1 = y0 + (y0 < h - 1 ? 1 : 0), x1 = x0 + (x0 < w - 1 ? 1 : 0);
+    const float ly1 = sy - (float)y0, lx1 = sx - (float)x0;
+    const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
+    const float* src = x + (size_t)item * 6 * h * w;
+    float v[8];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      const float* p = src + (size_t)c * h * w;
+      v[c] = ly0 * (lx0 * p[y0 * w + x0] + lx1 * p[y0 * w + x1]) + ly1 * (lx0 * p[y1 * w + x0] + lx1 * p[y1 * w + x1]);
+    }
+    v[6] = v[7] = 0.f;
+    float* o = out + (size_t)e * 8;
+    st4(o, f32x4{v[0], v[1], v[2], v[3]});
+    st4(o + 4, f32x4{v[4], v[5], v[6], v[7]});
+  }
+}
+
+}  // namespace
+
+extern "C" int stif_upsample_image(const float* x_nchw, float* out, int n, int h, int w, int s, void* stream) {
+  if (!x_nchw || !out || n < 1 || h < 1 || w < 1 || s < 1) return stif_fail(STIF_E_INVALID, "stif_upsample_image: bad arguments");
+  const long long total = (long long)n * s * h * s * w;
+  const long long blocks = std::min<long long>((total + 255) / 256, 1 << 20);
+  hipLaunchKernelGGL(k_up_img, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x_nchw, out, n, h, w, s);
+  return stif_check_launch("stif_upsample_image");
+}

@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 
   const int tiles_x = (a.Wo + 31) >> 5;
   const int tiles_y = (a.Ho + WR - 1) / WR;
-  const int slices = a.cout >> 6;
+  const int slices = (a.cout + 63) >> 6;
   const int H = a.H, W = a.W, C0 = a.C0, C1 = a.C1;
   const int NC0 = C0 >> 3;
   const int NC = NC0 + (IN1 ? (C1 >> 3) : 0);
@@ -154,6 +154,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     for (int nt = 0; nt < 2; ++nt) bw[j][nt] = ld4(wsl + (j * 2 + nt) * 256);
   int gp = 0;                      // phases staged so far: buffer of phase gp = gp & 1
   stage(cur, 0, 0);
+#ifdef WINO_EXP_STAGGER
+  // the second workgroup of a CU starts ~half a tile late, so the two workgroups' barrier and
+  // epilogue stretches interleave with each other's MFMA streams instead of coinciding
+  if (blockIdx.x >= gridDim.x / 2) {
+    __builtin_amdgcn_s_sleep(127);
+    __builtin_amdgcn_s_sleep(WINO_EXP_STAGGER);
+  }
+#endif
   lds_dma_barrier();
 
   for (;;) {
@@ -217,14 +225,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       yv[nt][0] = acc[0][nt] + acc[1][nt] + acc[2][nt];
       yv[nt][1] = acc[1][nt] - acc[2][nt] - acc[3][nt];
     }
+    // exchange image: [wave 1|2][nt][b][v 4][lane 64][4] -- a reader lane reads back exactly what
+    // the writer lane of the same index wrote (same accumulator layout), 16-B slots lane-linear
     if (!fin) {
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
-          float* dx = ex + (((wi - 1) * 2 + nt) * 2 + b) * 1024;
+          float* dx = ex + (((wi - 1) * 2 + nt) * 2 + b) * 1024 + lane * 4;
 #pragma unroll
-          for (int r = 0; r < 16; ++r) dx[mfma_row(r, lane) * 32 + tl] = yv[nt][b][r];
+          for (int v = 0; v < 4; ++v)
+            st4(dx + v * 256, f32x4{yv[nt][b][4 * v], yv[nt][b][4 * v + 1], yv[nt][b][4 * v + 2], yv[nt][b][4 * v + 3]});
         }
     }
     // output addressing: register r of this lane is pixel (oy0 + 2(r >> 3) + ar,
@@ -239,7 +250,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       const int oy = cur.oy0 + 2 * (r >> 3) + ar;
       const int ox = cur.ox0 + 2 * ((r & 3) + 8 * ((r >> 2) & 1) + 4 * hf) + b;
       const int co = cur.slice * 64 + nt * 32 + tl;
-      const bool ok = (oy < a.Ho) & (ox < a.Wo);
+      const bool ok = (oy < a.Ho) & (ox < a.Wo) & (co < a.cout);
       return ok ? (unsigned)(((oy * a.Wo + ox) * a.cout + co) * 4) : 0x80000000u;
     };
     __syncthreads();
@@ -248,12 +259,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
-          const float* s1p = ex + ((0 * 2 + nt) * 2 + b) * 1024;   // P_1
-          const float* s2p = ex + ((1 * 2 + nt) * 2 + b) * 1024;   // P_2
+          const float* s1p = ex + ((0 * 2 + nt) * 2 + b) * 1024 + lane * 4;   // P_1
+          const float* s2p = ex + ((1 * 2 + nt) * 2 + b) * 1024 + lane * 4;   // P_2
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int o = mfma_row(r, lane) * 32 + tl;
-            yv[nt][b][r] = fmaf(sg, yv[nt][b][r], s1p[o] + sg * s2p[o]);
+          for (int v = 0; v < 4; ++v) {
+            const f32x4 q1 = ld4(s1p + v * 256), q2 = ld4(s2p + v * 256);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) yv[nt][b][4 * v + e] = fmaf(sg, yv[nt][b][4 * v + e], q1[e] + sg * q2[e]);
           }
         }
     }
@@ -278,6 +290,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
             float y = yv[nt][b][r] + bv;
             if (EPI == STIF_EPI_LRELU) y = lrelu01(y);
             if (EPI == STIF_EPI_RELU) y = fmaxf(y, 0.f);
+            if (EPI == STIF_EPI_OFFMASK && (cur.slice * 64 + nt * 32 + tl) % 3 == 2) y = sigmoidf_(y);
             if (EPI == STIF_EPI_RES) y += rv[nt][b][r];
 #ifdef WINO_EXP_NOEPI
             if (y == 12345.f)
@@ -305,7 +318,8 @@ int num_cus() {
 
 template <int IN1, int EPI>
 int launch(const stif_conv_args& a, hipStream_t st) {
-  const long long tiles = (long long)((a.Wo + 31) / 32) * ((a.Ho + WR - 1) / WR) * (a.cout / 64) * a.ngroups * a.nitems;
+  const long long tiles =
+      (long long)((a.Wo + 31) / 32) * ((a.Ho + WR - 1) / WR) * ((a.cout + 63) / 64) * a.ngroups * a.nitems;
   if (tiles > 0x7fffffff) return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: too many tiles");
   if ((long long)a.H * a.W * std::max(a.C0, std::max(a.C1, a.cout)) * 4 >= 0x7fffffffLL)
     return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: item larger than 2 GB (buffer addressing)");
@@ -326,7 +340,10 @@ extern "C" int stif_conv3x3_wino(const stif_conv_args* pa, void* stream) {
     return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: 3x3 stride-1 'same' convolution only");
   if (a.C0 % 8 || a.C0 <= 0 || (a.in1_mode == 1 && (a.C1 % 8 || a.C1 <= 0)))
     return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: channel counts must be multiples of 8");
-  if (a.cout % 64) return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: cout must be a multiple of 64");
+  if (a.cout % 64 && a.epi != STIF_EPI_OFFMASK)
+    return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: cout must be a multiple of 64");
+  if (a.epi == STIF_EPI_OFFMASK && (a.cout != 216 || a.in1_mode != 0))
+    return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: offset/mask conv must be 64->216");
   if ((a.C0 + (a.in1_mode ? a.C1 : 0)) % (8 * PSUB))
     return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: total input channels must be a multiple of 32");
   if (a.epi == STIF_EPI_RES && !a.res[0]) return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: RES needs res");
@@ -338,6 +355,7 @@ extern "C" int stif_conv3x3_wino(const stif_conv_args* pa, void* stream) {
     case STIF_EPI_RES: return launch<IN1, STIF_EPI_RES>(a, st);          \
     default: break;                                                      \
   }
+  if (a.in1_mode == 0 && a.epi == STIF_EPI_OFFMASK) return launch<0, STIF_EPI_OFFMASK>(a, st);
   if (a.in1_mode == 0) { STIF_WINO_CASE(0) }
   else if (a.in1_mode == 1) { STIF_WINO_CASE(1) }
 #undef STIF_WINO_CASE

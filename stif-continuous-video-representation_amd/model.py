@@ -24,6 +24,7 @@ import torch
 from . import _lib as L
 from . import ops
 from . import weights as W
+from .coords import ensemble_weights
 
 
 def _np(v):
@@ -139,7 +140,7 @@ class LunaTokis:
                     n = f"{prefix}{ln}_{d}"
                     if cin is None:
                         conv(n)
-                        conv(n + ".conv_offset_mask", L.PACK_OFFMASK)
+                        conv(n + ".conv_offset_mask", L.PACK_WINO_OFFMASK if self.winograd else L.PACK_OFFMASK)
                     else:
                         conv(n, wino)
 
@@ -158,15 +159,8 @@ class LunaTokis:
             conv(f"recon_trunk.{i}.conv2", wino)
         # decoder
         lib = L.lib()
-        wd = np.empty(lib.stif_dec_proj_floats(), np.float32)
-        bd = np.empty(lib.stif_conv_bias_floats(256, L.PACK_PLAIN), np.float32)
-        f0 = h["feat_imnet.net.0.linear.weight"]
-        L.check(lib.stif_pack_dec_proj(f0.ctypes.data, h["feat_imnet.net.0.linear.bias"].ctypes.data,
-                                       h["flow_imnet.net.0.linear.weight"].ctypes.data,
-                                       h["encode_imnet.net.0.linear.weight"].ctypes.data,
-                                       wd.ctypes.data, bd.ctypes.data), "stif_pack_dec_proj")
-        lay["dec.proj"] = ops.PackedConv(torch.from_numpy(wd).to(dev), torch.from_numpy(bd).to(dev),
-                                         256, 200, 1, L.PACK_PLAIN)
+        self.layers = lay
+        self._pack_proj(lr_image=True)
 
         def siren_ptrs(prefix, n_sine):
             arrs = []
@@ -182,6 +176,20 @@ class LunaTokis:
         L.check(lib.stif_pack_dec_mlp(fp, lp, ep, mlp.ctypes.data), "stif_pack_dec_mlp")
         lay["dec.mlp"] = torch.from_numpy(mlp).to(dev)
         self.layers = lay
+
+    def _pack_proj(self, lr_image=True):
+        """LR projection of the decoder's first layers (stif_pack_dec_proj_ex); lr_image=False leaves
+        the LR frames out of P2..P4 for decoding_test, which samples the x4-upsampled frames."""
+        h, dev, lib = self._host, self.device, L.lib()
+        wd = np.empty(lib.stif_dec_proj_floats(), np.float32)
+        bd = np.empty(lib.stif_conv_bias_floats(256, L.PACK_PLAIN), np.float32)
+        L.check(lib.stif_pack_dec_proj_ex(h["feat_imnet.net.0.linear.weight"].ctypes.data,
+                                          h["feat_imnet.net.0.linear.bias"].ctypes.data,
+                                          h["flow_imnet.net.0.linear.weight"].ctypes.data,
+                                          h["encode_imnet.net.0.linear.weight"].ctypes.data, int(lr_image),
+                                          wd.ctypes.data, bd.ctypes.data), "stif_pack_dec_proj_ex")
+        self.layers["dec.proj" if lr_image else "dec.proj_hrimg"] = ops.PackedConv(
+            torch.from_numpy(wd).to(dev), torch.from_numpy(bd).to(dev), 256, 200, 1, L.PACK_PLAIN)
 
     # ------------------------------------------------------------------ encoder pieces
     def _empty(self, *shape):
@@ -421,38 +429,98 @@ class LunaTokis:
             raise ValueError("each time query must hold 1 or B values")
         return t.contiguous()
 
-    def decoding(self, times=None, scale=None):
-        """LunaTokis.decoding (:364-459): list over times of [B,3,HH,WW] (unclamped)."""
+    def _tab(self, H, Wd, HH, WW, shift=None):
+        key = (H, Wd, HH, WW, shift)
+        if key not in self._tables:
+            self._tables[key] = ops.DecTablesDev(H, Wd, HH, WW, self.device, shift)
+        return self._tables[key]
+
+    def _projection(self, lr_image=True):
+        """LR projections P1..P4 of the current latent (stage 0 of every decoder variant)."""
         if self._feat is None:
             raise RuntimeError("decoding needs gen_feat first")
-        if times is None:
-            raise ValueError("times must be a list of query times")
         feats, x = self._feat, self.inp
         _, B, H, Wd, _ = feats.shape
-        HH, WW = (H * 4, Wd * 4) if scale is None else (int(scale[0]), int(scale[1]))
-        key = (H, Wd, HH, WW)
-        if key not in self._tables:
-            self._tables[key] = ops.DecTablesDev(H, Wd, HH, WW, self.device)
-        tab = self._tables[key]
         src = self._empty(B, H, Wd, 200)
         ops.dec_pack_lr(feats[0], feats[1], feats[2], x, src)
         proj = self._empty(B, H, Wd, 256)
-        ops.conv2d([dict(layer=self.layers["dec.proj"], in0=src, out=proj)])
+        ops.conv2d([dict(layer=self.layers["dec.proj" if lr_image else "dec.proj_hrimg"], in0=src, out=proj)])
+        return proj
+
+    def _decode(self, proj, times, HH, WW, tab, image=None):
+        B = proj.shape[0]
         mlp = self.layers["dec.mlp"]
         preds = []
         hrf = self._empty(B, HH, WW, 64)
         flow = self._empty(B, HH, WW, 4)
         for tq in times:
             t = self._time_vec(tq, B)
-            ops.dec_stage1(proj, mlp, tab, t, hrf, flow)
+            ops.dec_stage1(proj, mlp, tab, t, hrf, flow, image)
             out = self._empty(B, 3, HH, WW)
-            ops.dec_stage2(proj, mlp, hrf, flow, tab, t, out)
+            ops.dec_stage2(proj, mlp, hrf, flow, tab, t, out, image)
             preds.append(out)
         return preds
 
+    def decoding(self, times=None, scale=None):
+        """LunaTokis.decoding (:364-459): list over times of [B,3,HH,WW] (unclamped)."""
+        if times is None:
+            raise ValueError("times must be a list of query times")
+        proj = self._projection()
+        _, H, Wd, _ = proj.shape
+        HH, WW = (H * 4, Wd * 4) if scale is None else (int(scale[0]), int(scale[1]))
+        return self._decode(proj, times, HH, WW, self._tab(H, Wd, HH, WW))
+
+    def decoding_test(self, times=None, scale=None):
+        """LunaTokis.decoding_test (:461-598), what forward(test=True) returns: the flow and encode
+        stages sample HRinp = F.upsample(inp, x4, bilinear) instead of the LR frames; HH = H * scale
+        (integer scale, default 4).  The reference's q/3 chunking only bounds its memory."""
+        if times is None:
+            raise ValueError("times must be a list of query times")
+        if "dec.proj_hrimg" not in self.layers:
+            self._pack_proj(lr_image=False)
+        proj = self._projection(lr_image=False)
+        _, H, Wd, _ = proj.shape
+        s = 4 if scale is None else int(scale)
+        HH, WW = H * s, Wd * s
+        image = ops.DecImageDev(self.inp, 4, HH, WW)
+        return self._decode(proj, times, HH, WW, self._tab(H, Wd, HH, WW), image)
+
+    def decoding_fasttest(self, times=None, scale=None):
+        """LunaTokis.decoding_fasttest (:863-960): `times` is a list of floats, the latent a batch of
+        one; all times come back as one batch [len(times), 3, HH, WW]."""
+        if self._feat is None:
+            raise RuntimeError("decoding needs gen_feat first")
+        if self._feat.shape[1] != 1:
+            raise ValueError("decoding_fasttest batches the query times: the latent must have batch 1")
+        tq = [torch.tensor([[float(t)]]) for t in times]
+        return torch.cat(self.decoding(tq, scale), 0)
+
+    def decoding_localensemble(self, times=None, scale=None):
+        """LunaTokis.decoding_localensemble (:962-1085): four decodes with the query shifted by
+        (+-1/H, +-1/W), blended per HR pixel by the diagonally opposite |rel_y rel_x| area; batch-1
+        latent, `times` a list of floats -> [len(times), 3, HH, WW]."""
+        if self._feat is None:
+            raise RuntimeError("decoding needs gen_feat first")
+        if self._feat.shape[1] != 1:
+            raise ValueError("decoding_localensemble batches the query times: the latent must have batch 1")
+        proj = self._projection()
+        _, H, Wd, _ = proj.shape
+        HH, WW = (H * 4, Wd * 4) if scale is None else (int(scale[0]), int(scale[1]))
+        key = ("ens", H, Wd, HH, WW)
+        if key not in self._tables:
+            self._tables[key] = [torch.from_numpy(a).to(self.device) for a in ensemble_weights(H, Wd, HH, WW)]
+        wts = self._tables[key]
+        tq = [torch.tensor([[float(t)]]) for t in times]
+        outs = []
+        decs = [torch.cat(self._decode(proj, tq, HH, WW, self._tab(H, Wd, HH, WW, (vx, vy))), 0)
+                for vx in (-1, 1) for vy in (-1, 1)]
+        out = self._empty(len(times), 3, HH, WW)
+        ops.dec_blend4(decs, wts, out)
+        return out
+
     def forward(self, x, times=None, scale=None, test=False, center=None, index=0):
-        """LunaTokis.forward (:1222-1231)."""
-        if test:
-            raise NotImplementedError("decoding_test (test=True) is a later-round decoder variant")
+        """LunaTokis.forward (:1222-1231): decoding, or decoding_test with test=True."""
         self.gen_feat(x)
+        if test:
+            return self.decoding_test(times, scale)
         return self.decoding(times, scale)

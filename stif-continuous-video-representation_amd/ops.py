@@ -105,8 +105,9 @@ def conv2d(groups, *, epi=L.EPI_NONE, in1_mode=0, in1_scale=1.0, stride=None):
     a.H, a.W, a.C0, a.C1 = H, W, C0, C1
     a.in1_mode, a.in1_scale = in1_mode, in1_scale
     a.Ho, a.Wo, a.cout, a.ks, a.stride, a.epi = Ho, Wo, lay.cout, ks, stride, epi
-    wino = lay.mode == L.PACK_WINO
-    if any((g["layer"].mode == L.PACK_WINO) != wino for g in groups):
+    wmodes = (L.PACK_WINO, L.PACK_WINO_OFFMASK)
+    wino = lay.mode in wmodes
+    if any((g["layer"].mode in wmodes) != wino for g in groups):
         raise ValueError("conv2d: groups mix Winograd and direct packings")
     tr = TRACE
     if tr is not None:
@@ -198,13 +199,37 @@ def dcn_v2_forward(input, weight, bias, offset, mask, kernel_h, kernel_w, stride
 
 
 class DecTablesDev:
-    """Device copies of coords.dec_tables(h, w, HH, WW) + the C struct pointing at them."""
+    """Device copies of coords.dec_tables(h, w, HH, WW[, shift]) + the C struct pointing at them.
+    With a shift (local ensemble) the HR remap tables are set too."""
 
-    def __init__(self, h, w, HH, WW, device="cuda"):
-        tab = dec_tables(h, w, HH, WW)
-        self._t = {k: torch.from_numpy(np.ascontiguousarray(tab[k])).to(device) for k in TABLE_ORDER}
-        self.c = L.DecTables(*[self._t[k].data_ptr() for k in TABLE_ORDER])
+    def __init__(self, h, w, HH, WW, device="cuda", shift=None):
+        tab = dec_tables(h, w, HH, WW, shift)
+        keys = TABLE_ORDER + (["hr_y", "hr_x"] if shift is not None else [])
+        self._t = {k: torch.from_numpy(np.ascontiguousarray(tab[k])).to(device) for k in keys}
+        self.c = L.DecTables(*[self._t[k].data_ptr() for k in keys])
         self.shape = (h, w, HH, WW)
+
+
+class DecImageDev:
+    """decoding_test's HRinp: the x`s` bilinear upsample of the frame pair ([n, s*h, s*w, 8] NHWC on
+    the device, stif_upsample_image) and its bilinear tables at the HR query grid (HH, WW)."""
+
+    def __init__(self, x_nchw, s, HH, WW):
+        n, _, _, h, w = x_nchw.shape
+        self.img = torch.empty(n, s * h, s * w, 8, device=x_nchw.device, dtype=torch.float32)
+        L.check(L.lib().stif_upsample_image(_vp(x_nchw), _vp(self.img), n, h, w, s, _stream()), "stif_upsample_image")
+        t = dec_tables(s * h, s * w, HH, WW)
+        keys = ["b0_y", "b1_y", "w0_y", "w1_y", "b0_x", "b1_x", "w0_x", "w1_x"]
+        self._t = {k: torch.from_numpy(np.ascontiguousarray(t[k])).to(x_nchw.device) for k in keys}
+        self.c = L.DecImage(self.img.data_ptr(), s * h, s * w, *[self._t[k].data_ptr() for k in keys])
+
+
+def dec_blend4(preds, weights, out):
+    """out = sum_k preds[k] * weights[k] (per HR pixel), the local ensemble's area blend."""
+    n, _, HH, WW = out.shape
+    pp = (C.c_void_p * 4)(*[_vp(p) for p in preds])
+    ww = (C.c_void_p * 4)(*[_vp(w_) for w_ in weights])
+    L.check(L.lib().stif_dec_blend4(pp, ww, _vp(out), n, HH, WW, _stream()), "stif_dec_blend4")
 
 
 def dec_pack_lr(f0, f1, f2, x, out):
@@ -213,25 +238,26 @@ def dec_pack_lr(f0, f1, f2, x, out):
             "stif_dec_pack_lr")
 
 
-def dec_stage1(proj, mlp, tables: DecTablesDev, t, hrfeat, flow):
+def dec_stage1(proj, mlp, tables: DecTablesDev, t, hrfeat, flow, image: "DecImageDev" = None):
     n, h, w, _ = proj.shape
     HH, WW = hrfeat.shape[1:3]
     tr = TRACE
     if tr is not None:   # executed MFMA work: 1,088 v_mfma_f32_32x32x2_f32 per 32 HR pixels
         tr.begin(("dec1",), 1088 / 32 * 4096.0 * n * HH * WW)
-    L.check(L.lib().stif_dec_stage1(_vp(proj), _vp(mlp), C.byref(tables.c), _vp(t), _vp(hrfeat), _vp(flow), n, h, w,
-                                    HH, WW, _stream()), "stif_dec_stage1")
+    L.check(L.lib().stif_dec_stage1(_vp(proj), _vp(mlp), C.byref(tables.c), C.byref(image.c) if image else None,
+                                    _vp(t), _vp(hrfeat), _vp(flow), n, h, w, HH, WW, _stream()), "stif_dec_stage1")
     if tr is not None:
         tr.end()
 
 
-def dec_stage2(proj, mlp, hrfeat, flow, tables: DecTablesDev, t, out):
+def dec_stage2(proj, mlp, hrfeat, flow, tables: DecTablesDev, t, out, image: "DecImageDev" = None):
     n, h, w, _ = proj.shape
     HH, WW = hrfeat.shape[1:3]
     tr = TRACE
     if tr is not None:   # executed MFMA work: 1,600 v_mfma_f32_32x32x2_f32 per 32 HR pixels
         tr.begin(("dec2",), 1600 / 32 * 4096.0 * n * HH * WW)
-    L.check(L.lib().stif_dec_stage2(_vp(proj), _vp(mlp), _vp(hrfeat), _vp(flow), C.byref(tables.c), _vp(t),
-                                    _vp(out), n, h, w, HH, WW, _stream()), "stif_dec_stage2")
+    L.check(L.lib().stif_dec_stage2(_vp(proj), _vp(mlp), _vp(hrfeat), _vp(flow), C.byref(tables.c),
+                                    C.byref(image.c) if image else None, _vp(t), _vp(out), n, h, w, HH, WW,
+                                    _stream()), "stif_dec_stage2")
     if tr is not None:
         tr.end()

@@ -131,3 +131,60 @@ def test_direct_conv_path_matches_reference(stif, sd, golden):
     for i, o in enumerate(outs):
         ok, err, mx = close(o[0], g["out"][i])
         assert ok, (i, err, mx)
+
+
+@pytest.fixture(scope="module")
+def latent16(model, golden):
+    x = torch.from_numpy(golden["model_16x20"]["x"]).cuda()
+    with torch.no_grad():
+        model.gen_feat(x)
+    return model
+
+
+def test_forward_test_true_is_decoding_test(model, golden):
+    """forward(test=True) -> decoding_test (Sakuya_arch_test.py:1225-1226, 461-598): flow / encode
+    stages sample the x4 bilinear-upsampled frames."""
+    d = golden["decoders_16x20"]
+    x = torch.from_numpy(golden["model_16x20"]["x"]).cuda()
+    with torch.no_grad():
+        outs = model(x, [torch.tensor([[float(t)]]) for t in d["test_times"]], test=True)
+    for i, o in enumerate(outs):
+        assert tuple(o.shape) == (1, 3, 64, 80)
+        ok, err, mx = close(o[0], d["test_out"][i])
+        assert ok, (i, err, mx)
+
+
+def test_decoding_test_scale3(latent16, golden):
+    d = golden["decoders_16x20"]
+    with torch.no_grad():
+        o = latent16.decoding_test([torch.tensor([[0.5]])], 3)[0]
+    assert tuple(o.shape) == (1, 3, 48, 60)
+    ok, err, mx = close(o[0], d["test_out_scale3"])
+    assert ok, (err, mx)
+
+
+@pytest.mark.parametrize("which", ["fast", "fast_40x50"])
+def test_decoding_fasttest(latent16, golden, which):
+    d = golden["decoders_16x20"]
+    with torch.no_grad():
+        if which == "fast":
+            o, ref = latent16.decoding_fasttest([float(t) for t in d["fast_times"]]), d["fast_out"]
+        else:
+            o, ref = latent16.decoding_fasttest([0.5], (40, 50)), d["fast_out_40x50"]
+    assert tuple(o.shape) == ref.shape
+    ok, err, mx = close(o, ref)
+    assert ok, (err, mx)
+
+
+@pytest.mark.parametrize("which", ["ens", "ens_40x50"])
+def test_decoding_localensemble(latent16, golden, which):
+    """four shifted decodes (HRfeat read at the shifted query's nearest HR pixel) + area blend"""
+    d = golden["decoders_16x20"]
+    with torch.no_grad():
+        if which == "ens":
+            o, ref = latent16.decoding_localensemble([0.5]), d["ens_out"]
+        else:
+            o, ref = latent16.decoding_localensemble([0.25], (40, 50)), d["ens_out_40x50"]
+    assert tuple(o.shape) == ref.shape
+    ok, err, mx = close(o, ref)
+    assert ok, (err, mx)

@@ -168,3 +168,16 @@ def test_pack_wino_layout(stif):
     got = a.transpose(0, 4, 6, 1, 5, 7, 2, 3).reshape(128, cin, 4, 4)
     assert np.allclose(got, Up, rtol=1e-6, atol=1e-7)
     assert np.array_equal(bd[:cout], b) and not bd[cout:].any()
+
+
+def test_ensemble_tables(stif):
+    """local-ensemble tables: rel_coord from the unshifted query, HR remap within range, weights
+    summing to 1 (the areas of the four shifted queries tile the LR cell)."""
+    C = stif.coords
+    t0 = C.dec_tables(16, 20, 64, 80)
+    t = C.dec_tables(16, 20, 64, 80, (-1, 1))
+    assert (t["hr_y"] >= 0).all() and (t["hr_y"] < 64).all() and (t["hr_x"] < 80).all()
+    assert np.array_equal(t0["hr_y"], np.arange(64)) and np.array_equal(t0["hr_x"], np.arange(80))
+    assert not np.array_equal(t["near_y"], t0["near_y"])
+    w = C.ensemble_weights(16, 20, 64, 80)
+    assert np.allclose(sum(w), 1.0, atol=1e-5)
