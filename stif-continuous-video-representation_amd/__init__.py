@@ -11,6 +11,7 @@ Layout:
   weights.py  state-dict spec + deterministic weight generator
   video.py    custom_video_test-style sliding-window driver
   parallel.py frame-pair sharding over ranks
+  serving.py  option files, define_G / load_network / VideoSRModel (checkpoint drop-in)
 """
 from . import weights  # noqa: F401
 from . import coords  # noqa: F401
@@ -18,7 +19,7 @@ from . import coords  # noqa: F401
 
 def __getattr__(name):
     # torch-dependent parts load lazily so that weight/coords utilities work without torch/GPU
-    if name in ("ops", "model", "dcn_v2", "video", "parallel", "_lib"):
+    if name in ("ops", "model", "dcn_v2", "video", "parallel", "_lib", "serving"):
         import importlib
         return importlib.import_module(f"{__name__}.{name}")
     if name == "LunaTokis":
