@@ -178,6 +178,18 @@ int stif_dec_blend4(const float* const* pred, const float* const* wgt, float* ou
  * of the NCHW pair x [n][2][3][h][w] as NHWC [n][s*h][s*w][8] (rgb0 rgb1 0 0). */
 int stif_upsample_image(const float* x_nchw, float* out, int n, int h, int w, int s, void* stream);
 
+/* ---- video harness I/O (custom_video_test.py:88-103) ---- */
+
+/* data.util.imresize_np(frame, scale, antialiasing) of nf cv2-style uint8 BGR HWC frames [nf][H][W][3]
+ * (separable cubic, symmetric padding; data/util.py:302-371), written as the model input: RGB NCHW
+ * float / 255 [nf][3][oH][oW].  wH [oH][PH], iH [oH] (first symmetric-padded row), sH (top padding)
+ * and the W equivalents come from calculate_weights_indices (stif_amd.video.resize_tables). */
+int stif_resize_frames(const unsigned char* bgr, float* out_rgb_nchw, int nf, int H, int W, int oH, int oW,
+                       const float* wH, const int* iH, int PH, int sH, const float* wW, const int* iW, int PW, int sW,
+                       void* stream);
+/* (clamp(x, 0, 1) * 255).astype(uint8) of NCHW RGB frames [n][3][H][W] -> HWC uint8 [n][H][W][3]. */
+int stif_frames_to_u8(const float* nchw, unsigned char* hwc, int n, int H, int W, void* stream);
+
 /* ---- host-side weight packing (pure CPU, callable without a GPU) ---- */
 enum { STIF_PACK_PLAIN = 0, STIF_PACK_OFFMASK = 1, STIF_PACK_LSTM = 2, STIF_PACK_WINO = 3, STIF_PACK_WINO_OFFMASK = 4 };
 

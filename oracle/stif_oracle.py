@@ -484,3 +484,61 @@ def forward(x, times, sd, scale=None, front_RBs=5, back_RBs=40, dtype=np.float64
     if capture is not None:
         capture["feat"] = feat
     return decoding(feat, x, times, sd, scale, dtype, capture)
+
+
+# ----------------------------------------------------------------------------- harness I/O
+def _cubic(x):
+    """data/util.py:240-246 (fp32)."""
+    ax = np.abs(x).astype(F32)
+    ax2 = (ax * ax).astype(F32)
+    ax3 = (ax2 * ax).astype(F32)
+    a = ((F32(1.5) * ax3 - F32(2.5) * ax2 + F32(1)) * (ax <= 1)).astype(F32)
+    b = ((F32(-0.5) * ax3 + F32(2.5) * ax2 - F32(4) * ax + F32(2)) * ((ax > 1) & (ax <= 2))).astype(F32)
+    return (a + b).astype(F32)
+
+
+def resize_weights_indices(in_len, out_len, scale, antialias=True):
+    """calculate_weights_indices (data/util.py:248-300) in fp32: MATLAB-style cubic weights
+    (widened by 1/scale when downscaling with antialiasing), rows normalised, all-zero edge
+    columns dropped.  Returns (weights [out, P], first index into the symmetric-padded input
+    [out], sym_len_s, sym_len_e)."""
+    kw = 4.0 / scale if (scale < 1 and antialias) else 4.0
+    x = np.linspace(1, out_len, out_len, dtype=np.float64).astype(F32)
+    u = (x / F32(scale) + F32(0.5 * (1 - 1 / scale))).astype(F32)
+    left = np.floor(u - F32(kw / 2)).astype(F32)
+    P = int(np.ceil(kw)) + 2
+    ind = (left[:, None] + np.arange(P, dtype=F32)[None, :]).astype(F32)
+    dist = (u[:, None] - ind).astype(F32)
+    if scale < 1 and antialias:
+        w = (F32(scale) * _cubic((dist * F32(scale)).astype(F32))).astype(F32)
+    else:
+        w = _cubic(dist)
+    w = (w / w.sum(1, dtype=F32)[:, None]).astype(F32)
+    zeros = (w == 0).sum(0)           # counted once, before either narrow (:286-291)
+    if zeros[0] != 0:
+        ind, w = ind[:, 1:P - 1], w[:, 1:P - 1]
+    if zeros[-1] != 0:
+        ind, w = ind[:, :P - 2], w[:, :P - 2]      # a no-op after the first narrow
+    s0 = int(-ind.min() + 1)
+    s1 = int(ind.max() - in_len)
+    return w, (ind[:, 0] + s0 - 1).astype(np.int64), s0, s1
+
+
+def _sym_index(j, n, s0):
+    """row of the symmetric-padded image (data/util.py:325-335) -> source row"""
+    k = j - s0
+    return np.where(k < 0, -k - 1, np.where(k >= n, 2 * n - 1 - k, k))
+
+
+def imresize_np(img, scale, antialias=True, dtype=np.float64):
+    """data/util.py:302-371 imresize_np: HWC image (the harness feeds cv2's uint8 BGR frames),
+    separable cubic resize along H then W with symmetric padding; float output, no rounding."""
+    img = np.asarray(img, dtype)
+    H, W, Cc = img.shape
+    oH, oW = int(np.ceil(H * scale)), int(np.ceil(W * scale))
+    wH, iH, sH, _ = resize_weights_indices(H, oH, scale, antialias)
+    wW, iW, sW, _ = resize_weights_indices(W, oW, scale, antialias)
+    rows = _sym_index(iH[:, None] + np.arange(wH.shape[1])[None, :], H, sH)       # [oH, P]
+    out1 = np.einsum("ip,ipxc->ixc", wH.astype(dtype), img[rows])
+    cols = _sym_index(iW[:, None] + np.arange(wW.shape[1])[None, :], W, sW)       # [oW, P]
+    return np.einsum("jp,ijpc->ijc", wW.astype(dtype), out1[:, cols])

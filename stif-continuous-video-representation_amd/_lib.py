@@ -67,6 +67,9 @@ EXPORTS = {
                         + [C.c_int] * 5 + [_P]),
     "stif_dec_blend4": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_int, _P]),
     "stif_upsample_image": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P]),
+    "stif_resize_frames": (C.c_int, [_P, _P] + [C.c_int] * 5 + [_P, _P, C.c_int, C.c_int, _P, _P, C.c_int, C.c_int,
+                                                                 _P]),
+    "stif_frames_to_u8": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, _P]),
     "stif_pack_dec_proj_ex": (C.c_int, [_P, _P, _P, _P, C.c_int, _P, _P]),
     "stif_conv_weight_floats": (C.c_size_t, [C.c_int, C.c_int, C.c_int, C.c_int]),
     "stif_conv_bias_floats": (C.c_size_t, [C.c_int, C.c_int]),

@@ -97,3 +97,92 @@ extern "C" int stif_upsample_image(const float* x_nchw, float* out, int n, int h
   hipLaunchKernelGGL(k_up_img, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x_nchw, out, n, h, w, s);
   return stif_check_launch("stif_upsample_image");
 }
+
+// ---------------------------------------------------------------- video harness I/O
+// custom_video_test.py:88-92,101-103: frames come in as cv2 uint8 BGR HWC, are resized by
+// data.util.imresize_np(img, 1/2, antialiasing=True) (data/util.py:302-371: separable MATLAB cubic,
+// symmetric padding, H pass then W pass), scaled by 1/255 and flipped to RGB NCHW; outputs go back
+// as (clamp(0,1) * 255).astype(uint8) HWC RGB.
+namespace {
+
+// symmetric-padded index (data/util.py:325-335, 350-360) -> source index
+STIF_DEV int sym_src(int j, int n, int s0) {
+  const int k = j - s0;
+  return k < 0 ? -k - 1 : (k >= n ? 2 * n - 1 - k : k);
+}
+
+// one thread = one output pixel (3 channels) of one frame
+__global__ __launch_bounds__(256) void k_resize_in(const unsigned char* __restrict__ src, float* __restrict__ out,
+                                                   int nf, int H, int W, int oH, int oW,
+                                                   const float* __restrict__ wH, const int* __restrict__ iH, int PH,
+                                                   int sH, const float* __restrict__ wW, const int* __restrict__ iW,
+                                                   int PW, int sW) {
+  const long long total = (long long)nf * oH * oW;
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const int x = (int)(e % oW);
+    long long r = e / oW;
+    const int y = (int)(r % oH);
+    const int f = (int)(r / oH);
+    const unsigned char* img = src + (size_t)f * H * W * 3;
+    float acc[3] = {0.f, 0.f, 0.f};
+    for (int p = 0; p < PW; ++p) {
+      const int sx = sym_src(iW[x] + p, W, sW);
+      float col[3] = {0.f, 0.f, 0.f};   // H pass at column sx (out_1 of the reference)
+      for (int q = 0; q < PH; ++q) {
+        const int sy = sym_src(iH[y] + q, H, sH);
+        const unsigned char* px = img + ((size_t)sy * W + sx) * 3;
+        const float w = wH[y * PH + q];
+        col[0] = fmaf(w, (float)px[0], col[0]);
+        col[1] = fmaf(w, (float)px[1], col[1]);
+        col[2] = fmaf(w, (float)px[2], col[2]);
+      }
+      const float w = wW[x * PW + p];
+      acc[0] = fmaf(w, col[0], acc[0]);
+      acc[1] = fmaf(w, col[1], acc[1]);
+      acc[2] = fmaf(w, col[2], acc[2]);
+    }
+    const size_t plane = (size_t)oH * oW;
+    float* o = out + (size_t)f * 3 * plane + (size_t)y * oW + x;
+    // .astype(float32) / 255, BGR -> RGB
+    o[0] = acc[2] / 255.f;
+    o[plane] = acc[1] / 255.f;
+    o[2 * plane] = acc[0] / 255.f;
+  }
+}
+
+// (img.clamp(0, 1).permute(1, 2, 0) * 255).numpy().astype(np.uint8): NCHW float -> HWC uint8
+__global__ __launch_bounds__(256) void k_to_u8(const float* __restrict__ in, unsigned char* __restrict__ out, int n,
+                                               int H, int W) {
+  const long long total = (long long)n * H * W;
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const long long item = e / ((long long)H * W);
+    const long long yx = e - item * H * W;
+    const float* p = in + (size_t)item * 3 * H * W + yx;
+    unsigned char* o = out + (size_t)e * 3;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) o[c] = (unsigned char)(fminf(fmaxf(p[(size_t)c * H * W], 0.f), 1.f) * 255.f);
+  }
+}
+
+}  // namespace
+
+extern "C" int stif_resize_frames(const unsigned char* bgr, float* out_rgb_nchw, int nf, int H, int W, int oH, int oW,
+                                  const float* wH, const int* iH, int PH, int sH, const float* wW, const int* iW,
+                                  int PW, int sW, void* stream) {
+  if (!bgr || !out_rgb_nchw || !wH || !iH || !wW || !iW || nf < 1 || H < 1 || W < 1 || oH < 1 || oW < 1 || PH < 1 ||
+      PW < 1 || sH < 1 || sW < 1 || sH > H || sW > W)
+    return stif_fail(STIF_E_INVALID, "stif_resize_frames: bad arguments");
+  const long long total = (long long)nf * oH * oW;
+  const long long blocks = std::min<long long>((total + 255) / 256, 1 << 20);
+  hipLaunchKernelGGL(k_resize_in, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, bgr, out_rgb_nchw, nf, H,
+                     W, oH, oW, wH, iH, PH, sH, wW, iW, PW, sW);
+  return stif_check_launch("stif_resize_frames");
+}
+
+extern "C" int stif_frames_to_u8(const float* nchw, unsigned char* hwc, int n, int H, int W, void* stream) {
+  if (!nchw || !hwc || n < 1 || H < 1 || W < 1) return stif_fail(STIF_E_INVALID, "stif_frames_to_u8: bad arguments");
+  const long long total = (long long)n * H * W;
+  const long long blocks = std::min<long long>((total + 255) / 256, 1 << 20);
+  hipLaunchKernelGGL(k_to_u8, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, nchw, hwc, n, H, W);
+  return stif_check_launch("stif_frames_to_u8");
+}

@@ -21,6 +21,7 @@ with ``load_state_dict(strict=True)``.
 
 Usage:  python tests/golden/make_golden.py             (model, window and per-op fixtures)
         python tests/golden/make_golden.py decoders    (decoding_test / _fasttest / _localensemble)
+        python tests/golden/make_golden.py harness     (custom_video_test's imresize_np input resize)
 """
 import json
 import os
@@ -286,8 +287,35 @@ def decoders():
     print("decoders:", {k: v.shape for k, v in res.items()})
 
 
+def harness():
+    """custom_video_test.py's input resize: data.util.imresize_np(img_uint8_bgr, 1/2, True)
+    (data/util.py:240-371) on cv2-style uint8 HWC frames -> harness.npz"""
+    if not os.path.isdir(REF):
+        print("reference absent; nothing to do")
+        return
+    install_shims()
+    # data/util.py imports cv2 at module level; imresize_np itself is pure torch (stub only)
+    sys.modules.setdefault("cv2", types.ModuleType("cv2"))
+    from data.util import imresize_np, calculate_weights_indices
+    rng = np.random.default_rng(77)
+    res = {}
+    for (h, w) in [(37, 50), (64, 90), (21, 33)]:
+        img = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
+        res[f"img_{h}x{w}"] = img
+        res[f"half_{h}x{w}"] = imresize_np(img, 1 / 2, True).astype(np.float32)
+    wts, idx, s0, s1 = calculate_weights_indices(37, 19, 0.5, "cubic", 4, True)
+    res["w_37_19"] = wts.numpy().astype(np.float32)
+    res["i_37_19"] = idx.numpy().astype(np.int64)
+    res["sym_37_19"] = np.array([s0, s1], np.int64)
+    np.savez_compressed(os.path.join(HERE, "harness.npz"), **res)
+    print("harness:", {k: v.shape for k, v in res.items()})
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["decoders"]:
         decoders()
+        sys.exit(0)
+    if sys.argv[1:] == ["harness"]:
+        harness()
         sys.exit(0)
     main()

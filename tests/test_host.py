@@ -181,3 +181,10 @@ def test_ensemble_tables(stif):
     assert not np.array_equal(t["near_y"], t0["near_y"])
     w = C.ensemble_weights(16, 20, 64, 80)
     assert np.allclose(sum(w), 1.0, atol=1e-5)
+
+
+def test_resize_tables_match_reference(stif):
+    """video.resize_tables = calculate_weights_indices (data/util.py:248-300), fixture from the reference"""
+    h = np.load(os.path.join(REPO, "tests", "golden", "harness.npz"))
+    w, i0, s0 = stif.video.resize_tables(37, 19, 0.5)
+    assert np.array_equal(w, h["w_37_19"]) and np.array_equal(i0, h["i_37_19"][:, 0]) and s0 == h["sym_37_19"][0]

@@ -1,5 +1,7 @@
 """The CPU oracle against the golden fixtures produced by the reference itself
 (tests/golden/make_golden.py).  CPU only."""
+import os
+
 import numpy as np
 import pytest
 
@@ -121,3 +123,13 @@ def test_oracle_decoder_variants_match_reference(sd, golden, which):
     else:
         got, ref = O.decoding_localensemble(feat, x, [0.25], sd, (40, 50)), d["ens_out_40x50"]
     assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max()
+
+
+def test_oracle_imresize_matches_reference():
+    """data.util.imresize_np(uint8 BGR frame, 1/2, True) restatement vs the reference's outputs."""
+    h = np.load(os.path.join(os.path.dirname(__file__), "golden", "harness.npz"))
+    w, i0, s0, s1 = O.resize_weights_indices(37, 19, 0.5)
+    assert np.array_equal(w, h["w_37_19"]) and np.array_equal(i0, h["i_37_19"][:, 0])
+    assert (s0, s1) == tuple(h["sym_37_19"])
+    for k in ("37x50", "64x90", "21x33"):
+        assert np.abs(O.imresize_np(h["img_" + k], 0.5) - h["half_" + k]).max() < 1e-3
