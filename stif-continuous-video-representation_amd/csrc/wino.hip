@@ -18,7 +18,7 @@
 //   * the B operands U[xi] (packed [slice][chunk][i][j][nt][lane][4]) are per-wave, so they are
 //     loaded straight from L2 into registers, one 8-channel chunk ahead;
 //   * the output transform's sum over j happens in registers (P_i = M_i A), only the sum over
-//     i crosses waves (one LDS exchange per 32-cout half).
+//     i crosses waves (an LDS exchange per 32-cout half, balanced over all 4 waves).
 // Input halo tiles (6 rows x 34 columns x 32 channels per phase) are LDS-DMA'd, double-buffered,
 // even and odd columns in separate runs so a lane's 4 patch columns are conflict-free reads.
 #include "abi_util.h"
@@ -45,6 +45,19 @@ constexpr int WG_PER_CU = 2;
 
 // slot of halo column c in its (row, chunk, half) run: even columns first, then odd
 STIF_DEV int col_slot(int c) { return (c & 1) ? 17 + (c >> 1) : (c >> 1); }
+
+#ifdef WINO_EXP_TRACE
+// per-wave s_memtime event trace (kernel experiment builds only): [block][wave][128 events]
+__device__ unsigned long long g_wtrace[512 * 4 * 128];
+#define WTR(tag)                                                                                   \
+  do {                                                                                             \
+    if (ntr < 128 && blockIdx.x < 512 && lane == 0)                                                \
+      g_wtrace[(blockIdx.x * 4 + wi) * 128 + ntr] = (__builtin_amdgcn_s_memtime() << 8) | (tag);   \
+    ++ntr;                                                                                         \
+  } while (0)
+#else
+#define WTR(tag) do {} while (0)
+#endif
 
 struct Tile {
   int oy0, ox0, slice, g, n;
@@ -145,6 +158,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 
   int T = blockIdx.x;
   if (T >= ntiles) return;
+#ifdef WINO_EXP_TRACE
+  int ntr = 0;
+#endif
   Tile cur = tile_of(T);
   const float* wsl = wbase(cur);
   f32x4 bw[4][2];
@@ -173,6 +189,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     f32x16 acc[4][2];
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[j][0] = acc[j][1] = f32x16{0};
+    WTR(1);
 
     for (int p = 0; p < NP; ++p, ++gp) {
       if (p + 1 < NP) stage(cur, p + 1, (gp + 1) & 1);
@@ -186,7 +203,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 #else
         transform(buf, s, v);
 #endif
-        // B operands of the next chunk (the next tile's first chunk after the last one)
+        // B operands of the next chunk (the next tile's first chunk after the last one).  bw[j] is
+        // reloaded right after its 8 MFMAs, 3/4 of a chunk (24 MFMAs) before its next use; the
+        // scheduling barriers keep the compiler from sinking those loads next to their use,
+        // which would expose the L2 latency on every j block.
         const int kn = p * PSUB + s + 1;
         const float* wn = kn < NC ? wsl + (size_t)kn * 8192 : wnx;
 #pragma unroll
@@ -203,102 +223,98 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
           for (int nt = 0; nt < 2; ++nt) bw[j][nt] += 1.f;
           (void)wn;
 #endif
+          __builtin_amdgcn_sched_barrier(0);
         }
       }
 #ifndef WINO_EXP_NOBAR
-      lds_dma_barrier();
+      // every load older than the last chunk's 8 B-operand prefetches -- the phase's LDS-DMA
+      // among them -- has landed; those 8 stay in flight across the barrier
+      WTR(6);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      __syncthreads();
+      WTR(2);
 #endif
     }
 
-    // ---- output transform: P_i[b] = sum_j M[i][j] A[j][b] (registers); Y[0] = P_0 + P_1 + P_2
-    // (wave 0), Y[1] = P_1 - P_2 - P_3 (wave 3); waves 1 and 2 hand P over through the buffer of
-    // the phase just finished (free after the barrier; the other one is receiving the next tile).
-    // The stores go straight from the accumulator layout: per register, lanes 0-31 / 32-63 write
-    // the 32 couts (128 B) of one output pixel each.
+    // ---- output transform, balanced over the 4 waves.  Wave i holds P_i[b] = sum_j M[i][j] A[j][b]
+    // (registers); Y[0] = P_0 + P_1 + P_2, Y[1] = P_1 - P_2 - P_3.  Two rounds (32-cout halves nt):
+    // every wave writes its P_i[nt] into the buffer of the phase just finished (free after the
+    // barrier; the other one is receiving the next tile) transposed to [i][b][tile][co], then every
+    // thread combines and stores 4 (pixel, 4-cout) vectors as coalesced 16-B accesses (8 lanes =
+    // one pixel's 128 B).  Row swizzle R ^ (bit2(tile) ^ b) keeps both the b32 writes (lane halves
+    // 4 tiles apart) and the b128 reads (16-lane groups = b 0/1 of one tile) conflict-free.
     float* ex = smem + ((gp - 1) & 1) * BUF_F;
-    const bool fin = wi == 0 || wi == 3;
-    const int ar = (wi == 0) ? 0 : 1;
+#ifdef WINO_EXP_PRIO
+    __builtin_amdgcn_s_setprio(1);
+#endif
     f32x16 yv[2][2];   // [nt][b]
-    const float sg = wi == 0 ? 1.f : -1.f;
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
       yv[nt][0] = acc[0][nt] + acc[1][nt] + acc[2][nt];
       yv[nt][1] = acc[1][nt] - acc[2][nt] - acc[3][nt];
     }
-    // exchange image: [wave 1|2][nt][b][v 4][lane 64][4] -- a reader lane reads back exactly what
-    // the writer lane of the same index wrote (same accumulator layout), 16-B slots lane-linear
-    if (!fin) {
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          float* dx = ex + (((wi - 1) * 2 + nt) * 2 + b) * 1024 + lane * 4;
-#pragma unroll
-          for (int v = 0; v < 4; ++v)
-            st4(dx + v * 256, f32x4{yv[nt][b][4 * v], yv[nt][b][4 * v + 1], yv[nt][b][4 * v + 2], yv[nt][b][4 * v + 3]});
-        }
-    }
-    // output addressing: register r of this lane is pixel (oy0 + 2(r >> 3) + ar,
-    // ox0 + 2((r & 3) + 8((r >> 2) & 1) + 4h) + b), cout slice*64 + nt*32 + (lane & 31)
+    auto xrow = [](int i, int b, int m) { return (((i * 2 + b) * 32 + m) ^ (((m >> 2) ^ b) & 1)) * 32; };
+    // this thread's outputs: cout quad c4, column ox of the tile, rows k = 0..3
+    const int c4 = tid & 7, oxl = tid >> 3;
+    const int ox = cur.ox0 + oxl;
+    const int bb = oxl & 1, txo = oxl >> 1;
     const size_t slab = (size_t)a.Ho * a.Wo * a.cout;
     const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(a.out[cur.g] + (size_t)cur.n * a.out_item), (short)0, (int)(slab * 4), 0x00020000);
     const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(EPI == STIF_EPI_RES ? a.res[cur.g] + (size_t)cur.n * a.res_item : a.in0[cur.g]), (short)0,
         (int)(slab * 4), 0x00020000);
-    auto voff = [&](int nt, int b, int r) -> unsigned {
-      const int oy = cur.oy0 + 2 * (r >> 3) + ar;
-      const int ox = cur.ox0 + 2 * ((r & 3) + 8 * ((r >> 2) & 1) + 4 * hf) + b;
-      const int co = cur.slice * 64 + nt * 32 + tl;
+    auto voff = [&](int nt, int k) -> unsigned {
+      const int oy = cur.oy0 + k;
+      const int co = cur.slice * 64 + nt * 32 + c4 * 4;
       const bool ok = (oy < a.Ho) & (ox < a.Wo) & (co < a.cout);
       return ok ? (unsigned)(((oy * a.Wo + ox) * a.cout + co) * 4) : 0x80000000u;
     };
-    __syncthreads();
-    if (fin) {
+    f32x4 rv[2][4];
+    if (EPI == STIF_EPI_RES) {
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          const float* s1p = ex + ((0 * 2 + nt) * 2 + b) * 1024 + lane * 4;   // P_1
-          const float* s2p = ex + ((1 * 2 + nt) * 2 + b) * 1024 + lane * 4;   // P_2
+        for (int k = 0; k < 4; ++k)
+          rv[nt][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, voff(nt, k), 0, 0));
+    }
 #pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            const f32x4 q1 = ld4(s1p + v * 256), q2 = ld4(s2p + v * 256);
+    for (int nt = 0; nt < 2; ++nt) {
+      if (nt) __syncthreads();   // round-0 readers are done with the exchange image
 #pragma unroll
-            for (int e = 0; e < 4; ++e) yv[nt][b][4 * v + e] = fmaf(sg, yv[nt][b][4 * v + e], q1[e] + sg * q2[e]);
-          }
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) ex[xrow(wi, b, mfma_row(r, lane)) + tl] = yv[nt][b][r];
+      __syncthreads();
+      WTR(3);
+      const int cob = cur.slice * 64 + nt * 32 + c4 * 4;
+      const f32x4 bv = cob < a.cout ? ld4(a.bias[cur.g] + cob) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int m = (k >> 1) * 16 + txo;
+        const f32x4 p1 = ld4(ex + xrow(1, bb, m) + c4 * 4), p2 = ld4(ex + xrow(2, bb, m) + c4 * 4);
+        const f32x4 pe = ld4(ex + xrow((k & 1) ? 3 : 0, bb, m) + c4 * 4);
+        f32x4 y = (k & 1) ? (p1 - p2 - pe) : (pe + p1 + p2);
+        y += bv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (EPI == STIF_EPI_LRELU) y[e] = lrelu01(y[e]);
+          if (EPI == STIF_EPI_RELU) y[e] = fmaxf(y[e], 0.f);
+          if (EPI == STIF_EPI_OFFMASK && (cob + e) % 3 == 2) y[e] = sigmoidf_(y[e]);
         }
+        if (EPI == STIF_EPI_RES) y += rv[nt][k];
+#ifdef WINO_EXP_NOEPI
+        if (y[0] == 12345.f)
+#endif
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, y), ro, voff(nt, k), 0, 0);
+      }
     }
     __syncthreads();   // exchange buffer free for the next tile's staging
-    if (fin) {
-      f32x16 rv[2][2];
-      if (EPI == STIF_EPI_RES) {
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-          for (int b = 0; b < 2; ++b)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) rv[nt][b][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, voff(nt, b, r), 0, 0));
-      }
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const float bv = a.bias[cur.g][cur.slice * 64 + nt * 32 + tl];
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            float y = yv[nt][b][r] + bv;
-            if (EPI == STIF_EPI_LRELU) y = lrelu01(y);
-            if (EPI == STIF_EPI_RELU) y = fmaxf(y, 0.f);
-            if (EPI == STIF_EPI_OFFMASK && (cur.slice * 64 + nt * 32 + tl) % 3 == 2) y = sigmoidf_(y);
-            if (EPI == STIF_EPI_RES) y += rv[nt][b][r];
-#ifdef WINO_EXP_NOEPI
-            if (y == 12345.f)
+#ifdef WINO_EXP_PRIO
+    __builtin_amdgcn_s_setprio(0);
 #endif
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ro, voff(nt, b, r), 0, 0);
-          }
-      }
-    }
+    WTR(4);
+    WTR(5);
     if (!has_next) break;
     T = Tn;
     cur = nxt;
@@ -329,6 +345,12 @@ int launch(const stif_conv_args& a, hipStream_t st) {
 }
 
 }  // namespace
+
+#ifdef WINO_EXP_TRACE
+extern "C" int stif_exp_wino_trace(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wtrace), sizeof(g_wtrace)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int stif_conv3x3_wino(const stif_conv_args* pa, void* stream) {
   if (!pa) return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: null args");
