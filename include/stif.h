@@ -75,7 +75,8 @@ int stif_conv2d_nhwc(const stif_conv_args* args, void* stream);
 
 /* The same operator for 3x3 / stride 1 / 'same' shapes by Winograd F(2x2,3x3) on fp32 MFMA
  * (2.25x fewer multiply-adds; all arithmetic fp32): weights packed with STIF_PACK_WINO
- * (epi NONE / LRELU / RELU / RES) or STIF_PACK_WINO_OFFMASK (epi OFFMASK, cout 216);
+ * (epi NONE / LRELU / RELU / RES), STIF_PACK_WINO_OFFMASK (epi OFFMASK, cout 216) or
+ * STIF_PACK_WINO_LSTM (epi LSTM, 128 -> 256: out = h_next, out2 = c_next, res = c_cur, 64-ch maps);
  * in1_mode 0 or 1; total input channels a multiple of 32. */
 int stif_conv3x3_wino(const stif_conv_args* args, void* stream);
 
@@ -191,7 +192,8 @@ int stif_resize_frames(const unsigned char* bgr, float* out_rgb_nchw, int nf, in
 int stif_frames_to_u8(const float* nchw, unsigned char* hwc, int n, int H, int W, void* stream);
 
 /* ---- host-side weight packing (pure CPU, callable without a GPU) ---- */
-enum { STIF_PACK_PLAIN = 0, STIF_PACK_OFFMASK = 1, STIF_PACK_LSTM = 2, STIF_PACK_WINO = 3, STIF_PACK_WINO_OFFMASK = 4 };
+enum { STIF_PACK_PLAIN = 0, STIF_PACK_OFFMASK = 1, STIF_PACK_LSTM = 2, STIF_PACK_WINO = 3, STIF_PACK_WINO_OFFMASK = 4,
+       STIF_PACK_WINO_LSTM = 5 };
 
 /* Size in floats of a packed conv weight / bias for a packing mode. */
 size_t stif_conv_weight_floats(int cout, int cin, int ks, int mode);
@@ -206,7 +208,9 @@ size_t stif_conv_bias_floats(int cout, int mode);
  * (F(2x2,3x3), computed in double) as [cout/64][cin/8][i 4][j 4][nt 2][lane 64][4], lane l of
  * (i, j, nt) holding U[i][j] of cout slice*64 + nt*32 + (l & 31), input channel
  * chunk*8 + 4(l >> 5) + e; cout padded to a multiple of 64.  STIF_PACK_WINO_OFFMASK: the same
- * with the OFFMASK row permutation (216 -> 256 rows). */
+ * with the OFFMASK row permutation (216 -> 256 rows).  STIF_PACK_WINO_LSTM: the same for the
+ * ConvLSTMCell conv (128 -> 256) with packed cout 4h + gate = reference row gate*64 + h (gates
+ * i, f, o, g; convlstm.py:49), so one 4-cout quad holds the four gates of hidden channel h. */
 int stif_pack_conv_weight(const float* w_oihw, const float* b, int cout, int cin, int ks, int mode,
                           float* w_dst, float* b_dst);
 

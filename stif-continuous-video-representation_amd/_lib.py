@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("STIF_HIP_LIB") or os.path.join(os.path.dirname(os.pat
 
 MAXG = 8
 EPI_NONE, EPI_LRELU, EPI_RELU, EPI_RES, EPI_OFFMASK, EPI_LSTM = range(6)
-PACK_PLAIN, PACK_OFFMASK, PACK_LSTM, PACK_WINO, PACK_WINO_OFFMASK = range(5)
+PACK_PLAIN, PACK_OFFMASK, PACK_LSTM, PACK_WINO, PACK_WINO_OFFMASK, PACK_WINO_LSTM = range(6)
 
 _P = C.c_void_p
 _PA = _P * MAXG

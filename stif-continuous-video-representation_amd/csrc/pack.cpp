@@ -44,6 +44,10 @@ int src_row(int j, int cout, int mode) {
     if (e == 1) return g * 18 + 2 * k + 1;
     return 144 + g * 9 + k;
   }
+  if (mode == STIF_PACK_WINO_LSTM) {
+    // packed 4h + gate <- reference row gate*64 + h (gates i, f, o, g; convlstm.py:49)
+    return (j & 3) * 64 + (j >> 2);
+  }
   if (mode == STIF_PACK_LSTM) {
     // packed slice s (128 outputs) = gates i, f, o, g of hidden channels 32s..32s+31 (convlstm.py:49)
     const int s = j / 128, gate = (j % 128) / 32, jj = j % 32;
@@ -82,13 +86,15 @@ void column(float* dst, const float* W, int ld, int rows, int col) {
 }  // namespace
 
 extern "C" size_t stif_conv_weight_floats(int cout, int cin, int ks, int mode) {
-  if (mode == STIF_PACK_WINO || mode == STIF_PACK_WINO_OFFMASK) return (size_t)round64(cout) * cin * 16;
+  if (mode == STIF_PACK_WINO || mode == STIF_PACK_WINO_OFFMASK || mode == STIF_PACK_WINO_LSTM)
+    return (size_t)round64(cout) * cin * 16;
   return (size_t)cout_padded(cout, mode) * cin * ks * ks;
 }
 
 extern "C" size_t stif_conv_bias_floats(int cout, int mode) {
-  return (mode == STIF_PACK_WINO || mode == STIF_PACK_WINO_OFFMASK) ? (size_t)round64(cout)
-                                                                     : (size_t)cout_padded(cout, mode);
+  return (mode == STIF_PACK_WINO || mode == STIF_PACK_WINO_OFFMASK || mode == STIF_PACK_WINO_LSTM)
+             ? (size_t)round64(cout)
+             : (size_t)cout_padded(cout, mode);
 }
 
 namespace {
@@ -127,10 +133,12 @@ extern "C" int stif_pack_conv_weight(const float* w, const float* b, int cout, i
     return stif_fail(STIF_E_INVALID, "stif_pack_conv_weight: bad arguments");
   if ((mode == STIF_PACK_OFFMASK || mode == STIF_PACK_WINO_OFFMASK) && cout != 216)
     return stif_fail(STIF_E_INVALID, "offmask pack needs cout=216");
-  if (mode == STIF_PACK_LSTM && cout != 256) return stif_fail(STIF_E_INVALID, "lstm pack needs cout=256");
-  if (mode == STIF_PACK_WINO || mode == STIF_PACK_WINO_OFFMASK) {
+  if ((mode == STIF_PACK_LSTM || mode == STIF_PACK_WINO_LSTM) && cout != 256)
+    return stif_fail(STIF_E_INVALID, "lstm pack needs cout=256");
+  if (mode == STIF_PACK_WINO || mode == STIF_PACK_WINO_OFFMASK || mode == STIF_PACK_WINO_LSTM) {
     if (ks != 3) return stif_fail(STIF_E_INVALID, "winograd pack needs a 3x3 kernel");
-    return pack_wino(w, b, cout, cin, mode == STIF_PACK_WINO ? STIF_PACK_PLAIN : STIF_PACK_OFFMASK, w_dst, b_dst);
+    const int perm = mode == STIF_PACK_WINO ? STIF_PACK_PLAIN : (mode == STIF_PACK_WINO_OFFMASK ? STIF_PACK_OFFMASK : mode);
+    return pack_wino(w, b, cout, cin, perm, w_dst, b_dst);
   }
   // layout [slice][chunk][tap][nt][lane][4]: the B fragments of one (slice, chunk) are one
   // contiguous block, copied to LDS by LDS-DMA; lane l of N-tile nt holds cout

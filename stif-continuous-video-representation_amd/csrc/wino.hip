@@ -258,25 +258,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     const int c4 = tid & 7, oxl = tid >> 3;
     const int ox = cur.ox0 + oxl;
     const int bb = oxl & 1, txo = oxl >> 1;
-    const size_t slab = (size_t)a.Ho * a.Wo * a.cout;
+    // LSTM: the quad is (i, f, o, g) of hidden channel cout/4; out / out2 / res are 64-ch maps
+    constexpr bool LSTM = EPI == STIF_EPI_LSTM;
+    const int ostride = LSTM ? 64 : a.cout;
+    const size_t slab = (size_t)a.Ho * a.Wo * ostride;
     const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(a.out[cur.g] + (size_t)cur.n * a.out_item), (short)0, (int)(slab * 4), 0x00020000);
     const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(EPI == STIF_EPI_RES ? a.res[cur.g] + (size_t)cur.n * a.res_item : a.in0[cur.g]), (short)0,
+        (void*)(EPI == STIF_EPI_RES || LSTM ? a.res[cur.g] + (size_t)cur.n * a.res_item : a.in0[cur.g]), (short)0,
         (int)(slab * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ro2 = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(LSTM ? a.out2[cur.g] + (size_t)cur.n * a.out2_item : a.out[cur.g]), (short)0, (int)(slab * 4),
+        0x00020000);
     auto voff = [&](int nt, int k) -> unsigned {
       const int oy = cur.oy0 + k;
       const int co = cur.slice * 64 + nt * 32 + c4 * 4;
       const bool ok = (oy < a.Ho) & (ox < a.Wo) & (co < a.cout);
-      return ok ? (unsigned)(((oy * a.Wo + ox) * a.cout + co) * 4) : 0x80000000u;
+      return ok ? (unsigned)(((oy * a.Wo + ox) * ostride + (LSTM ? co >> 2 : co)) * 4) : 0x80000000u;
     };
     f32x4 rv[2][4];
+    float cc[2][4];
     if (EPI == STIF_EPI_RES) {
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
         for (int k = 0; k < 4; ++k)
           rv[nt][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, voff(nt, k), 0, 0));
+    }
+    if (LSTM) {
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          cc[nt][k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, voff(nt, k), 0, 0));
     }
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
@@ -303,6 +317,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
           if (EPI == STIF_EPI_OFFMASK && (cob + e) % 3 == 2) y[e] = sigmoidf_(y[e]);
         }
         if (EPI == STIF_EPI_RES) y += rv[nt][k];
+        if (LSTM) {
+          // ConvLSTMCell (convlstm.py:51-56): c_next = f * c_cur + i * g, h_next = o * tanh(c_next)
+          const float cn = sigmoidf_(y[1]) * cc[nt][k] + sigmoidf_(y[0]) * tanhf(y[3]);
+          const float hn = sigmoidf_(y[2]) * tanhf(cn);
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, hn), ro, voff(nt, k), 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, cn), ro2, voff(nt, k), 0, 0);
+          continue;
+        }
 #ifdef WINO_EXP_NOEPI
         if (y[0] == 12345.f)
 #endif
@@ -362,6 +384,8 @@ extern "C" int stif_conv3x3_wino(const stif_conv_args* pa, void* stream) {
     return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: 3x3 stride-1 'same' convolution only");
   if (a.C0 % 8 || a.C0 <= 0 || (a.in1_mode == 1 && (a.C1 % 8 || a.C1 <= 0)))
     return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: channel counts must be multiples of 8");
+  if (a.epi == STIF_EPI_LSTM && (a.cout != 256 || a.in1_mode != 1 || !a.res[0] || !a.out2[0]))
+    return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: LSTM conv must be 128->256 with res = c_cur, out2 = c_next");
   if (a.cout % 64 && a.epi != STIF_EPI_OFFMASK)
     return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: cout must be a multiple of 64");
   if (a.epi == STIF_EPI_OFFMASK && (a.cout != 216 || a.in1_mode != 0))
@@ -378,6 +402,7 @@ extern "C" int stif_conv3x3_wino(const stif_conv_args* pa, void* stream) {
     default: break;                                                      \
   }
   if (a.in1_mode == 0 && a.epi == STIF_EPI_OFFMASK) return launch<0, STIF_EPI_OFFMASK>(a, st);
+  if (a.in1_mode == 1 && a.epi == STIF_EPI_LSTM) return launch<1, STIF_EPI_LSTM>(a, st);
   if (a.in1_mode == 0) { STIF_WINO_CASE(0) }
   else if (a.in1_mode == 1) { STIF_WINO_CASE(1) }
 #undef STIF_WINO_CASE

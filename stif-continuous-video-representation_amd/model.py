@@ -120,8 +120,9 @@ class LunaTokis:
             lay[name] = ops.pack_conv(h[name + ".weight"], h[name + ".bias"], mode, dev)
 
         # 3x3 / stride-1 / 64-cout convs run by Winograd F(2x2,3x3) (stif_conv3x3_wino; the
-        # cat(., up(.)) ones on a materialised x2-upsampled second input); the strided, 1x1,
-        # offset/mask and ConvLSTM convs keep the direct kernel.
+        # cat(., up(.)) ones on a materialised x2-upsampled second input), as do the offset/mask
+        # (64 -> 216) and ConvLSTMCell (128 -> 256, gate epilogue) convs; the strided and 1x1
+        # convs keep the direct kernel.
         wino = L.PACK_WINO if self.winograd else L.PACK_PLAIN
 
         lay["conv_first.w"] = torch.from_numpy(h["conv_first.weight"]).to(dev)
@@ -146,7 +147,7 @@ class LunaTokis:
 
         pcd("pcd_align.")
         conv("fusion")
-        conv("ConvBLSTM.forward_net.cell_list.0.conv", L.PACK_LSTM)
+        conv("ConvBLSTM.forward_net.cell_list.0.conv", L.PACK_WINO_LSTM if self.winograd else L.PACK_LSTM)
         for p in ("ConvBLSTM.forward_net.pcd_h.", "ConvBLSTM.forward_net.pcd_c."):
             for n in ("fea_L2_conv1", "fea_L3_conv1", "fusion"):
                 conv(p + n)

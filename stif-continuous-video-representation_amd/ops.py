@@ -105,7 +105,7 @@ def conv2d(groups, *, epi=L.EPI_NONE, in1_mode=0, in1_scale=1.0, stride=None):
     a.H, a.W, a.C0, a.C1 = H, W, C0, C1
     a.in1_mode, a.in1_scale = in1_mode, in1_scale
     a.Ho, a.Wo, a.cout, a.ks, a.stride, a.epi = Ho, Wo, lay.cout, ks, stride, epi
-    wmodes = (L.PACK_WINO, L.PACK_WINO_OFFMASK)
+    wmodes = (L.PACK_WINO, L.PACK_WINO_OFFMASK, L.PACK_WINO_LSTM)
     wino = lay.mode in wmodes
     if any((g["layer"].mode in wmodes) != wino for g in groups):
         raise ValueError("conv2d: groups mix Winograd and direct packings")

@@ -163,3 +163,23 @@ def test_wino_offmask_matches_direct(stif):
     msk = 1 / (1 + np.exp(-ref[:, 144:].reshape(2, 8, 9, 10, 40).transpose(0, 3, 4, 1, 2)))
     assert relmax(got[..., :2], off) < RTOL
     assert np.abs(got[..., 2] - msk).max() < 1e-5
+
+
+@pytest.mark.parametrize("hw", [(6, 40), (13, 37), (32, 64)])
+def test_wino_lstm_cell_conv(stif, sd, hw):
+    """ConvLSTMCell conv + gates (convlstm.py:42-58) on the Winograd path (STIF_PACK_WINO_LSTM),
+    both BiConvLSTM directions as two launch groups, against the oracle cell."""
+    L, ops = stif._lib, stif.ops
+    H, W = hw
+    p = "ConvBLSTM.forward_net.cell_list.0."
+    layer = ops.pack_conv(sd[p + "conv.weight"], sd[p + "conv.bias"], L.PACK_WINO_LSTM)
+    groups, refs = [], []
+    for d in range(2):
+        x, h, c = (rnd(2, 64, H, W, seed=30 + 3 * d + k) for k in range(3))
+        refs.append(O.conv_lstm_cell(x, h, c, sd, p, np.float64))
+        groups.append(dict(layer=layer, in0=nhwc(x), in1=nhwc(h), res=nhwc(c),
+                           out=torch.empty(2, H, W, 64, device="cuda"), out2=torch.empty(2, H, W, 64, device="cuda")))
+    ops.conv2d(groups, epi=L.EPI_LSTM, in1_mode=1)
+    for g, (hn, cn) in zip(groups, refs):
+        assert relmax(to_nchw(g["out"]), hn) < RTOL
+        assert relmax(to_nchw(g["out2"]), cn) < RTOL
