@@ -77,7 +77,7 @@ int stif_conv2d_nhwc(const stif_conv_args* args, void* stream);
  * (2.25x fewer multiply-adds; all arithmetic fp32): weights packed with STIF_PACK_WINO
  * (epi NONE / LRELU / RELU / RES), STIF_PACK_WINO_OFFMASK (epi OFFMASK, cout 216) or
  * STIF_PACK_WINO_LSTM (epi LSTM, 128 -> 256: out = h_next, out2 = c_next, res = c_cur, 64-ch maps);
- * in1_mode 0 or 1; total input channels a multiple of 32. */
+ * in1_mode 0 or 1; C0 and C1 multiples of 32. */
 int stif_conv3x3_wino(const stif_conv_args* args, void* stream);
 
 /* out = scale * F.interpolate(in, scale_factor=2, mode='bilinear', align_corners=False) on NHWC

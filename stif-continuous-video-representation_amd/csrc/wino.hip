@@ -104,34 +104,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   auto wbase = [&](const Tile& t) { return a.w[t.g] + (size_t)t.slice * NC * 8192 + wi * 2048 + lane * 4; };
 
   auto stage = [&](const Tile& t, int p, int buf) {
-    const float* in0 = a.in0[t.g] + (size_t)t.n * a.in0_item;
-    const float* in1 = IN1 ? a.in1[t.g] + (size_t)t.n * a.in1_item : in0;
-    const __amdgpu_buffer_rsrc_t r0 =
-        __builtin_amdgcn_make_buffer_rsrc((void*)in0, (short)0, (int)((size_t)H * W * C0 * 4), 0x00020000);
-    const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)in1, (short)0, (int)((size_t)H * W * (IN1 ? C1 : C0) * 4), 0x00020000);
+    // a phase lies entirely in one input (NC0 % PSUB == 0, host-checked)
+    const bool second = IN1 && p * PSUB >= NC0;
+    const float* src = second ? a.in1[t.g] + (size_t)t.n * a.in1_item : a.in0[t.g] + (size_t)t.n * a.in0_item;
+    const int Cs = second ? C1 : C0;
+    const int cbase = (second ? p * PSUB - NC0 : p * PSUB) * 8;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, (int)((size_t)H * W * Cs * 4), 0x00020000);
     float* dst = smem + buf * BUF_F;
     const int iy0 = t.oy0 - 1, ix0 = t.ox0 - 1;
 #ifdef WINO_EXP_NOSTAGE
     if (p < 1000000) return;
 #endif
     for (int q = wi; q < IN_INST; q += 4) {
+      // 16-B element e of the phase image = (halo row, 8-channel sub-chunk, half h, column slot)
       const int e = q * 64 + lane;
       const int slot = e % HC;
       const int rest = e / HC;
       const int h = rest & 1, sub = (rest >> 1) % PSUB, row = (rest >> 1) / PSUB;
       const int col = slot < 17 ? 2 * slot : 2 * (slot - 17) + 1;
-      const int k = p * PSUB + sub;
       const int y = iy0 + row, x = ix0 + col;
-      const bool ok = e < IN_EL && y >= 0 && y < H && x >= 0 && x < W;
-      const bool second = IN1 && k >= NC0;
-      const int Cs = second ? C1 : C0;
-      const int cc = second ? k - NC0 : k;
-      const unsigned voff = ok ? (unsigned)((((size_t)y * W + x) * Cs + cc * 8 + h * 4) * 4) : 0x80000000u;
-      if (second)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(r1, dst + q * 256, 16, voff, 0, 0, 0);
-      else
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(r0, dst + q * 256, 16, voff, 0, 0, 0);
+      const bool ok = (e < IN_EL) & ((unsigned)y < (unsigned)H) & ((unsigned)x < (unsigned)W);
+      const unsigned voff = ok ? (unsigned)(((y * W + x) * Cs + cbase + sub * 8 + h * 4) * 4) : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, dst + q * 256, 16, voff, 0, 0, 0);
     }
   };
 
@@ -189,6 +184,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     f32x16 acc[4][2];
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[j][0] = acc[j][1] = f32x16{0};
+    // offset/mask conv: couts 224..255 of the last slice are padding (216 = 6.75 x 32), skip them
+    const bool skip1 = EPI == STIF_EPI_OFFMASK && cur.slice * 64 + 32 >= a.cout;
     WTR(1);
 
     for (int p = 0; p < NP; ++p, ++gp) {
@@ -213,6 +210,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         for (int j = 0; j < 4; ++j) {
 #pragma unroll
           for (int nt = 0; nt < 2; ++nt) {
+            if (nt == 1 && skip1) continue;
 #pragma unroll
             for (int e = 0; e < 4; ++e) acc[j][nt] = mfma32(v[j][e], bw[j][nt][e], acc[j][nt]);
           }
@@ -390,8 +388,8 @@ extern "C" int stif_conv3x3_wino(const stif_conv_args* pa, void* stream) {
     return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: cout must be a multiple of 64");
   if (a.epi == STIF_EPI_OFFMASK && (a.cout != 216 || a.in1_mode != 0))
     return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: offset/mask conv must be 64->216");
-  if ((a.C0 + (a.in1_mode ? a.C1 : 0)) % (8 * PSUB))
-    return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: total input channels must be a multiple of 32");
+  if (a.C0 % (8 * PSUB) || (a.in1_mode && a.C1 % (8 * PSUB)))
+    return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: input channel counts must be multiples of 32");
   if (a.epi == STIF_EPI_RES && !a.res[0]) return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: RES needs res");
 #define STIF_WINO_CASE(IN1)                                              \
   switch (a.epi) {                                                       \
