@@ -51,7 +51,7 @@ STIF_DEV int col_slot(int c) { return (c & 1) ? 17 + (c >> 1) : (c >> 1); }
 __device__ unsigned long long g_wtrace[512 * 4 * 128];
 #define WTR(tag)                                                                                   \
   do {                                                                                             \
-    if (ntr < 128 && blockIdx.x < 512 && lane == 0)                                                \
+    if (ntr < 127 && blockIdx.x < 512 && lane == 0)                                                \
       g_wtrace[(blockIdx.x * 4 + wi) * 128 + ntr] = (__builtin_amdgcn_s_memtime() << 8) | (tag);   \
     ++ntr;                                                                                         \
   } while (0)
@@ -138,13 +138,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 
   // input transform row i of 8-channel chunk s of the phase in `buf`, for this lane's tile and
   // channels 4h..4h+3: the wave's MFMA A operands for xi = 4i + j
-  auto transform = [&](const float* buf, int s, f32x4* v) {
+  // split in the LDS reads (issued one chunk ahead, so their latency hides under the MFMAs of the
+  // current chunk) and the add/subtract part
+  auto xread = [&](const float* buf, int s, f32x4* rd) {
     const float* ra = buf + (((2 * tyl + rA) * PSUB + s) * 2 + hf) * HC * 4;
     const float* rb = buf + (((2 * tyl + rB) * PSUB + s) * 2 + hf) * HC * 4;
-    const f32x4 t0 = ld4(ra + s0 * 4) + sB * ld4(rb + s0 * 4);
-    const f32x4 t1 = ld4(ra + s1 * 4) + sB * ld4(rb + s1 * 4);
-    const f32x4 t2 = ld4(ra + s2 * 4) + sB * ld4(rb + s2 * 4);
-    const f32x4 t3 = ld4(ra + s3 * 4) + sB * ld4(rb + s3 * 4);
+    rd[0] = ld4(ra + s0 * 4); rd[1] = ld4(rb + s0 * 4);
+    rd[2] = ld4(ra + s1 * 4); rd[3] = ld4(rb + s1 * 4);
+    rd[4] = ld4(ra + s2 * 4); rd[5] = ld4(rb + s2 * 4);
+    rd[6] = ld4(ra + s3 * 4); rd[7] = ld4(rb + s3 * 4);
+  };
+  auto xform = [&](const f32x4* rd, f32x4* v) {
+    const f32x4 t0 = rd[0] + sB * rd[1];
+    const f32x4 t1 = rd[2] + sB * rd[3];
+    const f32x4 t2 = rd[4] + sB * rd[5];
+    const f32x4 t3 = rd[6] + sB * rd[7];
     v[0] = t0 - t2;
     v[1] = t1 + t2;
     v[2] = t2 - t1;
@@ -155,6 +163,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   if (T >= ntiles) return;
 #ifdef WINO_EXP_TRACE
   int ntr = 0;
+  if (blockIdx.x < 512 && lane == 0) {   // slot 127: hardware placement (HW_ID, XCC_ID)
+    const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));
+    const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));
+    g_wtrace[(blockIdx.x * 4 + wi) * 128 + 127] = ((unsigned long long)xcc << 32) | hw;
+  }
 #endif
   Tile cur = tile_of(T);
   const float* wsl = wbase(cur);
@@ -168,10 +181,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 #ifdef WINO_EXP_STAGGER
   // the second workgroup of a CU starts ~half a tile late, so the two workgroups' barrier and
   // epilogue stretches interleave with each other's MFMA streams instead of coinciding
-  if (blockIdx.x >= gridDim.x / 2) {
-    __builtin_amdgcn_s_sleep(127);
-    __builtin_amdgcn_s_sleep(WINO_EXP_STAGGER);
-  }
+  if (blockIdx.x >= gridDim.x / 2)
+    for (int i = 0; i < WINO_EXP_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
 #endif
   lds_dma_barrier();
 
@@ -192,13 +203,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       if (p + 1 < NP) stage(cur, p + 1, (gp + 1) & 1);
       else if (has_next) stage(nxt, 0, (gp + 1) & 1);
       const float* buf = smem + (gp & 1) * BUF_F;
+      f32x4 rd[8];
+      xread(buf, 0, rd);
 #pragma unroll
       for (int s = 0; s < PSUB; ++s) {
         f32x4 v[4];
 #ifdef WINO_EXP_NOXF
         v[0] = v[1] = v[2] = v[3] = f32x4{1.f * s, 1.f, 1.f, (float)lane};
 #else
-        transform(buf, s, v);
+        xform(rd, v);
+        if (s + 1 < PSUB) xread(buf, s + 1, rd);
 #endif
         // B operands of the next chunk (the next tile's first chunk after the last one).  bw[j] is
         // reloaded right after its 8 MFMAs, 3/4 of a chunk (24 MFMAs) before its next use; the
@@ -208,12 +222,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         const float* wn = kn < NC ? wsl + (size_t)kn * 8192 : wnx;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
+#ifdef WINO_EXP_ILV
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {
+              if (nt == 1 && skip1) continue;
+              acc[j][nt] = mfma32(v[j][e], bw[j][nt][e], acc[j][nt]);
+            }
+#else
 #pragma unroll
           for (int nt = 0; nt < 2; ++nt) {
             if (nt == 1 && skip1) continue;
 #pragma unroll
             for (int e = 0; e < 4; ++e) acc[j][nt] = mfma32(v[j][e], bw[j][nt][e], acc[j][nt]);
           }
+#endif
 #ifndef WINO_EXP_NOB
 #pragma unroll
           for (int nt = 0; nt < 2; ++nt) bw[j][nt] = ld4(wn + (j * 2 + nt) * 256);
@@ -251,7 +275,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       yv[nt][0] = acc[0][nt] + acc[1][nt] + acc[2][nt];
       yv[nt][1] = acc[1][nt] - acc[2][nt] - acc[3][nt];
     }
-    auto xrow = [](int i, int b, int m) { return (((i * 2 + b) * 32 + m) ^ (((m >> 2) ^ b) & 1)) * 32; };
+    // element address of (wave i, b, tile m, cout co) in the exchange image: row
+    // ((i*2 + b)*32 + m) ^ (bit2(m) ^ b), 32 couts a row.  Written out as a per-lane base plus
+    // compile-time offsets, so the compiler does not hoist 48 addresses into VGPRs.
+    //   writer (m = mfma_row(r, lane), bit2(m) = hf): row bit 0 is flipped iff hf ^ b, i.e.
+    //   +32 floats for even r, -32 for odd r;
+    //   reader (m = 16(k >> 1) + txo): bit2(m) = bit2(txo).
     // this thread's outputs: cout quad c4, column ox of the tile, rows k = 0..3
     const int c4 = tid & 7, oxl = tid >> 3;
     const int ox = cur.ox0 + oxl;
@@ -294,18 +323,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     for (int nt = 0; nt < 2; ++nt) {
       if (nt) __syncthreads();   // round-0 readers are done with the exchange image
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
+      for (int b = 0; b < 2; ++b) {
+        const int fl = (hf ^ b) * 32;
+        float* wb = ex + ((wi * 2 + b) * 32 + 4 * hf) * 32 + tl;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) ex[xrow(wi, b, mfma_row(r, lane)) + tl] = yv[nt][b][r];
+        for (int r = 0; r < 16; ++r)
+          wb[((r & 3) + 8 * (r >> 2)) * 32 + ((r & 1) ? -fl : fl)] = yv[nt][b][r];
+      }
       __syncthreads();
       WTR(3);
       const int cob = cur.slice * 64 + nt * 32 + c4 * 4;
       const f32x4 bv = cob < a.cout ? ld4(a.bias[cur.g] + cob) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const int m = (k >> 1) * 16 + txo;
-        const f32x4 p1 = ld4(ex + xrow(1, bb, m) + c4 * 4), p2 = ld4(ex + xrow(2, bb, m) + c4 * 4);
-        const f32x4 pe = ld4(ex + xrow((k & 1) ? 3 : 0, bb, m) + c4 * 4);
+        const float* rbase = ex + (bb * 32 + (txo ^ (((txo >> 2) ^ bb) & 1))) * 32 + c4 * 4 + (k >> 1) * 512;
+        const f32x4 p1 = ld4(rbase + 1 * 2048), p2 = ld4(rbase + 2 * 2048);
+        const f32x4 pe = ld4(rbase + ((k & 1) ? 3 : 0) * 2048);
         f32x4 y = (k & 1) ? (p1 - p2 - pe) : (pe + p1 + p2);
         y += bv;
 #pragma unroll

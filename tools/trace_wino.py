@@ -1,7 +1,8 @@
 """Per-wave s_memtime trace of the Winograd conv (kernel-experiment build with -DWINO_EXP_TRACE):
-average cycles of each segment between trace points, per wave role.  STIF_HIP_LIB must point at
-the trace build.  Tags: 1 tile start, 6 before a phase barrier, 2 after it, 3 after the exchange
-barrier, 4 after the second epilogue barrier, 5 end of the tile's stores."""
+average cycles of each segment between trace points per wave, and for the two waves that share a
+SIMD, how much of the time at least one of them is inside a phase (MFMA stream).  STIF_HIP_LIB must
+point at the trace build.  Tags: 1 tile start, 6 before a phase barrier, 2 after it, 3 after the
+exchange barrier(s), 4 after the final epilogue barrier, 5 end of the tile."""
 import ctypes as C
 import os
 import sys
@@ -33,17 +34,49 @@ lib.stif_exp_wino_trace.argtypes = [C.c_void_p]
 assert lib.stif_exp_wino_trace(buf.ctypes.data) == 0
 tr = buf.reshape(512, 4, 128)
 seg = defaultdict(list)
+simd = defaultdict(list)   # placement -> list of (block, wave)
 for blk in range(512):
     for wv in range(4):
-        ev = [(int(v) >> 8, int(v) & 0xFF) for v in tr[blk, wv] if v]
+        ev = [(int(v) >> 8, int(v) & 0xFF) for v in tr[blk, wv, :127] if v]
         for (t0, a), (t1, bb) in zip(ev, ev[1:]):
             seg[(wv, a, bb)].append(t1 - t0)
+        hw = int(tr[blk, wv, 127])
+        xcc, hid = hw >> 32, hw & 0xFFFFFFFF
+        simd[(xcc & 0xF, (hid >> 8) & 0xF, (hid >> 12) & 1, (hid >> 13) & 7, (hid >> 4) & 3)].append((blk, wv))
 names = {1: "start", 6: "pre-bar", 2: "post-bar", 3: "xchg", 4: "comb", 5: "stored"}
-tot = defaultdict(float)
 for k in sorted(seg):
     v = np.array(seg[k])
     print(f"wave {k[0]} {names[k[1]]:>8s} -> {names[k[2]]:<8s} n={len(v):5d} avg {v.mean():8.0f} med {np.median(v):8.0f} cyc")
-# per-tile period
-for wv in range(4):
-    st = [int(v) >> 8 for v in tr[:, wv].reshape(-1) if v and (int(v) & 0xFF) == 1]
 print("MFMA cycles per tile per wave at peak: 256 x 64 =", 256 * 64)
+
+
+def phase_intervals(blk, wv):
+    """[start, end) intervals in which the wave runs a phase: tag 1 or 2 -> next tag 6"""
+    ev = [(int(v) >> 8, int(v) & 0xFF) for v in tr[blk, wv, :127] if v]
+    iv = []
+    for (t0, a), (t1, bb) in zip(ev, ev[1:]):
+        if a in (1, 2) and bb == 6:
+            iv.append((t0, t1))
+    return iv, (ev[0][0], ev[-1][0]) if ev else (0, 0)
+
+
+sizes = defaultdict(int)
+both_idle = tot = 0.0
+for key, members in simd.items():
+    sizes[len(members)] += 1
+    if len(members) != 2:
+        continue
+    (i1, s1), (i2, s2) = [phase_intervals(*m) for m in members]
+    lo, hi = max(s1[0], s2[0]), min(s1[1], s2[1])
+    if hi <= lo:
+        continue
+    grid = np.zeros(int(hi - lo) // 16 + 1, bool)
+    for iv in (i1, i2):
+        for a0, a1 in iv:
+            a0, a1 = max(a0, lo), min(a1, hi)
+            if a1 > a0:
+                grid[int(a0 - lo) // 16:int(a1 - lo) // 16] = True
+    both_idle += (~grid).sum()
+    tot += grid.size
+print("waves per SIMD histogram:", dict(sizes))
+print(f"fraction of the common window with NEITHER wave of a SIMD inside a phase: {both_idle / max(tot, 1):.3f}")
