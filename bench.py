@@ -57,17 +57,19 @@ class KernelTimer:
 
     def __init__(self, kind):
         self.kind = kind
+        self.nbytes = []
         self.rec = []
         self.all = []
         self._cur = None
 
     kinds = None
 
-    def begin(self, kind, flops):
+    def begin(self, kind, flops, nbytes=0.0):
         if self.kind is None or kind == self.kind:
             if self.kinds is None:
                 self.kinds = []
             self.kinds.append(kind)
+            self.nbytes.append(nbytes)
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -102,7 +104,9 @@ class KernelTimer:
     def summary(self):
         ms = [a.elapsed_time(b) for a, b, _ in self.rec]
         fl = [f for _, _, f in self.rec]
-        return len(ms), float(np.mean(ms)) if ms else 0.0, float(np.mean(fl)) if fl else 0.0
+        nb = self.nbytes[:len(ms)]
+        return (len(ms), float(np.mean(ms)) if ms else 0.0, float(np.mean(fl)) if fl else 0.0,
+                float(np.mean(nb)) if nb else 0.0)
 
 
 def synth_frames(first, count, H, W, device):
@@ -142,7 +146,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c1", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_r01.json"))
+    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_r01.json"),
+                    help="PMC summary (tools/pmc_summary.py) giving the dominant kernel's HBM bytes/dispatch")
     ap.add_argument("--kernel-report", action="store_true", help="time every conv launch kind (stderr)")
     args = ap.parse_args()
 
@@ -198,7 +203,7 @@ def main():
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         td.all_reduce(t, op=td.ReduceOp.MAX)
         elapsed = float(t.item())
-    n_launch, avg_ms, avg_flops = timer.summary()
+    n_launch, avg_ms, avg_flops, avg_bytes = timer.summary()
     if args.kernel_report and rank == 0:
         with torch.no_grad():
             rep = KernelTimer(None)
@@ -215,12 +220,14 @@ def main():
         achieved = avg_flops / (avg_ms * 1e-3) / 1e12 if avg_ms else 0.0
         kname, kdesc, peak = kernel_desc(dom)
         traffic = None
-        # the committed PMC summary was measured at C1 (per-launch bytes of that configuration)
+        # HBM bytes per dispatch of the same kernel from the committed PMC passes over this bench
+        # (tools/pmc_summary.py); they were measured at C1, so only a C1 line carries them
         if args.config == "c1" and os.path.exists(args.traffic):
             try:
-                pmc = json.load(open(args.traffic))
-                if kname.split("<")[0] in pmc.get("kernel", "") and pmc.get("kind") == list(dom):
-                    traffic = pmc.get("hbm_bytes_per_launch")
+                pmc = json.load(open(args.traffic))["per_kernel"]
+                hits = [v for k, v in pmc.items() if kname in k]
+                if len(hits) == 1:
+                    traffic = round(hits[0]["hbm_bytes_per_dispatch"])
             except Exception:
                 traffic = None
         res = {
@@ -243,7 +250,9 @@ def main():
                          "achieved": round(achieved, 3), "peak": round(peak, 2), "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4), "traffic": traffic,
                          "launches": n_launch, "avg_launch_us": round(avg_ms * 1e3, 2),
-                         "flops_per_launch": avg_flops},
+                         "flops_per_launch": avg_flops,
+                         "algorithmic_bytes_per_launch": round(avg_bytes),
+                         "hbm_gbps_algorithmic": round(avg_bytes / (avg_ms * 1e-3) / 1e9, 1) if avg_ms else None},
         }
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(stif, sd, frames_cpu, times, scale)

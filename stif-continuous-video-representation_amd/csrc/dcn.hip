@@ -70,6 +70,9 @@ __global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
       __builtin_amdgcn_make_buffer_rsrc((void*)in, (short)0, (int)((size_t)H * W * 64 * 4), 0x00020000);
 
   auto stage = [&](int dg, int buf) {
+#ifdef DCN_EXP_NOSTAGE
+    if (dg < 100) return;
+#endif
     float* st = smem + buf * BUF_F;
     float* sw = st + T_F;
     for (int i = wv; i < T_INST; i += NW) {
@@ -95,7 +98,13 @@ __global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
     if (dg + 1 < 8) {
       stage(dg + 1, (dg + 1) & 1);
 #pragma unroll
-      for (int k = 0; k < 27; ++k) omn[k] = omp[(dg + 1) * 27 + k];
+      for (int k = 0; k < 27; ++k) {
+#ifdef DCN_EXP_NOOM
+        omn[k] = omc[k] + 0.5f;
+#else
+        omn[k] = omp[(dg + 1) * 27 + k];
+#endif
+      }
     }
     const float* st = smem + (dg & 1) * BUF_F;
     const float* sw = st + T_F;
@@ -105,6 +114,10 @@ __global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
       const float h_im = (float)(oy - 1 + tap / 3) + omc[tap * 3];
       const float w_im = (float)(ox - 1 + tap % 3) + omc[tap * 3 + 1];
       f32x4 av = f32x4{0};
+#ifdef DCN_EXP_NOSAMPLE
+      av = f32x4{h_im, w_im, 1.f, 2.f};
+      if (0)
+#endif
       if (pix_ok && h_im > -1.f && w_im > -1.f && h_im < (float)H && w_im < (float)W) {
         const float fh = floorf(h_im), fw = floorf(w_im);
         const int h_low = (int)fh, w_low = (int)fw;

@@ -86,14 +86,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   const int NC = NC0 + (IN1 ? (C1 >> 3) : 0);
   const int NP = NC / PSUB;   // host guarantees NC % PSUB == 0
 
+  // tile order: cout slice fastest (the slices of one spatial tile share its input), then x, y, item
   auto tile_of = [&](int T) {
     Tile t;
-    const int x = T % tiles_x;
-    int r = T / tiles_x;
+    t.slice = T % slices;
+    int r = T / slices;
+    const int x = r % tiles_x;
+    r /= tiles_x;
     const int y = r % tiles_y;
     r /= tiles_y;
-    t.slice = r % slices;
-    r /= slices;
     t.g = r / a.nitems;
     t.n = r - t.g * a.nitems;
     t.oy0 = y * WR;
@@ -159,8 +160,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     v[3] = t1 - t3;
   };
 
-  int T = blockIdx.x;
-  if (T >= ntiles) return;
+  // XCD-aware persistent schedule: workgroup b is dispatched to XCD b % 8, and XCD x owns the
+  // contiguous tile range [x * per, (x + 1) * per), its workgroups striding through it -- tiles
+  // that share input (cout slices, halo rows) run at the same time under the same L2
+  const int xcd = blockIdx.x & 7, nl = gridDim.x >> 3;   // host: grid is a multiple of 8
+  const int per = (ntiles + 7) >> 3;
+  const int tend = min((xcd + 1) * per, ntiles);
+  int T = xcd * per + (blockIdx.x >> 3);
+  if (T >= tend) return;
 #ifdef WINO_EXP_TRACE
   int ntr = 0;
   if (blockIdx.x < 512 && lane == 0) {   // slot 127: hardware placement (HW_ID, XCC_ID)
@@ -178,17 +185,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     for (int nt = 0; nt < 2; ++nt) bw[j][nt] = ld4(wsl + (j * 2 + nt) * 256);
   int gp = 0;                      // phases staged so far: buffer of phase gp = gp & 1
   stage(cur, 0, 0);
-#ifdef WINO_EXP_STAGGER
-  // the second workgroup of a CU starts ~half a tile late, so the two workgroups' barrier and
-  // epilogue stretches interleave with each other's MFMA streams instead of coinciding
-  if (blockIdx.x >= gridDim.x / 2)
-    for (int i = 0; i < WINO_EXP_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
-#endif
   lds_dma_barrier();
 
   for (;;) {
-    const int Tn = T + gridDim.x;
-    const bool has_next = Tn < ntiles;
+    const int Tn = T + nl;
+    const bool has_next = Tn < tend;
     const Tile nxt = tile_of(has_next ? Tn : T);
     const float* wnx = wbase(nxt);
 
@@ -392,7 +393,7 @@ int launch(const stif_conv_args& a, hipStream_t st) {
   if (tiles > 0x7fffffff) return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: too many tiles");
   if ((long long)a.H * a.W * std::max(a.C0, std::max(a.C1, a.cout)) * 4 >= 0x7fffffffLL)
     return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: item larger than 2 GB (buffer addressing)");
-  const int grid = (int)std::min<long long>(tiles, (long long)WG_PER_CU * num_cus());
+  const int grid = 8 * (int)std::min<long long>((tiles + 7) / 8, (long long)WG_PER_CU * num_cus() / 8);
   hipLaunchKernelGGL((k_wino<IN1, EPI>), dim3(grid), dim3(256), 0, st, a, (int)tiles);
   return stif_check_launch("stif_conv3x3_wino");
 }

@@ -112,8 +112,14 @@ def conv2d(groups, *, epi=L.EPI_NONE, in1_mode=0, in1_scale=1.0, stride=None):
     tr = TRACE
     if tr is not None:
         # algorithmic (direct-convolution) FLOPs, whichever algorithm runs
+        # algorithmic HBM bytes: every input read once, every output written once
+        px_in, px_out = H * W * nitems * len(groups), Ho * Wo * nitems * len(groups)
+        c_in = C0 + (C1 if in1_mode == 1 else C1 / 4.0 if in1_mode == 2 else 0)
+        c_out = 128 if epi == L.EPI_LSTM else lay.cout
+        c_res = 64 if epi in (L.EPI_RES, L.EPI_LSTM) else 0
         tr.begin(("wino" if wino else "conv", ks, stride, epi, in1_mode, lay.cout),
-                 2.0 * lay.cout * (C0 + C1) * ks * ks * Ho * Wo * nitems * len(groups))
+                 2.0 * lay.cout * (C0 + C1) * ks * ks * Ho * Wo * nitems * len(groups),
+                 4.0 * (c_in * px_in + (c_out + c_res) * px_out))
     if wino:
         L.check(L.lib().stif_conv3x3_wino(C.byref(a), _stream()), "stif_conv3x3_wino")
     else:
@@ -166,7 +172,8 @@ def dcn(groups, *, epi=L.EPI_NONE):
     a.ngroups, a.nitems, a.H, a.W, a.epi = len(groups), nitems, H, W, epi
     tr = TRACE
     if tr is not None:
-        tr.begin(("dcn", epi), 2.0 * 64 * 576 * H * W * nitems * len(groups))
+        tr.begin(("dcn", epi), 2.0 * 64 * 576 * H * W * nitems * len(groups),
+                 4.0 * (64 + 216 + 64) * H * W * nitems * len(groups))
     L.check(L.lib().stif_dcn_nhwc(C.byref(a), _stream()), "stif_dcn_nhwc")
     if tr is not None:
         tr.end()
