@@ -51,7 +51,7 @@ STIF_DEV int col_slot(int c) { return (c & 1) ? 17 + (c >> 1) : (c >> 1); }
 __device__ unsigned long long g_wtrace[512 * 4 * 128];
 #define WTR(tag)                                                                                   \
   do {                                                                                             \
-    if (ntr < 127 && blockIdx.x < 512 && lane == 0)                                                \
+    if (ntr < 127 && blockIdx.x < 512 && lane == 0 && wv < 4)                                                \
       g_wtrace[(blockIdx.x * 4 + wi) * 128 + ntr] = (__builtin_amdgcn_s_memtime() << 8) | (tag);   \
     ++ntr;                                                                                         \
   } while (0)
@@ -67,13 +67,22 @@ struct Tile {
 // 64-cout slice of one item), and the last staging phase of a tile already LDS-DMAs the first
 // phase of the next tile and the last chunk prefetches the next tile's first B operands, so a
 // workgroup's MFMA stream only pauses at the per-phase barriers and the short epilogue exchange.
-template <int IN1, int EPI>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_wino(stif_conv_args a,
-                                                                                      int ntiles) {
+// SPLIT = 0: 4 waves, wave i = transform row i for both 32-cout halves (2 waves/SIMD, ~250 VGPRs);
+// SPLIT = 1: 8 waves, wave (i, nh) = transform row i for cout half nh (4 waves/SIMD, <= 128 VGPRs:
+// twice the waves to hide latencies, the input transform computed by both halves).
+template <int IN1, int EPI, int SPLIT>
+__global__ __launch_bounds__(SPLIT ? 512 : 256) __attribute__((amdgpu_waves_per_eu(SPLIT ? 4 : 2))) void k_wino(
+    stif_conv_args a, int ntiles) {
+  constexpr int NWV = SPLIT ? 8 : 4;      // waves per workgroup
+  constexpr int NTW = SPLIT ? 1 : 2;      // 32-cout halves per wave
+  constexpr int NTHR = NWV * 64;
+  constexpr int KPT = 4 / (NWV / 4);      // output rows per thread in the epilogue
   __shared__ __attribute__((aligned(16))) float smem[2 * BUF_F];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wi = __builtin_amdgcn_readfirstlane(tid >> 6);   // transform row i of this wave
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wi = wv & 3;                                     // transform row i of this wave
+  const int nh = SPLIT ? (wv >> 2) : 0;                      // its cout half (SPLIT)
   const int hf = lane >> 5;
   const int tl = lane & 31;                                  // Winograd tile of this lane
   const int tyl = tl >> 4, txl = tl & 15;
@@ -101,8 +110,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     t.ox0 = x * 32;
     return t;
   };
-  // packed U: [slice][chunk][i][j][nt][lane][4]
-  auto wbase = [&](const Tile& t) { return a.w[t.g] + (size_t)t.slice * NC * 8192 + wi * 2048 + lane * 4; };
+  // packed U: [slice][chunk][i][j][nt][lane][4]; B fragment (j, local half u) at wsl + (j*2 + u)*256
+  auto wbase = [&](const Tile& t) {
+    return a.w[t.g] + (size_t)t.slice * NC * 8192 + wi * 2048 + nh * 256 + lane * 4;
+  };
 
   auto stage = [&](const Tile& t, int p, int buf) {
     // a phase lies entirely in one input (NC0 % PSUB == 0, host-checked)
@@ -117,7 +128,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 #ifdef WINO_EXP_NOSTAGE
     if (p < 1000000) return;
 #endif
-    for (int q = wi; q < IN_INST; q += 4) {
+    for (int q = wv; q < IN_INST; q += NWV) {
       // 16-B element e of the phase image = (halo row, 8-channel sub-chunk, half h, column slot)
       const int e = q * 64 + lane;
       const int slot = e % HC;
@@ -138,9 +149,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   const int s0 = col_slot(0) + txl, s1 = col_slot(1) + txl, s2 = col_slot(2) + txl, s3 = col_slot(3) + txl;
 
   // input transform row i of 8-channel chunk s of the phase in `buf`, for this lane's tile and
-  // channels 4h..4h+3: the wave's MFMA A operands for xi = 4i + j
-  // split in the LDS reads (issued one chunk ahead, so their latency hides under the MFMAs of the
-  // current chunk) and the add/subtract part
+  // channels 4h..4h+3: the wave's MFMA A operands for xi = 4i + j.  Split in the LDS reads (issued
+  // one chunk ahead where registers allow, so their latency hides under the current chunk's MFMAs)
+  // and the add/subtract part.
   auto xread = [&](const float* buf, int s, f32x4* rd) {
     const float* ra = buf + (((2 * tyl + rA) * PSUB + s) * 2 + hf) * HC * 4;
     const float* rb = buf + (((2 * tyl + rB) * PSUB + s) * 2 + hf) * HC * 4;
@@ -170,7 +181,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   if (T >= tend) return;
 #ifdef WINO_EXP_TRACE
   int ntr = 0;
-  if (blockIdx.x < 512 && lane == 0) {   // slot 127: hardware placement (HW_ID, XCC_ID)
+  if (blockIdx.x < 512 && lane == 0 && wv < 4) {   // slot 127: hardware placement (HW_ID, XCC_ID)
     const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));
     const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));
     g_wtrace[(blockIdx.x * 4 + wi) * 128 + 127] = ((unsigned long long)xcc << 32) | hw;
@@ -178,11 +189,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 #endif
   Tile cur = tile_of(T);
   const float* wsl = wbase(cur);
-  f32x4 bw[4][2];
+  f32x4 bw[4][NTW];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) bw[j][nt] = ld4(wsl + (j * 2 + nt) * 256);
+    for (int u = 0; u < NTW; ++u) bw[j][u] = ld4(wsl + (j * 2 + u) * 256);
   int gp = 0;                      // phases staged so far: buffer of phase gp = gp & 1
   stage(cur, 0, 0);
   lds_dma_barrier();
@@ -193,11 +204,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     const Tile nxt = tile_of(has_next ? Tn : T);
     const float* wnx = wbase(nxt);
 
-    f32x16 acc[4][2];
+    f32x16 acc[4][NTW];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j][0] = acc[j][1] = f32x16{0};
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int u = 0; u < NTW; ++u) acc[j][u] = f32x16{0};
     // offset/mask conv: couts 224..255 of the last slice are padding (216 = 6.75 x 32), skip them
-    const bool skip1 = EPI == STIF_EPI_OFFMASK && cur.slice * 64 + 32 >= a.cout;
+    const bool last_half_pad = EPI == STIF_EPI_OFFMASK && cur.slice * 64 + 32 >= a.cout;
     WTR(1);
 
     for (int p = 0; p < NP; ++p, ++gp) {
@@ -205,85 +218,83 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       else if (has_next) stage(nxt, 0, (gp + 1) & 1);
       const float* buf = smem + (gp & 1) * BUF_F;
       f32x4 rd[8];
-      xread(buf, 0, rd);
+      if (!SPLIT) xread(buf, 0, rd);
 #pragma unroll
       for (int s = 0; s < PSUB; ++s) {
         f32x4 v[4];
 #ifdef WINO_EXP_NOXF
         v[0] = v[1] = v[2] = v[3] = f32x4{1.f * s, 1.f, 1.f, (float)lane};
 #else
+        if (SPLIT) xread(buf, s, rd);
         xform(rd, v);
-        if (s + 1 < PSUB) xread(buf, s + 1, rd);
+        if (!SPLIT && s + 1 < PSUB) xread(buf, s + 1, rd);
 #endif
         // B operands of the next chunk (the next tile's first chunk after the last one).  bw[j] is
-        // reloaded right after its 8 MFMAs, 3/4 of a chunk (24 MFMAs) before its next use; the
-        // scheduling barriers keep the compiler from sinking those loads next to their use,
-        // which would expose the L2 latency on every j block.
+        // reloaded right after its MFMAs, 3/4 of a chunk before its next use; the scheduling
+        // barriers keep the compiler from sinking those loads next to their use, which would
+        // expose the L2 latency on every j block.
         const int kn = p * PSUB + s + 1;
         const float* wn = kn < NC ? wsl + (size_t)kn * 8192 : wnx;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-#ifdef WINO_EXP_ILV
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
+          for (int u = 0; u < NTW; ++u) {
+            if (last_half_pad && (SPLIT ? nh : u) == 1) continue;
 #pragma unroll
-            for (int nt = 0; nt < 2; ++nt) {
-              if (nt == 1 && skip1) continue;
-              acc[j][nt] = mfma32(v[j][e], bw[j][nt][e], acc[j][nt]);
-            }
-#else
-#pragma unroll
-          for (int nt = 0; nt < 2; ++nt) {
-            if (nt == 1 && skip1) continue;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) acc[j][nt] = mfma32(v[j][e], bw[j][nt][e], acc[j][nt]);
+            for (int e = 0; e < 4; ++e) acc[j][u] = mfma32(v[j][e], bw[j][u][e], acc[j][u]);
           }
-#endif
 #ifndef WINO_EXP_NOB
 #pragma unroll
-          for (int nt = 0; nt < 2; ++nt) bw[j][nt] = ld4(wn + (j * 2 + nt) * 256);
+          for (int u = 0; u < NTW; ++u) bw[j][u] = ld4(wn + (j * 2 + u) * 256);
 #else
-          for (int nt = 0; nt < 2; ++nt) bw[j][nt] += 1.f;
+          for (int u = 0; u < NTW; ++u) bw[j][u] += 1.f;
           (void)wn;
 #endif
           __builtin_amdgcn_sched_barrier(0);
         }
       }
 #ifndef WINO_EXP_NOBAR
-      // every load older than the last chunk's 8 B-operand prefetches -- the phase's LDS-DMA
-      // among them -- has landed; those 8 stay in flight across the barrier
+      // every load older than the last chunk's B-operand prefetches -- the phase's LDS-DMA among
+      // them -- has landed; those 4*NTW stay in flight across the barrier
       WTR(6);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      if (SPLIT) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       __syncthreads();
       WTR(2);
 #endif
     }
 
-    // ---- output transform, balanced over the 4 waves.  Wave i holds P_i[b] = sum_j M[i][j] A[j][b]
-    // (registers); Y[0] = P_0 + P_1 + P_2, Y[1] = P_1 - P_2 - P_3.  Two rounds (32-cout halves nt):
-    // every wave writes its P_i[nt] into the buffer of the phase just finished (free after the
-    // barrier; the other one is receiving the next tile) transposed to [i][b][tile][co], then every
-    // thread combines and stores 4 (pixel, 4-cout) vectors as coalesced 16-B accesses (8 lanes =
-    // one pixel's 128 B).  Row swizzle R ^ (bit2(tile) ^ b) keeps both the b32 writes (lane halves
-    // 4 tiles apart) and the b128 reads (16-lane groups = b 0/1 of one tile) conflict-free.
-    float* ex = smem + ((gp - 1) & 1) * BUF_F;
-#ifdef WINO_EXP_PRIO
-    __builtin_amdgcn_s_setprio(1);
-#endif
-    f32x16 yv[2][2];   // [nt][b]
+#ifdef WINO_EXP_NOEPI2
+    // kernel experiment: no output transform at all (keep the accumulators alive)
+    {
+      float sum = 0.f;
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      yv[nt][0] = acc[0][nt] + acc[1][nt] + acc[2][nt];
-      yv[nt][1] = acc[1][nt] - acc[2][nt] - acc[3][nt];
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int u = 0; u < NTW; ++u) sum += acc[j][u][j + u];
+      if (sum == 1234.5f) a.out[0][tid] = sum;
     }
-    // element address of (wave i, b, tile m, cout co) in the exchange image: row
-    // ((i*2 + b)*32 + m) ^ (bit2(m) ^ b), 32 couts a row.  Written out as a per-lane base plus
-    // compile-time offsets, so the compiler does not hoist 48 addresses into VGPRs.
+#else
+    // ---- output transform, balanced over all waves.  Wave i holds P_i[b] = sum_j M[i][j] A[j][b]
+    // (registers); Y[0] = P_0 + P_1 + P_2, Y[1] = P_1 - P_2 - P_3.  Two rounds (32-cout halves nt):
+    // the waves holding half nt write their P_i[nt] into the buffer of the phase just finished
+    // (free after the barrier; the other one is receiving the next tile) transposed to
+    // [i][b][tile][co], then every thread combines and stores (pixel, 4-cout) vectors as coalesced
+    // 16-B accesses (8 lanes = one pixel's 128 B).  Row swizzle R ^ (bit2(tile) ^ b) keeps both the
+    // b32 writes (lane halves 4 tiles apart) and the b128 reads (16-lane groups = b 0/1 of one
+    // tile) conflict-free.
+    float* ex = smem + ((gp - 1) & 1) * BUF_F;
+    f32x16 yv[NTW][2];   // [local half][b]
+#pragma unroll
+    for (int u = 0; u < NTW; ++u) {
+      yv[u][0] = acc[0][u] + acc[1][u] + acc[2][u];
+      yv[u][1] = acc[1][u] - acc[2][u] - acc[3][u];
+    }
+    // Exchange addresses as a per-lane base plus compile-time offsets (no hoisted address VGPRs):
     //   writer (m = mfma_row(r, lane), bit2(m) = hf): row bit 0 is flipped iff hf ^ b, i.e.
-    //   +32 floats for even r, -32 for odd r;
-    //   reader (m = 16(k >> 1) + txo): bit2(m) = bit2(txo).
-    // this thread's outputs: cout quad c4, column ox of the tile, rows k = 0..3
-    const int c4 = tid & 7, oxl = tid >> 3;
+    //   +32 floats for even r, -32 for odd r;  reader (m = 16(k >> 1) + txo): bit2(m) = bit2(txo).
+    // this thread's outputs: cout quad c4, column ox of the tile, rows k = k0 + (NWV/4) r
+    const int c4 = tid & 7, oxl = (tid >> 3) & 31, k0 = tid >> 8;
     const int ox = cur.ox0 + oxl;
     const int bb = oxl & 1, txo = oxl >> 1;
     // LSTM: the quad is (i, f, o, g) of hidden channel cout/4; out / out2 / res are 64-ch maps
@@ -304,39 +315,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       const bool ok = (oy < a.Ho) & (ox < a.Wo) & (co < a.cout);
       return ok ? (unsigned)(((oy * a.Wo + ox) * ostride + (LSTM ? co >> 2 : co)) * 4) : 0x80000000u;
     };
-    f32x4 rv[2][4];
-    float cc[2][4];
+    f32x4 rv[2][KPT];
+    float cc[2][KPT];
     if (EPI == STIF_EPI_RES) {
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-          rv[nt][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, voff(nt, k), 0, 0));
+        for (int r = 0; r < KPT; ++r)
+          rv[nt][r] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, voff(nt, k0 + (NWV / 4) * r), 0, 0));
     }
     if (LSTM) {
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-          cc[nt][k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, voff(nt, k), 0, 0));
+        for (int r = 0; r < KPT; ++r)
+          cc[nt][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, voff(nt, k0 + (NWV / 4) * r), 0, 0));
     }
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
       if (nt) __syncthreads();   // round-0 readers are done with the exchange image
+      if (!SPLIT || nh == nt) {
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const int fl = (hf ^ b) * 32;
-        float* wb = ex + ((wi * 2 + b) * 32 + 4 * hf) * 32 + tl;
+        for (int b = 0; b < 2; ++b) {
+          const int fl = (hf ^ b) * 32;
+          float* wb = ex + ((wi * 2 + b) * 32 + 4 * hf) * 32 + tl;
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          wb[((r & 3) + 8 * (r >> 2)) * 32 + ((r & 1) ? -fl : fl)] = yv[nt][b][r];
+          for (int r = 0; r < 16; ++r)
+            wb[((r & 3) + 8 * (r >> 2)) * 32 + ((r & 1) ? -fl : fl)] = yv[SPLIT ? 0 : nt][b][r];
+        }
       }
       __syncthreads();
       WTR(3);
       const int cob = cur.slice * 64 + nt * 32 + c4 * 4;
       const f32x4 bv = cob < a.cout ? ld4(a.bias[cur.g] + cob) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int r = 0; r < KPT; ++r) {
+        const int k = k0 + (NWV / 4) * r;
         const float* rbase = ex + (bb * 32 + (txo ^ (((txo >> 2) ^ bb) & 1))) * 32 + c4 * 4 + (k >> 1) * 512;
         const f32x4 p1 = ld4(rbase + 1 * 2048), p2 = ld4(rbase + 2 * 2048);
         const f32x4 pe = ld4(rbase + ((k & 1) ? 3 : 0) * 2048);
@@ -348,10 +362,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
           if (EPI == STIF_EPI_RELU) y[e] = fmaxf(y[e], 0.f);
           if (EPI == STIF_EPI_OFFMASK && (cob + e) % 3 == 2) y[e] = sigmoidf_(y[e]);
         }
-        if (EPI == STIF_EPI_RES) y += rv[nt][k];
+        if (EPI == STIF_EPI_RES) y += rv[nt][r];
         if (LSTM) {
           // ConvLSTMCell (convlstm.py:51-56): c_next = f * c_cur + i * g, h_next = o * tanh(c_next)
-          const float cn = sigmoidf_(y[1]) * cc[nt][k] + sigmoidf_(y[0]) * tanhf(y[3]);
+          const float cn = sigmoidf_(y[1]) * cc[nt][r] + sigmoidf_(y[0]) * tanhf(y[3]);
           const float hn = sigmoidf_(y[2]) * tanhf(cn);
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, hn), ro, voff(nt, k), 0, 0);
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, cn), ro2, voff(nt, k), 0, 0);
@@ -364,10 +378,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       }
     }
     __syncthreads();   // exchange buffer free for the next tile's staging
-#ifdef WINO_EXP_PRIO
-    __builtin_amdgcn_s_setprio(0);
-#endif
     WTR(4);
+#endif
     WTR(5);
     if (!has_next) break;
     T = Tn;
@@ -386,6 +398,10 @@ int num_cus() {
   return n;
 }
 
+#ifndef WINO_SPLIT
+#define WINO_SPLIT 0
+#endif
+
 template <int IN1, int EPI>
 int launch(const stif_conv_args& a, hipStream_t st) {
   const long long tiles =
@@ -394,7 +410,7 @@ int launch(const stif_conv_args& a, hipStream_t st) {
   if ((long long)a.H * a.W * std::max(a.C0, std::max(a.C1, a.cout)) * 4 >= 0x7fffffffLL)
     return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: item larger than 2 GB (buffer addressing)");
   const int grid = 8 * (int)std::min<long long>((tiles + 7) / 8, (long long)WG_PER_CU * num_cus() / 8);
-  hipLaunchKernelGGL((k_wino<IN1, EPI>), dim3(grid), dim3(256), 0, st, a, (int)tiles);
+  hipLaunchKernelGGL((k_wino<IN1, EPI, WINO_SPLIT>), dim3(grid), dim3(WINO_SPLIT ? 512 : 256), 0, st, a, (int)tiles);
   return stif_check_launch("stif_conv3x3_wino");
 }
 
