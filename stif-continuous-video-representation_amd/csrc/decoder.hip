@@ -115,7 +115,10 @@ STIF_DEV f32x4 img_sample(const float* __restrict__ I, const Bilin& b, int hf) {
 // is being consumed (double-buffered, one barrier per segment), and every wave reads its A
 // operands from LDS -- one tile feeds 16 MFMAs in each wave of the workgroup.
 constexpr int DEC_NW = 8;    // waves per workgroup of k_dec1 (178 VGPRs: 2 waves/SIMD)
-constexpr int DEC2_NW = 4;   // k_dec2 keeps 8 layer-2 tiles (128 VGPRs) live: 1 wave/SIMD
+constexpr int DEC2_NW = 4;   // k_dec2: 8 layer-3 accumulator tiles (128 VGPRs) live
+#ifndef DEC2_WPE
+#define DEC2_WPE 2           // waves per SIMD k_dec2 is register-budgeted for (2 workgroups/CU, 80 KB LDS each)
+#endif
 constexpr int SEG = 10;      // max tiles per segment
 
 // Buffer loads with the tile offset in SGPRs: the per-lane operand is the same lane*16 for every
@@ -325,7 +328,7 @@ __global__ __launch_bounds__(DEC_NW * 64) void k_dec1(const float* __restrict__ 
 }
 
 template <bool HRIMG>
-__global__ __launch_bounds__(DEC2_NW * 64) void k_dec2(const float* __restrict__ proj, const float* __restrict__ mlp,
+__global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DEC2_WPE))) void k_dec2(const float* __restrict__ proj, const float* __restrict__ mlp,
                                                      const float* __restrict__ hrfeat, const float* __restrict__ flow,
                                                      stif_dec_tables tb, stif_dec_image im,
                                                      const float* __restrict__ tq, float* __restrict__ out, int n,
@@ -362,17 +365,13 @@ __global__ __launch_bounds__(DEC2_NW * 64) void k_dec2(const float* __restrict__
   // ---- encode_imnet layer 0: W[:, :128] . [q_feat1 | q_feat2] + P3(grid1) + P4(grid2) + w_t t + b
   f32x16 x0[2];
   {
-    // four 64-channel bilinear gathers (32 x 16-B loads per lane each); the compiler barriers
-    // keep it from hoisting all 128 loads at once (VGPR budget)
-    f32x16 q[4];
-    gather64(q, HRF, 64, 0, bilin(g1x, g1y, WW, HH), hf);
-    asm volatile("" ::: "memory");
-    gather64(q + 2, HRF, 64, 0, bilin(g2x, g2y, WW, HH), hf);
-    asm volatile("" ::: "memory");
-    f32x16 z[2], z2[2];
+    // four 64-channel bilinear gathers (32 x 16-B loads per lane each), consumed one at a time so
+    // at most two 64-wide register tiles are live (2 waves/SIMD fit in 256 VGPRs); the compiler
+    // barriers keep it from hoisting the next gather's loads over the current one
+    f32x16 z[2], q[2];
     gather64(z, P, PROJ_C, 128, bilin(g1x, g1y, w, h), hf);
     asm volatile("" ::: "memory");
-    gather64(z2, P, PROJ_C, 192, bilin(g2x, g2y, w, h), hf);
+    gather64(q, P, PROJ_C, 192, bilin(g2x, g2y, w, h), hf);
 #pragma unroll
     for (int ot = 0; ot < 2; ++ot)
 #pragma unroll
@@ -380,19 +379,27 @@ __global__ __launch_bounds__(DEC2_NW * 64) void k_dec2(const float* __restrict__
         const int f = ot * 32 + 8 * v + 4 * hf;
         const f32x4 wt = ld4(mlp + E_WT + f), bb = ld4(mlp + E_B0 + f);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) z[ot][4 * v + e] += z2[ot][4 * v + e] + wt[e] * t + bb[e];
+        for (int e = 0; e < 4; ++e) z[ot][4 * v + e] += q[ot][4 * v + e] + wt[e] * t + bb[e];
       }
     if constexpr (HRIMG) {   // q_img1 / q_img2 from the high-resolution image (decoding_test :558-583)
       const float* I = im.img + (size_t)item * im.ih * im.iw * IMG_C;
       img_mma(z, mlp + I_E1, img_sample(I, bilin(g1x, g1y, im.iw, im.ih), hf), lane);
       img_mma(z, mlp + I_E2, img_sample(I, bilin(g2x, g2y, im.iw, im.ih), hf), lane);
     }
+    asm volatile("" ::: "memory");
+    gather64(q, HRF, 64, 0, bilin(g1x, g1y, WW, HH), hf);   // q_feat1 -> W0 columns 0..63
     lds_dma_barrier();
     dma_tiles<DEC2_NW>(B1, rm, E_W1, 4, wv, lane);
 #pragma unroll
+    for (int ot = 0; ot < 2; ++ot)
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) tile_mma(z[ot], B0 + (ot * 4 + kt) * T, q[kt], lane);
+    asm volatile("" ::: "memory");
+    gather64(q, HRF, 64, 0, bilin(g2x, g2y, WW, HH), hf);   // q_feat2 -> W0 columns 64..127
+#pragma unroll
     for (int ot = 0; ot < 2; ++ot) {
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt) tile_mma(z[ot], B0 + (ot * 4 + kt) * T, q[kt], lane);
+      for (int kt = 2; kt < 4; ++kt) tile_mma(z[ot], B0 + (ot * 4 + kt) * T, q[kt - 2], lane);
 #pragma unroll
       for (int r = 0; r < 16; ++r) x0[ot][r] = stif_sin(30.0f * z[ot][r]);
     }
