@@ -114,7 +114,13 @@ STIF_DEV f32x4 img_sample(const float* __restrict__ I, const Bilin& b, int hf) {
 // (a few 4-KB tiles: one layer, or one output tile's K-tiles) is LDS-DMA'd while the previous one
 // is being consumed (double-buffered, one barrier per segment), and every wave reads its A
 // operands from LDS -- one tile feeds 16 MFMAs in each wave of the workgroup.
-constexpr int DEC_NW = 8;    // waves per workgroup of k_dec1 (178 VGPRs: 2 waves/SIMD)
+#ifndef DEC1_NW
+#define DEC1_NW 4
+#endif
+// waves per workgroup of k_dec1 (~240 VGPRs: 2 waves/SIMD).  4-wave workgroups, 2 per CU (80 KB LDS
+// each): the two waves sharing a SIMD come from different workgroups, so one's segment barrier or
+// sin stretch overlaps the other's MFMAs
+constexpr int DEC_NW = DEC1_NW;
 constexpr int DEC2_NW = 4;   // k_dec2: 8 layer-3 accumulator tiles (128 VGPRs) live
 #ifndef DEC2_WPE
 #define DEC2_WPE 2           // waves per SIMD k_dec2 is register-budgeted for (2 workgroups/CU, 80 KB LDS each)
@@ -153,7 +159,7 @@ STIF_DEV void tile_mma(f32x16& acc, const float* t, const f32x16& x, int lane) {
 // MODE 1: feat_imnet only; MODE 2: flow_imnet only, reading HRfeat at (hr_y, hr_x) of the query
 // (local ensemble).  HRIMG: the flow stage's image input comes from the high-resolution image.
 template <int MODE, bool HRIMG>
-__global__ __launch_bounds__(DEC_NW * 64) void k_dec1(const float* __restrict__ proj, const float* __restrict__ mlp,
+__global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))) void k_dec1(const float* __restrict__ proj, const float* __restrict__ mlp,
                                                      stif_dec_tables tb, stif_dec_image im,
                                                      const float* __restrict__ tq, float* __restrict__ hrfeat,
                                                      float* __restrict__ flow, int n, int h, int w, int HH,
