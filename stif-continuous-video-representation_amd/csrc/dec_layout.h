@@ -42,7 +42,14 @@ constexpr int I_E1 = I_L + 2 * T;      // encode_imnet.net.0 columns 512..517 (q
 constexpr int I_E2 = I_E1 + 2 * T;     // encode_imnet.net.0 columns 518..523 (q_img2)
 constexpr int I_END = I_E2 + 2 * T;
 
-constexpr int MLP_FLOATS = I_END;
+// the two narrow last layers (flow 256 -> 4, rgb 256 -> 3) as plain row-major [out][256] rows: they
+// run as per-lane VALU dot products over the lane's 128 features + one cross-half add, instead of
+// 128 MFMAs per 32 pixels of which 28/32 (29/32) would multiply zero-padded rows
+constexpr int L_W3V = I_END;             // [4][256]
+constexpr int E_W4V = L_W3V + 4 * 256;   // [3][256], padded to a whole 4-KB tile (LDS-DMA granule)
+constexpr int V_END = E_W4V + 1024;
+
+constexpr int MLP_FLOATS = V_END;
 constexpr int IMG_C = 8;      // high-resolution image channels: rgb0 rgb1 + 2 zero (16-B aligned pixels)
 constexpr int PROJ_C = 256;   // LR projection channels: P1 | P2 | P3 | P4
 constexpr int SRC_C = 200;    // LR source channels: feat t0|t1|t2 (192) + rgb0 rgb1 (6) + 2 zero

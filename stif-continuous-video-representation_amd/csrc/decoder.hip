@@ -125,7 +125,8 @@ constexpr int DEC2_NW = 4;   // k_dec2: 8 layer-3 accumulator tiles (128 VGPRs) 
 #ifndef DEC2_WPE
 #define DEC2_WPE 2           // waves per SIMD k_dec2 is register-budgeted for (2 workgroups/CU, 80 KB LDS each)
 #endif
-constexpr int SEG = 10;      // max tiles per segment
+constexpr int SEG = 10;      // max tiles per segment (k_dec2)
+constexpr int SEG1 = 8;      // max tiles per segment (k_dec1)
 
 // Buffer loads with the tile offset in SGPRs: the per-lane operand is the same lane*16 for every
 // tile (flat global_load_lds would keep a 64-bit VGPR address per hoisted tile live).
@@ -155,6 +156,20 @@ STIF_DEV void tile_mma(f32x16& acc, const float* t, const f32x16& x, int lane) {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// o[c] += W[c][32 kt + F(r, hf)] . x[r] over this lane's 16 features of register tile kt (W: plain
+// [NO][256] rows in LDS; the two lane halves read two addresses per instruction, a broadcast)
+template <int NO>
+STIF_DEV void narrow_dot(float* o, const float* W, int kt, const f32x16& x, int hf) {
+#pragma unroll
+  for (int c = 0; c < NO; ++c)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const f32x4 w = ld4(W + c * 256 + kt * 32 + 8 * v + 4 * hf);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[c] = fmaf(w[e], x[4 * v + e], o[c]);
+    }
+}
+
 // MODE 0: feat_imnet + flow_imnet fused (the flow stage reads the pixel's own HRfeat);
 // MODE 1: feat_imnet only; MODE 2: flow_imnet only, reading HRfeat at (hr_y, hr_x) of the query
 // (local ensemble).  HRIMG: the flow stage's image input comes from the high-resolution image.
@@ -164,12 +179,15 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
                                                      const float* __restrict__ tq, float* __restrict__ hrfeat,
                                                      float* __restrict__ flow, int n, int h, int w, int HH,
                                                      int WW) {
-  __shared__ __attribute__((aligned(16))) float wbuf[2 * SEG * T];
+  // two segment buffers of SEG1 tiles + the flow's last layer (plain [4][256], resident)
+  __shared__ __attribute__((aligned(16))) float wbuf[2 * SEG1 * T + T];
   const int lane = threadIdx.x & 63, hf = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
   float* const B0 = wbuf;
-  float* const B1 = wbuf + SEG * T;
+  float* const B1 = wbuf + SEG1 * T;
+  float* const W3V = wbuf + 2 * SEG1 * T;
   const __amdgpu_buffer_rsrc_t rm = mlp_rsrc(mlp);
+  if (MODE != 1) dma_tiles<DEC_NW>(W3V, rm, L_W3V, 1, wv, lane);
   // segment 0: feat layer 1 (4 tiles); segments 1..8: feat layer 2 tile kt + layer 3 (0, kt), (1, kt)
   if (MODE != 2) dma_tiles<DEC_NW>(B0, rm, F_W1, 4, wv, lane);
   else {   // flow only: flow layers 0 / 1 straight into B1
@@ -292,9 +310,8 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
   }
   // flow layers 0/1 live in B1 (prefetched during the last feat segment, or at the start)
   lds_dma_barrier();
-  auto seg_flow23 = [&](float* dst, int kt) {   // W2 rows kt (2 tiles), W3 (kt)
+  auto seg_flow23 = [&](float* dst, int kt) {   // W2 rows kt (2 tiles); W3 is resident (W3V)
     dma_tiles<DEC_NW>(dst, rm, L_W2 + kt * 2 * T, 2, wv, lane);
-    dma_tiles<DEC_NW>(dst + 2 * T, rm, L_W3 + kt * T, 1, wv, lane);
   };
   seg_flow23(B0, 0);
 #pragma unroll
@@ -311,7 +328,7 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
     for (int kt = 0; kt < 2; ++kt) tile_mma(acc, B1 + (4 + ot * 2 + kt) * T, z[kt], lane);
     x1[ot] = bias_sin(acc, mlp + L_B1 + ot * 32, hf);
   }
-  f32x16 fl = f32x16{0};
+  float fl[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
   for (int kt = 0; kt < 8; ++kt) {
     lds_dma_barrier();
@@ -322,8 +339,10 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
     tile_mma(acc, cur, x1[0], lane);
     tile_mma(acc, cur + T, x1[1], lane);
     const f32x16 h2 = bias_sin(acc, mlp + L_B2 + kt * 32, hf);
-    tile_mma(fl, cur + 2 * T, h2, lane);
+    narrow_dot<4>(fl, W3V, kt, h2, hf);   // flow_imnet.net.3 (256 -> 4, linear)
   }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) fl[c] += __shfl_xor(fl[c], 32);   // the other lane half's 128 features
   if (valid && hf == 0) {
     const f32x4 bb = ld4(mlp + L_B3);
     f32x4 s;
@@ -441,7 +460,7 @@ __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DE
     float* cur = (kt & 1) ? B1 : B0;
     float* nxt = (kt & 1) ? B0 : B1;
     if (kt < 7) seg_l23(nxt, kt + 1);
-    else dma_tiles<DEC2_NW>(nxt, rm, E_W4, 8, wv, lane);
+    else dma_tiles<DEC2_NW>(nxt, rm, E_W4V, 1, wv, lane);
     f32x16 acc = f32x16{0};
     tile_mma(acc, cur, x1[0], lane);
     tile_mma(acc, cur + T, x1[1], lane);
@@ -449,14 +468,17 @@ __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DE
 #pragma unroll
     for (int ot = 0; ot < 8; ++ot) tile_mma(a3[ot], cur + (2 + ot) * T, h2, lane);
   }
-  // layer 3 sine streamed into layer 4 (256 -> 3, linear); W4 sits in B0 (kt = 7 prefetch)
+  // layer 3 sine streamed into layer 4 (256 -> 3, linear, VALU dot products); W4 sits in B0 as
+  // plain rows (kt = 7 prefetch)
   lds_dma_barrier();
-  f32x16 o4 = f32x16{0};
+  float o4[3] = {0.f, 0.f, 0.f};
 #pragma unroll
   for (int kt = 0; kt < 8; ++kt) {
     const f32x16 h3 = bias_sin(a3[kt], mlp + E_B3 + kt * 32, hf);
-    tile_mma(o4, B0 + kt * T, h3, lane);
+    narrow_dot<3>(o4, B0, kt, h3, hf);
   }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) o4[c] += __shfl_xor(o4[c], 32);   // the other lane half's 128 features
   if (valid && hf == 0) {
     const size_t plane = (size_t)HH * WW;
     float* o = out + (size_t)item * 3 * plane + (size_t)py * WW + px;

@@ -253,5 +253,8 @@ extern "C" int stif_pack_dec_mlp(const float* const* f, const float* const* l, c
   pack_tiles(d + I_L, l[0], 263, 0, 256, 64, 6);
   pack_tiles(d + I_E1, e[0], 525, 0, 512, 64, 6);
   pack_tiles(d + I_E2, e[0], 525, 0, 518, 64, 6);
+  // plain last layers for the VALU dot products
+  memcpy(d + L_W3V, l[6], sizeof(float) * 4 * 256);
+  memcpy(d + E_W4V, e[8], sizeof(float) * 3 * 256);
   return STIF_OK;
 }

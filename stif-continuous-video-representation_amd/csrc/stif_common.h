@@ -31,6 +31,9 @@ enum { STIF_ACT_NONE = 0, STIF_ACT_LRELU = 1, STIF_ACT_RELU = 2, STIF_ACT_RES = 
 // |x| <= 3000 (glibc sinf: 3.3e-8); SIREN arguments 30*z stay far inside the range.
 // Used instead of ocml sinf, whose Payne-Hanek path costs ~200 VGPRs in the MLP kernels.
 STIF_DEV float stif_sin(float x) {
+#ifdef DEC_EXP_NOSIN
+  return x * 0.001f;   // kernel experiment: the cost of the sines
+#endif
   const float q = rintf(x * 0.636619772367581343f);
   const int qi = (int)q;
   float r = fmaf(q, -1.5703125f, x);

@@ -249,8 +249,8 @@ def dec_stage1(proj, mlp, tables: DecTablesDev, t, hrfeat, flow, image: "DecImag
     n, h, w, _ = proj.shape
     HH, WW = hrfeat.shape[1:3]
     tr = TRACE
-    if tr is not None:   # executed MFMA work: 1,088 v_mfma_f32_32x32x2_f32 per 32 HR pixels
-        tr.begin(("dec1",), 1088 / 32 * 4096.0 * n * HH * WW)
+    if tr is not None:   # per HR px: feat_imnet layers 1-3 (36,864 MAC) + flow_imnet HRfeat/1-3 (25,600 MAC)
+        tr.begin(("dec1",), 2.0 * 62464 * n * HH * WW)
     L.check(L.lib().stif_dec_stage1(_vp(proj), _vp(mlp), C.byref(tables.c), C.byref(image.c) if image else None,
                                     _vp(t), _vp(hrfeat), _vp(flow), n, h, w, HH, WW, _stream()), "stif_dec_stage1")
     if tr is not None:
@@ -261,8 +261,8 @@ def dec_stage2(proj, mlp, hrfeat, flow, tables: DecTablesDev, t, out, image: "De
     n, h, w, _ = proj.shape
     HH, WW = hrfeat.shape[1:3]
     tr = TRACE
-    if tr is not None:   # executed MFMA work: 1,600 v_mfma_f32_32x32x2_f32 per 32 HR pixels
-        tr.begin(("dec2",), 1600 / 32 * 4096.0 * n * HH * WW)
+    if tr is not None:   # per HR px: encode_imnet HRfeat part + layers 1-4 (94,976 MAC)
+        tr.begin(("dec2",), 2.0 * 94976 * n * HH * WW)
     L.check(L.lib().stif_dec_stage2(_vp(proj), _vp(mlp), _vp(hrfeat), _vp(flow), C.byref(tables.c),
                                     C.byref(image.c) if image else None, _vp(t), _vp(out), n, h, w, HH, WW,
                                     _stream()), "stif_dec_stage2")
