@@ -26,13 +26,14 @@ namespace {
 
 using namespace stif_dec;
 
-// SineLayer: sin(30 * (z + b))  (SIREN.py:44-45, omega_0 = 30)
+// SineLayer: sin(30 * (z + b)) (SIREN.py:44-45, omega_0 = 30); the packed weights and biases of every
+// sine layer carry the factor 30 (pack.cpp), so the kernel evaluates sin(z + b)
 STIF_DEV f32x16 bias_sin(f32x16 z, const float* __restrict__ b, int hf) {
 #pragma unroll
   for (int v = 0; v < 4; ++v) {
     const f32x4 bb = ld4(b + 8 * v + 4 * hf);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) z[4 * v + e] = stif_sin(30.0f * (z[4 * v + e] + bb[e]));
+    for (int e = 0; e < 4; ++e) z[4 * v + e] = stif_sin(z[4 * v + e] + bb[e]);
   }
   return z;
 }
@@ -219,7 +220,7 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
         const int f = ot * 32 + 8 * v + 4 * hf;
         const f32x4 z = ld4(p1 + f) + ld4(mlp + F_WRY + f) * ry + ld4(mlp + F_WRX + f) * rx + ld4(mlp + F_WT + f) * t;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) x0[ot][4 * v + e] = stif_sin(30.0f * z[e]);
+        for (int e = 0; e < 4; ++e) x0[ot][4 * v + e] = stif_sin(z[e]);
       }
   }
   auto seg_feat23 = [&](float* dst, int kt) {   // W2 rows kt (2 tiles), W3 (0, kt), (1, kt)
@@ -319,7 +320,7 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) tile_mma(z[ot], B1 + (ot * 2 + kt) * T, hr[kt], lane);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) z[ot][r] = stif_sin(30.0f * z[ot][r]);
+    for (int r = 0; r < 16; ++r) z[ot][r] = stif_sin(z[ot][r]);
   }
 #pragma unroll
   for (int ot = 0; ot < 2; ++ot) {
@@ -426,7 +427,7 @@ __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DE
 #pragma unroll
       for (int kt = 2; kt < 4; ++kt) tile_mma(z[ot], B0 + (ot * 4 + kt) * T, q[kt - 2], lane);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) x0[ot][r] = stif_sin(30.0f * z[ot][r]);
+      for (int r = 0; r < 16; ++r) x0[ot][r] = stif_sin(z[ot][r]);
     }
   }
   lds_dma_barrier();

@@ -83,6 +83,16 @@ void column(float* dst, const float* W, int ld, int rows, int col) {
   for (int i = 0; i < rows; ++i) dst[i] = W[(size_t)i * ld + col];
 }
 
+// SineLayer: sin(omega_0 * (W x + b)) with omega_0 = 30 (SIREN.py:44-51): the packed copies of every
+// sine layer's weights and bias carry the factor (computed in double, rounded once), so the kernels
+// evaluate sin(W' x + b') without the multiply
+constexpr double OMEGA0 = 30.0;
+std::vector<float> omega(const float* src, size_t n) {
+  std::vector<float> d(n);
+  for (size_t i = 0; i < n; ++i) d[i] = (float)(OMEGA0 * (double)src[i]);
+  return d;
+}
+
 }  // namespace
 
 extern "C" size_t stif_conv_weight_floats(int cout, int cin, int ks, int mode) {
@@ -188,6 +198,13 @@ extern "C" int stif_pack_dec_proj_ex(const float* feat_w0, const float* feat_b0,
     return stif_fail(STIF_E_INVALID, "stif_pack_dec_proj: null");
   const int C = stif_dec::SRC_C;
   std::vector<float> W((size_t)256 * C, 0.f), B(256, 0.f);
+  // first layers are sine layers: omega_0-scaled (see stif_pack_dec_mlp)
+  const std::vector<float> fw = omega(feat_w0, 64 * 201), fb = omega(feat_b0, 64), lw = omega(flow_w0, 64 * 263),
+                           ew = omega(enc_w0, 64 * 525);
+  feat_w0 = fw.data();
+  feat_b0 = fb.data();
+  flow_w0 = lw.data();
+  enc_w0 = ew.data();
   for (int o = 0; o < 64; ++o) {
     for (int c = 0; c < 198; ++c) {
       W[(size_t)o * C + c] = feat_w0[(size_t)o * 201 + c];
@@ -208,6 +225,8 @@ extern "C" int stif_pack_dec_proj_ex(const float* feat_w0, const float* feat_b0,
 
 extern "C" size_t stif_dec_mlp_floats(void) { return stif_dec::MLP_FLOATS; }
 
+
+
 extern "C" int stif_pack_dec_mlp(const float* const* f, const float* const* l, const float* const* e,
                                  float* d) {
   using namespace stif_dec;
@@ -217,6 +236,30 @@ extern "C" int stif_pack_dec_mlp(const float* const* f, const float* const* l, c
   for (int i = 0; i < 10; ++i)
     if (!e[i]) return stif_fail(STIF_E_INVALID, "stif_pack_dec_mlp: null layer");
   memset(d, 0, sizeof(float) * MLP_FLOATS);
+  // omega_0-scaled copies of the sine layers (all but the last, linear, layer of each MLP)
+  std::vector<float> fs[6], ls[6], es[8];
+  const size_t fn[6] = {64 * 201, 64, 64 * 64, 64, 256 * 64, 256};
+  const size_t ln[6] = {64 * 263, 64, 64 * 64, 64, 256 * 64, 256};
+  const size_t en[8] = {64 * 525, 64, 64 * 64, 64, 256 * 64, 256, 256 * 256, 256};
+  const float* F[8];
+  const float* Lw[8];
+  const float* E[10];
+  for (int i = 0; i < 6; ++i) {
+    fs[i] = omega(f[i], fn[i]);
+    ls[i] = omega(l[i], ln[i]);
+    F[i] = fs[i].data();
+    Lw[i] = ls[i].data();
+  }
+  for (int i = 0; i < 8; ++i) {
+    es[i] = omega(e[i], en[i]);
+    E[i] = es[i].data();
+  }
+  F[6] = f[6]; F[7] = f[7];
+  Lw[6] = l[6]; Lw[7] = l[7];
+  E[8] = e[8]; E[9] = e[9];
+  f = F;
+  l = Lw;
+  e = E;
   // feat_imnet: f = {w0[64x201], b0, w1[64x64], b1, w2[256x64], b2, w3[64x256], b3}
   column(d + F_WRY, f[0], 201, 64, 198);
   column(d + F_WRX, f[0], 201, 64, 199);

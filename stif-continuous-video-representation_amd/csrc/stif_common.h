@@ -26,26 +26,27 @@ STIF_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 enum { STIF_ACT_NONE = 0, STIF_ACT_LRELU = 1, STIF_ACT_RELU = 2, STIF_ACT_RES = 3,
        STIF_ACT_OFFMASK = 4, STIF_ACT_LSTM = 5 };
 
-// sin(x) with Cody-Waite reduction by pi/2 (3-part constant, exact q*C1 for |q| < 2^16)
-// and the cephes minimax polynomials on [-pi/4, pi/4].  Max abs error 9.3e-8 over
-// |x| <= 3000 (glibc sinf: 3.3e-8); SIREN arguments 30*z stay far inside the range.
-// Used instead of ocml sinf, whose Payne-Hanek path costs ~200 VGPRs in the MLP kernels.
+// sin(x): Cody-Waite reduction by pi (3-part constant, q * P1 exact for |q| < 2^16), then an odd
+// degree-11 polynomial on [-pi/2, pi/2] (coefficients fitted by iteratively reweighted least
+// squares, near-minimax) and the sign of (-1)^q.  Max abs error 1.2e-7 over |x| <= 3000 (glibc
+// sinf: 3.3e-8); 15 VALU ops.  Used instead of ocml sinf, whose Payne-Hanek path costs ~200 VGPRs
+// in the MLP kernels.
 STIF_DEV float stif_sin(float x) {
 #ifdef DEC_EXP_NOSIN
   return x * 0.001f;   // kernel experiment: the cost of the sines
 #endif
-  const float q = rintf(x * 0.636619772367581343f);
-  const int qi = (int)q;
-  float r = fmaf(q, -1.5703125f, x);
-  r = fmaf(q, -4.837512969970703125e-4f, r);
-  r = fmaf(q, -7.54978995489188216e-8f, r);
+  const float q = rintf(x * 0.318309886183790671538f);
+  float r = fmaf(q, -3.140625f, x);
+  r = fmaf(q, -9.67502593994140625e-4f, r);
+  r = fmaf(q, -1.509957990e-7f, r);
   const float r2 = r * r;
-  const float s = fmaf(r * r2, fmaf(r2, fmaf(r2, -1.9515295891e-4f, 8.3321608736e-3f), -1.6666654611e-1f), r);
-  const float c = fmaf(r2 * r2, fmaf(r2, fmaf(r2, 2.443315711809948e-5f, -1.388731625493765e-3f),
-                                     4.166664568298827e-2f),
-                       fmaf(-0.5f, r2, 1.0f));
-  const float res = (qi & 1) ? c : s;
-  return (qi & 2) ? -res : res;
+  float p = fmaf(r2, -2.3845164e-08f, 2.7522526e-06f);
+  p = fmaf(r2, p, -1.9840802e-04f);
+  p = fmaf(r2, p, 8.3333300e-03f);
+  p = fmaf(r2, p, -1.6666667e-01f);
+  const float s = fmaf(r * r2, p, r);
+  // (-1)^q: flip the sign bit when q is odd
+  return __int_as_float(__float_as_int(s) ^ (((int)q & 1) << 31));
 }
 
 // Epilogue helper: write one 32 px x 32 cout accumulator tile (lane = cout, regs = px) into the

@@ -106,8 +106,9 @@ def test_pack_dec_mlp_tile_layout(stif, sd):
                 for e in range(4):
                     q = 4 * v + e
                     f = (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5)
-                    assert tile[v, lane, e] == W1[ot * 32 + (lane & 31), kt * 32 + f]
-    assert np.array_equal(mlp[0:64], arrs["feat_imnet."][0][:, 198])
+                    # sine layers carry omega_0 = 30 (SIREN.py:44-51), scaled in double
+                    assert tile[v, lane, e] == np.float32(30.0 * np.float64(W1[ot * 32 + (lane & 31), kt * 32 + f]))
+    assert np.array_equal(mlp[0:64], (30.0 * arrs["feat_imnet."][0][:, 198].astype(np.float64)).astype(np.float32))
 
 
 def test_decoder_tables_match_reference_nearest(stif, golden):
