@@ -110,35 +110,39 @@ __global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
     const float* sw = st + T_F;
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
-      // modulated_deformable_im2col (dcn_v2_im2col_cuda.cu:158-192) for this lane's pixel / tap
+      // modulated_deformable_im2col (dcn_v2_im2col_cuda.cu:158-192) for this lane's pixel / tap.
+      // Common case without branches: the 2x2 footprint lies in the staged tile (zeros outside the
+      // frame = dmcn_im2col_bilinear's per-corner checks), the `> -1 / < H` gate and the mask are
+      // folded into the corner weights; a wave-uniform branch handles the rare lanes whose offset
+      // leaves the tile margin with global loads.
       const float h_im = (float)(oy - 1 + tap / 3) + omc[tap * 3];
       const float w_im = (float)(ox - 1 + tap % 3) + omc[tap * 3 + 1];
-      f32x4 av = f32x4{0};
+      const bool valid = pix_ok & (h_im > -1.f) & (w_im > -1.f) & (h_im < (float)H) & (w_im < (float)W);
+      const float fh = floorf(h_im), fw = floorf(w_im);
+      const float lh = h_im - fh, lw = w_im - fw, hh = 1.f - lh, hw = 1.f - lw;
+      const int h_low = (int)fh, w_low = (int)fw;
+      const int r0 = h_low - ty0, c0 = w_low - tx0;
+      const bool in_tile = ((unsigned)r0 < (unsigned)(TR - 1)) & ((unsigned)c0 < (unsigned)(TC - 1));
+      const float m = valid ? omc[tap * 3 + 2] : 0.f;
+      const float hm = hh * m, lm = lh * m;
+      const float w1 = hm * hw, w2 = hm * lw, w3 = lm * hw, w4 = lm * lw;
+      const float* p0 = st + (((in_tile ? r0 : 0) * 2 + hf) * TC + (in_tile ? c0 : 0)) * 4;
+      const float* p1 = p0 + 2 * TC * 4;
+      f32x4 av = w1 * ld4(p0) + w2 * ld4(p0 + 4) + w3 * ld4(p1) + w4 * ld4(p1 + 4);
 #ifdef DCN_EXP_NOSAMPLE
-      av = f32x4{h_im, w_im, 1.f, 2.f};
-      if (0)
+      av = f32x4{h_im, w_im, 1.f, m};
 #endif
-      if (pix_ok && h_im > -1.f && w_im > -1.f && h_im < (float)H && w_im < (float)W) {
-        const float fh = floorf(h_im), fw = floorf(w_im);
-        const int h_low = (int)fh, w_low = (int)fw;
-        const float lh = h_im - fh, lw = w_im - fw, hh = 1.f - lh, hw = 1.f - lw;
-        const int r0 = h_low - ty0, c0 = w_low - tx0;
-        f32x4 v1, v2, v3, v4;
-        if (r0 >= 0 && r0 + 1 < TR && c0 >= 0 && c0 + 1 < TC) {
-          // in the staged tile (zero outside the frame = dmcn_im2col_bilinear's corner checks)
-          const float* p0 = st + ((r0 * 2 + hf) * TC + c0) * 4;
-          const float* p1 = p0 + 2 * TC * 4;
-          v1 = ld4(p0); v2 = ld4(p0 + 4); v3 = ld4(p1); v4 = ld4(p1 + 4);
-        } else {
+      const bool fb = valid & !in_tile;
+      if (__builtin_amdgcn_ballot_w64(fb)) {
+        if (fb) {
           const int h_high = h_low + 1, w_high = w_low + 1, co = dg * 8 + hf * 4;
-          v1 = (h_low >= 0 && w_low >= 0) ? ld4(in + ((size_t)h_low * W + w_low) * 64 + co) : f32x4{0};
-          v2 = (h_low >= 0 && w_high <= W - 1) ? ld4(in + ((size_t)h_low * W + w_high) * 64 + co) : f32x4{0};
-          v3 = (h_high <= H - 1 && w_low >= 0) ? ld4(in + ((size_t)h_high * W + w_low) * 64 + co) : f32x4{0};
-          v4 = (h_high <= H - 1 && w_high <= W - 1) ? ld4(in + ((size_t)h_high * W + w_high) * 64 + co)
-                                                     : f32x4{0};
+          const f32x4 v1 = (h_low >= 0 && w_low >= 0) ? ld4(in + ((size_t)h_low * W + w_low) * 64 + co) : f32x4{0};
+          const f32x4 v2 = (h_low >= 0 && w_high <= W - 1) ? ld4(in + ((size_t)h_low * W + w_high) * 64 + co) : f32x4{0};
+          const f32x4 v3 = (h_high <= H - 1 && w_low >= 0) ? ld4(in + ((size_t)h_high * W + w_low) * 64 + co) : f32x4{0};
+          const f32x4 v4 =
+              (h_high <= H - 1 && w_high <= W - 1) ? ld4(in + ((size_t)h_high * W + w_high) * 64 + co) : f32x4{0};
+          av = w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4;
         }
-        const float w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
-        av = (w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4) * omc[tap * 3 + 2];
       }
       const f32x4 b0 = ld4(sw + ((tap * 2 + 0) * 64 + lane) * 4);
       const f32x4 b1 = ld4(sw + ((tap * 2 + 1) * 64 + lane) * 4);
