@@ -20,7 +20,8 @@
 //   * the output transform's sum over j happens in registers (P_i = M_i A), only the sum over
 //     i crosses waves (an LDS exchange per 32-cout half, balanced over all 4 waves).
 // Input halo tiles (6 rows x 34 columns x 32 channels per phase) are LDS-DMA'd, double-buffered,
-// even and odd columns in separate runs so a lane's 4 patch columns are conflict-free reads.
+// even and odd columns in separate runs, a pixel's channel chunks consecutive (coalesced loads) at an
+// odd pitch (conflict-free transform reads).
 #include "abi_util.h"
 #include "stif.h"
 #include "stif_common.h"
@@ -37,7 +38,12 @@ constexpr int PSUB = 4;    // 8-channel chunks per staging phase
 #else
 constexpr int PSUB = WINO_PSUB;
 #endif
-constexpr int IN_EL = HR * PSUB * 2 * HC;      // 16-B elements per phase buffer
+// phase image: [halo row][column slot][16-B channel chunk: 2 * PSUB of them + 1 pad] -- a pixel's
+// chunks are consecutive, so 8 lanes of an LDS-DMA instruction read one pixel's 128 B (8 cache
+// lines per instruction instead of 64), and the odd pitch (2 * PSUB + 1 = 9 slots) keeps 16
+// consecutive pixels in 16 distinct bank groups for the transform's ds_read_b128
+constexpr int PITCH = 2 * PSUB + 1;
+constexpr int IN_EL = HR * HC * PITCH;      // 16-B elements per phase buffer
 constexpr int IN_INST = (IN_EL + 63) / 64;     // LDS-DMA instructions per phase
 constexpr int EX_F = 2 * 2 * 2 * 1024;         // epilogue exchange: [wave 1|2][nt][b][32 tiles][32 co]
 constexpr int BUF_F = (IN_INST * 256 > EX_F) ? IN_INST * 256 : EX_F;   // floats per buffer (32 KB)
@@ -131,13 +137,13 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256) __attribute__((amdgpu_waves_per_
     for (int q = wv; q < IN_INST; q += NWV) {
       // 16-B element e of the phase image = (halo row, 8-channel sub-chunk, half h, column slot)
       const int e = q * 64 + lane;
-      const int slot = e % HC;
-      const int rest = e / HC;
-      const int h = rest & 1, sub = (rest >> 1) % PSUB, row = (rest >> 1) / PSUB;
+      const int px = e / PITCH;                 // pixel = row * HC + column slot
+      const int ck = e - px * PITCH;            // 16-B chunk (channels cbase + 4 ck ..), PITCH - 1 = pad
+      const int row = px / HC, slot = px - row * HC;
       const int col = slot < 17 ? 2 * slot : 2 * (slot - 17) + 1;
       const int y = iy0 + row, x = ix0 + col;
-      const bool ok = (e < IN_EL) & ((unsigned)y < (unsigned)H) & ((unsigned)x < (unsigned)W);
-      const unsigned voff = ok ? (unsigned)(((y * W + x) * Cs + cbase + sub * 8 + h * 4) * 4) : 0x80000000u;
+      const bool ok = (e < IN_EL) & (ck < 2 * PSUB) & ((unsigned)y < (unsigned)H) & ((unsigned)x < (unsigned)W);
+      const unsigned voff = ok ? (unsigned)(((y * W + x) * Cs + cbase + ck * 4) * 4) : 0x80000000u;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, dst + q * 256, 16, voff, 0, 0, 0);
     }
   };
@@ -153,12 +159,12 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256) __attribute__((amdgpu_waves_per_
   // one chunk ahead where registers allow, so their latency hides under the current chunk's MFMAs)
   // and the add/subtract part.
   auto xread = [&](const float* buf, int s, f32x4* rd) {
-    const float* ra = buf + (((2 * tyl + rA) * PSUB + s) * 2 + hf) * HC * 4;
-    const float* rb = buf + (((2 * tyl + rB) * PSUB + s) * 2 + hf) * HC * 4;
-    rd[0] = ld4(ra + s0 * 4); rd[1] = ld4(rb + s0 * 4);
-    rd[2] = ld4(ra + s1 * 4); rd[3] = ld4(rb + s1 * 4);
-    rd[4] = ld4(ra + s2 * 4); rd[5] = ld4(rb + s2 * 4);
-    rd[6] = ld4(ra + s3 * 4); rd[7] = ld4(rb + s3 * 4);
+    const float* ra = buf + ((2 * tyl + rA) * HC * PITCH + 2 * s + hf) * 4;
+    const float* rb = buf + ((2 * tyl + rB) * HC * PITCH + 2 * s + hf) * 4;
+    rd[0] = ld4(ra + s0 * PITCH * 4); rd[1] = ld4(rb + s0 * PITCH * 4);
+    rd[2] = ld4(ra + s1 * PITCH * 4); rd[3] = ld4(rb + s1 * PITCH * 4);
+    rd[4] = ld4(ra + s2 * PITCH * 4); rd[5] = ld4(rb + s2 * PITCH * 4);
+    rd[6] = ld4(ra + s3 * PITCH * 4); rd[7] = ld4(rb + s3 * PITCH * 4);
   };
   auto xform = [&](const f32x4* rd, f32x4* v) {
     const f32x4 t0 = rd[0] + sB * rd[1];
@@ -388,6 +394,311 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256) __attribute__((amdgpu_waves_per_
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_wino_ws: the same operator with warp specialisation.  One workgroup per CU, 8 waves: waves 0-3
+// are the MFMA waves (wave i = transform row i, exactly the k_wino loop), waves 4-7 are helpers
+// sharing their SIMDs: they issue all the LDS-DMA staging (so the MFMA waves' vmcnt queue only holds
+// their own B-operand prefetches and never waits on a DMA), and they run the output transform of
+// tile T-1 from a dedicated 64-KB exchange image while the MFMA waves already compute tile T.
+// The MFMA waves' per-tile epilogue shrinks to summing over j and writing P_i (64 ds_write_b32)
+// before one extra barrier.  Barrier sequence, identical for both roles: one per staging phase,
+// one after the P write.  Staging runs two phases ahead (3 buffers).
+// Measured (s_memtime trace, tools/trace_wino_ws.py): slower than k_wino (465 vs 425 us on the
+// trunk RELU conv at C1).  The MFMA waves alone keep the pipe ~80 % busy inside a phase, but the
+// helpers' LDS-DMA issue is the bottleneck: 8 buffer_load...lds instructions take 8-10K cycles
+// to issue even with the MFMA waves idle (WINO_EXP_NOMFMA), ~3 B/clk per CU -- k_wino hides that
+// cost because two workgroups per CU overlap each other's staging.  Kept behind WINO_WS=1.
+template <int IN1, int EPI>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_wino_ws(stif_conv_args a,
+                                                                                        int ntiles) {
+  constexpr int IN_F = IN_INST * 256;                // floats per staging buffer
+  constexpr int XF = 2 * 4 * 2 * 32 * 32;            // exchange image [nt][i][b][tile 32][co 32]
+  __shared__ __attribute__((aligned(16))) float smem[3 * IN_F + XF];   // 3 staging buffers + exchange
+  float* const X = smem + 3 * IN_F;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool mf = wv < 4;                                    // MFMA wave
+  const int wi = wv & 3;                                     // transform row (MFMA) / helper index
+  const int hf = lane >> 5;
+  const int tl = lane & 31;
+  const int tyl = tl >> 4, txl = tl & 15;
+
+  const int tiles_x = (a.Wo + 31) >> 5;
+  const int tiles_y = (a.Ho + WR - 1) / WR;
+  const int slices = (a.cout + 63) >> 6;
+  const int H = a.H, W = a.W, C0 = a.C0, C1 = a.C1;
+  const int NC0 = C0 >> 3;
+  const int NC = NC0 + (IN1 ? (C1 >> 3) : 0);
+  const int NP = NC / PSUB;
+
+  auto tile_of = [&](int T) {
+    Tile t;
+    t.slice = T % slices;
+    int r = T / slices;
+    const int x = r % tiles_x;
+    r /= tiles_x;
+    const int y = r % tiles_y;
+    r /= tiles_y;
+    t.g = r / a.nitems;
+    t.n = r - t.g * a.nitems;
+    t.oy0 = y * WR;
+    t.ox0 = x * 32;
+    return t;
+  };
+  auto wbase = [&](const Tile& t) { return a.w[t.g] + (size_t)t.slice * NC * 8192 + wi * 2048 + lane * 4; };
+
+  // helpers: LDS-DMA of staging phase p of tile t (the k_wino phase image)
+  auto stage = [&](const Tile& t, int p, int buf) {
+    const bool second = IN1 && p * PSUB >= NC0;
+    const float* src = second ? a.in1[t.g] + (size_t)t.n * a.in1_item : a.in0[t.g] + (size_t)t.n * a.in0_item;
+    const int Cs = second ? C1 : C0;
+    const int cbase = (second ? p * PSUB - NC0 : p * PSUB) * 8;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, (int)((size_t)H * W * Cs * 4), 0x00020000);
+    float* dst = smem + buf * IN_F;
+    const int iy0 = t.oy0 - 1, ix0 = t.ox0 - 1;
+    for (int q = wi; q < IN_INST; q += 4) {
+      const int e = q * 64 + lane;
+      const int px = e / PITCH;                 // pixel = row * HC + column slot
+      const int ck = e - px * PITCH;            // 16-B chunk (channels cbase + 4 ck ..), PITCH - 1 = pad
+      const int row = px / HC, slot = px - row * HC;
+      const int col = slot < 17 ? 2 * slot : 2 * (slot - 17) + 1;
+      const int y = iy0 + row, x = ix0 + col;
+      const bool ok = (e < IN_EL) & (ck < 2 * PSUB) & ((unsigned)y < (unsigned)H) & ((unsigned)x < (unsigned)W);
+      const unsigned voff = ok ? (unsigned)(((y * W + x) * Cs + cbase + ck * 4) * 4) : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, dst + q * 256, 16, voff, 0, 0, 0);
+    }
+  };
+
+  // helpers: output transform + epilogue of tile t from the exchange image (k_wino's reader side,
+  // both cout halves): thread = (cout quad c4, column oxl), rows k = 0..3
+  auto epilogue = [&](const Tile& t) {
+    const int ht = tid - 256;
+    const int c4 = ht & 7, oxl = ht >> 3;
+    const int ox = t.ox0 + oxl;
+    const int bb = oxl & 1, txo = oxl >> 1;
+    constexpr bool LSTM = EPI == STIF_EPI_LSTM;
+    const int ostride = LSTM ? 64 : a.cout;
+    const size_t slab = (size_t)a.Ho * a.Wo * ostride;
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.out[t.g] + (size_t)t.n * a.out_item), (short)0, (int)(slab * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(EPI == STIF_EPI_RES || LSTM ? a.res[t.g] + (size_t)t.n * a.res_item : a.in0[t.g]), (short)0,
+        (int)(slab * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ro2 = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(LSTM ? a.out2[t.g] + (size_t)t.n * a.out2_item : a.out[t.g]), (short)0, (int)(slab * 4),
+        0x00020000);
+    auto voff = [&](int nt, int k) -> unsigned {
+      const int oy = t.oy0 + k;
+      const int co = t.slice * 64 + nt * 32 + c4 * 4;
+      const bool ok = (oy < a.Ho) & (ox < a.Wo) & (co < a.cout);
+      return ok ? (unsigned)(((oy * a.Wo + ox) * ostride + (LSTM ? co >> 2 : co)) * 4) : 0x80000000u;
+    };
+    f32x4 rv[2][4];
+    float cc[2][4];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (EPI == STIF_EPI_RES)
+          rv[nt][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, voff(nt, k), 0, 0));
+        if (LSTM) cc[nt][k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, voff(nt, k), 0, 0));
+      }
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int cob = t.slice * 64 + nt * 32 + c4 * 4;
+      const f32x4 bv = cob < a.cout ? ld4(a.bias[t.g] + cob) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float* rbase =
+            X + nt * 8192 + (bb * 32 + (txo ^ (((txo >> 2) ^ bb) & 1))) * 32 + c4 * 4 + (k >> 1) * 512;
+        const f32x4 p1 = ld4(rbase + 1 * 2048), p2 = ld4(rbase + 2 * 2048);
+        const f32x4 pe = ld4(rbase + ((k & 1) ? 3 : 0) * 2048);
+        f32x4 y = (k & 1) ? (p1 - p2 - pe) : (pe + p1 + p2);
+        y += bv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (EPI == STIF_EPI_LRELU) y[e] = lrelu01(y[e]);
+          if (EPI == STIF_EPI_RELU) y[e] = fmaxf(y[e], 0.f);
+          if (EPI == STIF_EPI_OFFMASK && (cob + e) % 3 == 2) y[e] = sigmoidf_(y[e]);
+        }
+        if (EPI == STIF_EPI_RES) y += rv[nt][k];
+        if (LSTM) {
+          // ConvLSTMCell (convlstm.py:51-56): c_next = f * c_cur + i * g, h_next = o * tanh(c_next)
+          const float cn = sigmoidf_(y[1]) * cc[nt][k] + sigmoidf_(y[0]) * tanhf(y[3]);
+          const float hn = sigmoidf_(y[2]) * tanhf(cn);
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, hn), ro, voff(nt, k), 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, cn), ro2, voff(nt, k), 0, 0);
+          continue;
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, y),
+                                               ro, voff(nt, k), 0, 0);
+      }
+    }
+  };
+
+  // MFMA waves: transform row i (see k_wino)
+  const int rA = (wi == 0) ? 0 : (wi == 2 ? 2 : 1);
+  const int rB = (wi == 3) ? 3 : (wi == 2 ? 1 : 2);
+  const float sB = (wi == 1) ? 1.f : -1.f;
+  const int s0 = col_slot(0) + txl, s1 = col_slot(1) + txl, s2 = col_slot(2) + txl, s3 = col_slot(3) + txl;
+  auto xread = [&](const float* buf, int s, f32x4* rd) {
+    const float* ra = buf + ((2 * tyl + rA) * HC * PITCH + 2 * s + hf) * 4;
+    const float* rb = buf + ((2 * tyl + rB) * HC * PITCH + 2 * s + hf) * 4;
+    rd[0] = ld4(ra + s0 * PITCH * 4); rd[1] = ld4(rb + s0 * PITCH * 4);
+    rd[2] = ld4(ra + s1 * PITCH * 4); rd[3] = ld4(rb + s1 * PITCH * 4);
+    rd[4] = ld4(ra + s2 * PITCH * 4); rd[5] = ld4(rb + s2 * PITCH * 4);
+    rd[6] = ld4(ra + s3 * PITCH * 4); rd[7] = ld4(rb + s3 * PITCH * 4);
+  };
+  auto xform = [&](const f32x4* rd, f32x4* v) {
+    const f32x4 t0 = rd[0] + sB * rd[1];
+    const f32x4 t1 = rd[2] + sB * rd[3];
+    const f32x4 t2 = rd[4] + sB * rd[5];
+    const f32x4 t3 = rd[6] + sB * rd[7];
+    v[0] = t0 - t2;
+    v[1] = t1 + t2;
+    v[2] = t2 - t1;
+    v[3] = t1 - t3;
+  };
+
+  // XCD-aware persistent schedule (see k_wino)
+  const int xcd = blockIdx.x & 7, nl = gridDim.x >> 3;
+  const int per = (ntiles + 7) >> 3;
+  const int tend = min((xcd + 1) * per, ntiles);
+  int T = xcd * per + (blockIdx.x >> 3);
+  if (T >= tend) return;   // uniform over the workgroup
+
+#ifdef WINO_EXP_TRACE
+  // MFMA waves in trace blocks [0, 256), helpers in [256, 512)
+  int ntr = 0;
+  const int trb = blockIdx.x + (mf ? 0 : 256);
+#define WTRW(tag)                                                                                  \
+  do {                                                                                             \
+    if (ntr < 127 && trb < 512 && lane == 0)                                                       \
+      g_wtrace[(trb * 4 + wi) * 128 + ntr] = (__builtin_amdgcn_s_memtime() << 8) | (tag);          \
+    ++ntr;                                                                                         \
+  } while (0)
+#else
+#define WTRW(tag) do {} while (0)
+#endif
+  Tile cur = tile_of(T), prev = cur;
+  const float* wsl = wbase(cur);
+  f32x4 bw[4][2];
+  // staging runs two phases ahead of the MFMA waves (3 buffers): the DMA of a phase has a whole
+  // phase to land before the helpers' counted wait.  Host: NP >= 2.
+  const int my_dma = (IN_INST - wi + 3) / 4;   // DMA instructions this helper issues per phase
+  if (mf) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) bw[j][nt] = ld4(wsl + (j * 2 + nt) * 256);
+  } else {
+#ifdef WINO_HELPER_PRIO
+    __builtin_amdgcn_s_setprio(WINO_HELPER_PRIO);   // kernel experiment: helper issue priority
+#endif
+    stage(cur, 0, 0);
+    stage(cur, 1, 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  int gp = 0;           // phases computed so far
+  int cb = 0;           // buffer of phase gp (gp % 3)
+  bool has_prev = false;
+
+  for (;;) {
+    const int Tn = T + nl;
+    const bool has_next = Tn < tend;
+    const Tile nxt = tile_of(has_next ? Tn : T);
+    const float* wnx = wbase(nxt);
+    const bool last_half_pad = EPI == STIF_EPI_OFFMASK && cur.slice * 64 + 32 >= a.cout;
+
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j][0] = acc[j][1] = f32x16{0};
+    WTRW(1);
+
+    for (int p = 0; p < NP; ++p, ++gp) {
+      if (!mf) {
+        const int sb = cb == 0 ? 2 : cb - 1;   // (gp + 2) % 3: the buffer phase gp - 1 just released
+        const bool staged = p + 2 < NP || has_next;
+        const Tile st = p + 2 < NP ? cur : nxt;
+        const int sp = p + 2 < NP ? p + 2 : p + 2 - NP;
+        if (p == 0 && has_prev) epilogue(prev);
+        WTRW(7);
+        if (staged) stage(st, sp, sb);
+        WTRW(8);
+        // everything but this phase's own DMA has landed -- in particular the next phase's image
+        if (!staged) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else if (my_dma >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+      } else {
+#ifdef WINO_EXP_NOMFMA
+        if (p < 100000) { __syncthreads(); WTRW(2); cb = cb == 2 ? 0 : cb + 1; continue; }
+#endif
+        const float* buf = smem + cb * IN_F;
+        f32x4 rd[8];
+        xread(buf, 0, rd);
+#pragma unroll
+        for (int s = 0; s < PSUB; ++s) {
+          f32x4 v[4];
+          xform(rd, v);
+          if (s + 1 < PSUB) xread(buf, s + 1, rd);
+          const int kn = p * PSUB + s + 1;
+          const float* wn = kn < NC ? wsl + (size_t)kn * 8192 : wnx;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {
+              if (nt == 1 && last_half_pad) continue;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) acc[j][nt] = mfma32(v[j][e], bw[j][nt][e], acc[j][nt]);
+            }
+#ifndef WINO_EXP_NOB
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) bw[j][nt] = ld4(wn + (j * 2 + nt) * 256);
+#else
+            for (int nt = 0; nt < 2; ++nt) bw[j][nt] += 1.f;
+            (void)wn;
+#endif
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      }
+      WTRW(6);
+      __syncthreads();
+      WTRW(2);
+      cb = cb == 2 ? 0 : cb + 1;
+    }
+    if (mf) {
+      // P_i[nt][b] = sum_j M[i][j] A[j][b] -> exchange image (k_wino's writer side, both halves)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const f32x16 y0 = acc[0][nt] + acc[1][nt] + acc[2][nt];
+        const f32x16 y1 = acc[1][nt] - acc[2][nt] - acc[3][nt];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int fl = (hf ^ b) * 32;
+          float* wb = X + nt * 8192 + ((wi * 2 + b) * 32 + 4 * hf) * 32 + tl;
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            wb[((r & 3) + 8 * (r >> 2)) * 32 + ((r & 1) ? -fl : fl)] = b ? y1[r] : y0[r];
+        }
+      }
+    }
+    WTRW(3);
+    __syncthreads();   // P of tile T published; the helpers read it during tile T+1's first phase
+    WTRW(4);
+    prev = cur;
+    has_prev = true;
+    if (!has_next) break;
+    T = Tn;
+    cur = nxt;
+    wsl = wnx;
+  }
+  if (!mf) epilogue(prev);
+}
+
 int num_cus() {
   static int n = 0;
   if (!n) {
@@ -402,6 +713,10 @@ int num_cus() {
 #define WINO_SPLIT 0
 #endif
 
+#ifndef WINO_WS
+#define WINO_WS 0   // measured slower (k_wino_ws comment); kept as a build switch
+#endif
+
 template <int IN1, int EPI>
 int launch(const stif_conv_args& a, hipStream_t st) {
   const long long tiles =
@@ -409,6 +724,11 @@ int launch(const stif_conv_args& a, hipStream_t st) {
   if (tiles > 0x7fffffff) return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: too many tiles");
   if ((long long)a.H * a.W * std::max(a.C0, std::max(a.C1, a.cout)) * 4 >= 0x7fffffffLL)
     return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: item larger than 2 GB (buffer addressing)");
+  if (WINO_WS && (a.C0 + (a.in1_mode ? a.C1 : 0)) >= 16 * PSUB) {   // one warp-specialised workgroup per CU
+    const int grid = 8 * (int)std::min<long long>((tiles + 7) / 8, (long long)num_cus() / 8);
+    hipLaunchKernelGGL((k_wino_ws<IN1, EPI>), dim3(grid), dim3(512), 0, st, a, (int)tiles);
+    return stif_check_launch("stif_conv3x3_wino");
+  }
   const int grid = 8 * (int)std::min<long long>((tiles + 7) / 8, (long long)WG_PER_CU * num_cus() / 8);
   hipLaunchKernelGGL((k_wino<IN1, EPI, WINO_SPLIT>), dim3(grid), dim3(WINO_SPLIT ? 512 : 256), 0, st, a, (int)tiles);
   return stif_check_launch("stif_conv3x3_wino");
