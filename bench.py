@@ -148,6 +148,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_r01.json"),
                     help="PMC summary (tools/pmc_summary.py) giving the dominant kernel's HBM bytes/dispatch")
+    ap.add_argument("--mfma", default="f32", choices=["f32", "f16x3"],
+                    help="Winograd conv operand mode (model.LunaTokis mfma=)")
     ap.add_argument("--kernel-report", action="store_true", help="time every conv launch kind (stderr)")
     args = ap.parse_args()
 
@@ -167,7 +169,7 @@ def main():
     nframes, H, W, scale, times = CONFIGS[args.config]
     pairs = nframes - 1
     sd = stif.weights.make_state_dict(seed=0)
-    model = stif.LunaTokis(64, 6, 8, 5, 40, device=device)
+    model = stif.LunaTokis(64, 6, 8, 5, 40, device=device, mfma=args.mfma)
     model.load_state_dict(sd, strict=True)
     frames_cpu = synth_frames(rank * pairs, nframes, H, W, "cpu")
     frames = frames_cpu.to(device)

@@ -69,7 +69,13 @@ typedef struct {
   int cout;                /* logical output channels (64, 216, 256) */
   int ks, stride;          /* 1 or 3; 1 or 2 (padding = ks/2) */
   int epi;                 /* STIF_EPI_* */
+  int flags;               /* STIF_CONV_F16X3: weights packed with STIF_PACK_F16X3 (stif_conv3x3_wino only) */
 } stif_conv_args;
+
+/* stif_conv_args.flags: fp32 products on the fp16 MFMA pipe by 3-term operand splitting (x = h + l,
+ * a*b = ah*bh + ah*bl + al*bh, fp32 accumulation; ~22 significant bits per operand, see
+ * stif_common.h).  Valid range: |activations| < 1024, |Winograd weights| < 64. */
+#define STIF_CONV_F16X3 1
 
 int stif_conv2d_nhwc(const stif_conv_args* args, void* stream);
 
@@ -194,6 +200,9 @@ int stif_frames_to_u8(const float* nchw, unsigned char* hwc, int n, int H, int W
 /* ---- host-side weight packing (pure CPU, callable without a GPU) ---- */
 enum { STIF_PACK_PLAIN = 0, STIF_PACK_OFFMASK = 1, STIF_PACK_LSTM = 2, STIF_PACK_WINO = 3, STIF_PACK_WINO_OFFMASK = 4,
        STIF_PACK_WINO_LSTM = 5 };
+/* OR'ed into a STIF_PACK_WINO* mode: the f16x3 split packing for stif_conv3x3_wino with
+ * flags = STIF_CONV_F16X3 (same size in bytes) */
+#define STIF_PACK_F16X3 16
 
 /* Size in floats of a packed conv weight / bias for a packing mode. */
 size_t stif_conv_weight_floats(int cout, int cin, int ks, int mode);
@@ -210,7 +219,10 @@ size_t stif_conv_bias_floats(int cout, int mode);
  * chunk*8 + 4(l >> 5) + e; cout padded to a multiple of 64.  STIF_PACK_WINO_OFFMASK: the same
  * with the OFFMASK row permutation (216 -> 256 rows).  STIF_PACK_WINO_LSTM: the same for the
  * ConvLSTMCell conv (128 -> 256) with packed cout 4h + gate = reference row gate*64 + h (gates
- * i, f, o, g; convlstm.py:49), so one 4-cout quad holds the four gates of hidden channel h. */
+ * i, f, o, g; convlstm.py:49), so one 4-cout quad holds the four gates of hidden channel h.
+ * STIF_PACK_WINO* | STIF_PACK_F16X3: U * 2^10 split into fp16 h = rne(U 2^10), l = rne(U 2^10 - h)
+ * as [cout/64][cin/16][i 4][j 4][nt 2][plane h|l][lane 64][8 halves], lane l's element e holding
+ * input channel 16 q + 8 (e >> 2) + 4 (l >> 5) + (e & 3) (the chunk pair of one f16 MFMA). */
 int stif_pack_conv_weight(const float* w_oihw, const float* b, int cout, int cin, int ks, int mode,
                           float* w_dst, float* b_dst);
 

@@ -14,6 +14,8 @@ LIB_PATH = os.environ.get("STIF_HIP_LIB") or os.path.join(os.path.dirname(os.pat
 MAXG = 8
 EPI_NONE, EPI_LRELU, EPI_RELU, EPI_RES, EPI_OFFMASK, EPI_LSTM = range(6)
 PACK_PLAIN, PACK_OFFMASK, PACK_LSTM, PACK_WINO, PACK_WINO_OFFMASK, PACK_WINO_LSTM = range(6)
+PACK_F16X3 = 16          # OR'ed into a PACK_WINO* mode (stif.h STIF_PACK_F16X3)
+CONV_F16X3 = 1           # stif_conv_args.flags
 
 _P = C.c_void_p
 _PA = _P * MAXG
@@ -28,7 +30,7 @@ class ConvArgs(C.Structure):
         ("H", C.c_int), ("W", C.c_int), ("C0", C.c_int),
         ("C1", C.c_int), ("in1_mode", C.c_int), ("in1_scale", C.c_float),
         ("Ho", C.c_int), ("Wo", C.c_int), ("cout", C.c_int), ("ks", C.c_int), ("stride", C.c_int),
-        ("epi", C.c_int),
+        ("epi", C.c_int), ("flags", C.c_int),
     ]
 
 

@@ -325,6 +325,7 @@ extern "C" int stif_conv2d_nhwc(const stif_conv_args* pa, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (a.ngroups < 1 || a.ngroups > STIF_MAX_GROUPS || a.nitems < 1)
     return stif_fail(STIF_E_INVALID, "stif_conv2d_nhwc: bad ngroups/nitems");
+  if (a.flags & STIF_CONV_F16X3) return stif_fail(STIF_E_INVALID, "stif_conv2d_nhwc: STIF_CONV_F16X3 is a Winograd-only mode");
   if (a.C0 % 8 || a.C0 <= 0 || (a.in1_mode && (a.C1 % 8 || a.C1 <= 0)))
     return stif_fail(STIF_E_INVALID, "stif_conv2d_nhwc: channel counts must be multiples of 8");
   const int pad = a.ks / 2;

@@ -96,12 +96,14 @@ std::vector<float> omega(const float* src, size_t n) {
 }  // namespace
 
 extern "C" size_t stif_conv_weight_floats(int cout, int cin, int ks, int mode) {
+  mode &= ~STIF_PACK_F16X3;   // same bytes: two fp16 planes per fp32 value
   if (mode == STIF_PACK_WINO || mode == STIF_PACK_WINO_OFFMASK || mode == STIF_PACK_WINO_LSTM)
     return (size_t)round64(cout) * cin * 16;
   return (size_t)cout_padded(cout, mode) * cin * ks * ks;
 }
 
 extern "C" size_t stif_conv_bias_floats(int cout, int mode) {
+  mode &= ~STIF_PACK_F16X3;
   return (mode == STIF_PACK_WINO || mode == STIF_PACK_WINO_OFFMASK || mode == STIF_PACK_WINO_LSTM)
              ? (size_t)round64(cout)
              : (size_t)cout_padded(cout, mode);
@@ -135,12 +137,51 @@ int pack_wino(const float* w, const float* b, int cout, int cin, int perm, float
     }
   return STIF_OK;
 }
+
+// STIF_PACK_F16X3: [slice][pair q][i][j][nt][plane][lane][8 halves]; element e of lane l holds input
+// channel 16 q + 8 (e >> 2) + 4 (l >> 5) + (e & 3) -- lane half h supplies channels 4h..4h+3 of both
+// 8-channel chunks of the pair, exactly the A operand k_wino<F16> builds -- as U * 2^10 split into
+// h = rne16(U 2^10), l = rne16(U 2^10 - h) (double arithmetic, so l is the correctly rounded residual)
+int pack_wino_f16x3(const float* w, const float* b, int cout, int cin, int perm, float* w_dst, float* b_dst) {
+  if (cin % 16) return stif_fail(STIF_E_INVALID, "f16x3 winograd pack needs cin % 16 == 0");
+  const int cp = round64(cout), NS = cp / 64, NQ = cin / 16;
+  _Float16* dst = reinterpret_cast<_Float16*>(w_dst);
+  for (int s = 0; s < NS; ++s)
+    for (int nt = 0; nt < 2; ++nt)
+      for (int l = 0; l < 64; ++l) {
+        const int co = s * 64 + nt * 32 + (l & 31);
+        const int sr = src_row(co, cout, perm);
+        for (int q = 0; q < NQ; ++q)
+          for (int e = 0; e < 8; ++e) {
+            const int ci = 16 * q + 8 * (e >> 2) + 4 * (l >> 5) + (e & 3);
+            double u[4][4] = {{0}};
+            if (sr >= 0) wino_u(w + ((size_t)sr * cin + ci) * 9, u);
+            for (int i = 0; i < 4; ++i)
+              for (int j = 0; j < 4; ++j) {
+                const double x = u[i][j] * 1024.0;
+                const _Float16 h = (_Float16)x;
+                const _Float16 lo = (_Float16)(x - (double)h);
+                const size_t o = ((((((size_t)s * NQ + q) * 4 + i) * 4 + j) * 2 + nt) * 2) * 512 + l * 8 + e;
+                dst[o] = h;
+                dst[o + 512] = lo;
+              }
+          }
+      }
+  if (b_dst)
+    for (int j = 0; j < cp; ++j) {
+      const int sr = src_row(j, cout, perm);
+      b_dst[j] = (sr >= 0 && b) ? b[sr] : 0.f;
+    }
+  return STIF_OK;
+}
 }  // namespace
 
 extern "C" int stif_pack_conv_weight(const float* w, const float* b, int cout, int cin, int ks, int mode,
                                      float* w_dst, float* b_dst) {
   if (!w || !w_dst || cout <= 0 || cin <= 0 || cin % 8 || (ks != 1 && ks != 3))
     return stif_fail(STIF_E_INVALID, "stif_pack_conv_weight: bad arguments");
+  const bool f16x3 = (mode & STIF_PACK_F16X3) != 0;
+  mode &= ~STIF_PACK_F16X3;
   if ((mode == STIF_PACK_OFFMASK || mode == STIF_PACK_WINO_OFFMASK) && cout != 216)
     return stif_fail(STIF_E_INVALID, "offmask pack needs cout=216");
   if ((mode == STIF_PACK_LSTM || mode == STIF_PACK_WINO_LSTM) && cout != 256)
@@ -148,8 +189,9 @@ extern "C" int stif_pack_conv_weight(const float* w, const float* b, int cout, i
   if (mode == STIF_PACK_WINO || mode == STIF_PACK_WINO_OFFMASK || mode == STIF_PACK_WINO_LSTM) {
     if (ks != 3) return stif_fail(STIF_E_INVALID, "winograd pack needs a 3x3 kernel");
     const int perm = mode == STIF_PACK_WINO ? STIF_PACK_PLAIN : (mode == STIF_PACK_WINO_OFFMASK ? STIF_PACK_OFFMASK : mode);
-    return pack_wino(w, b, cout, cin, perm, w_dst, b_dst);
+    return f16x3 ? pack_wino_f16x3(w, b, cout, cin, perm, w_dst, b_dst) : pack_wino(w, b, cout, cin, perm, w_dst, b_dst);
   }
+  if (f16x3) return stif_fail(STIF_E_INVALID, "STIF_PACK_F16X3 applies to the Winograd packings only");
   // layout [slice][chunk][tap][nt][lane][4]: the B fragments of one (slice, chunk) are one
   // contiguous block, copied to LDS by LDS-DMA; lane l of N-tile nt holds cout
   // slice*NJ + nt*32 + (l & 31), input channels chunk*8 + 4*(l >> 5) + e.

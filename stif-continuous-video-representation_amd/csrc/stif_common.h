@@ -15,6 +15,35 @@ STIF_DEV f32x16 mfma32(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
+// v_mfma_f32_32x32x16_f16: D[32x32] += A[32x16] * B[16x32]; lane l supplies 8 K values of row
+// (A) / column (B) l & 31, selected by (l >> 5, element) -- the same selection for A and B, so any
+// consistent (lane half, element) -> input-channel assignment is a valid K order.  D as mfma32.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+STIF_DEV f32x16 mfma16h(f16x8 a, f16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+STIF_DEV f16x8 ldh8(const float* p) { return __builtin_bit_cast(f16x8, *reinterpret_cast<const f32x4*>(p)); }
+
+// fp32 products on fp16 MFMA by operand splitting (Markidis et al. 2018; Ootomo & Yokota 2022):
+// x * 2^s = h + l with h = fp16(x * 2^s) (RNE) and l = fp16(x * 2^s - h) (the residual is exact in
+// fp32, then rounded to 11 bits), so x is carried to ~22 significant bits; a * b is accumulated as
+// ah*bh + ah*bl + al*bh in one fp32 accumulator (al*bl < 2^-22 |ab| dropped).  Scales: activations
+// (A) 2^4, weights (B, host packing) 2^10 -- the residual l stays a normal fp16 for |x| >= 2^-3
+// (A) / 2^-9 (B); below that its absolute error is < 2^-29 (A), 2^-35 (B).  Range: |A| < 4096
+// (Winograd-transformed inputs: |activation| < 1024), |B| < 64.  Result unscaled by 2^-14.
+#define F16X3_SCALE_A 16.0f
+#define F16X3_UNSCALE 0x1p-14f
+STIF_DEV void split_f16x3(f32x4 x0, f32x4 x1, f16x8& h, f16x8& l) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float a = x0[e] * F16X3_SCALE_A, b = x1[e] * F16X3_SCALE_A;
+    h[e] = (_Float16)a;
+    h[e + 4] = (_Float16)b;
+    l[e] = (_Float16)(a - (float)h[e]);
+    l[e + 4] = (_Float16)(b - (float)h[e + 4]);
+  }
+}
+
 STIF_DEV int mfma_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
 STIF_DEV f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }

@@ -48,6 +48,9 @@ constexpr int IN_INST = (IN_EL + 63) / 64;     // LDS-DMA instructions per phase
 constexpr int EX_F = 2 * 2 * 2 * 1024;         // epilogue exchange: [wave 1|2][nt][b][32 tiles][32 co]
 constexpr int BUF_F = (IN_INST * 256 > EX_F) ? IN_INST * 256 : EX_F;   // floats per buffer (32 KB)
 constexpr int WG_PER_CU = 2;
+#ifndef WINO_F16_XREAD_J
+#define WINO_F16_XREAD_J 3   // F16: block j after whose split the next pair's first chunk is read
+#endif
 
 // slot of halo column c in its (row, chunk, half) run: even columns first, then odd
 STIF_DEV int col_slot(int c) { return (c & 1) ? 17 + (c >> 1) : (c >> 1); }
@@ -76,7 +79,7 @@ struct Tile {
 // SPLIT = 0: 4 waves, wave i = transform row i for both 32-cout halves (2 waves/SIMD, ~250 VGPRs);
 // SPLIT = 1: 8 waves, wave (i, nh) = transform row i for cout half nh (4 waves/SIMD, <= 128 VGPRs:
 // twice the waves to hide latencies, the input transform computed by both halves).
-template <int IN1, int EPI, int SPLIT>
+template <int IN1, int EPI, int SPLIT, int F16>
 __global__ __launch_bounds__(SPLIT ? 512 : 256) __attribute__((amdgpu_waves_per_eu(SPLIT ? 4 : 2))) void k_wino(
     stif_conv_args a, int ntiles) {
   constexpr int NWV = SPLIT ? 8 : 4;      // waves per workgroup
@@ -100,6 +103,7 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256) __attribute__((amdgpu_waves_per_
   const int NC0 = C0 >> 3;
   const int NC = NC0 + (IN1 ? (C1 >> 3) : 0);
   const int NP = NC / PSUB;   // host guarantees NC % PSUB == 0
+  const int NQ = NC >> 1;     // F16: 16-channel chunk pairs
 
   // tile order: cout slice fastest (the slices of one spatial tile share its input), then x, y, item
   auto tile_of = [&](int T) {
@@ -117,8 +121,11 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256) __attribute__((amdgpu_waves_per_
     return t;
   };
   // packed U: [slice][chunk][i][j][nt][lane][4]; B fragment (j, local half u) at wsl + (j*2 + u)*256
+  // F16 (STIF_PACK_F16X3): [slice][pair][i][j][u][plane h|l][lane][8 halves]; fragment (j, u, plane)
+  // of pair q at wsl + q * 16384 + ((j * 2 + u) * 2 + plane) * 256 (float offsets)
   auto wbase = [&](const Tile& t) {
-    return a.w[t.g] + (size_t)t.slice * NC * 8192 + wi * 2048 + nh * 256 + lane * 4;
+    return F16 ? a.w[t.g] + (size_t)t.slice * NC * 8192 + wi * 4096 + lane * 4
+               : a.w[t.g] + (size_t)t.slice * NC * 8192 + wi * 2048 + nh * 256 + lane * 4;
   };
 
   auto stage = [&](const Tile& t, int p, int buf) {
@@ -196,11 +203,24 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256) __attribute__((amdgpu_waves_per_
   Tile cur = tile_of(T);
   const float* wsl = wbase(cur);
   f32x4 bw[4][NTW];
+  // F16: B operand ring over the (pair, j) blocks, two blocks deep: slot j & 1 holds block j's
+  // (u, plane) fragments and is refilled with block j + 2 right after block j's MFMAs
+  f16x8 bh[2][2], bl[2][2];
+  if constexpr (F16) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int u = 0; u < NTW; ++u) bw[j][u] = ld4(wsl + (j * 2 + u) * 256);
-  int gp = 0;                      // phases staged so far: buffer of phase gp = gp & 1
+      for (int u = 0; u < 2; ++u) {
+        bh[j][u] = ldh8(wsl + ((j * 2 + u) * 2) * 256);
+        bl[j][u] = ldh8(wsl + ((j * 2 + u) * 2 + 1) * 256);
+      }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int u = 0; u < NTW; ++u) bw[j][u] = ld4(wsl + (j * 2 + u) * 256);
+  }
+  int gp = 0;                     // phases staged so far: buffer of phase gp = gp & 1
   stage(cur, 0, 0);
   lds_dma_barrier();
 
@@ -219,6 +239,55 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256) __attribute__((amdgpu_waves_per_
     const bool last_half_pad = EPI == STIF_EPI_OFFMASK && cur.slice * 64 + 32 >= a.cout;
     WTR(1);
 
+    if constexpr (F16) {
+      for (int p = 0; p < NP; ++p, ++gp) {
+        if (p + 1 < NP) stage(cur, p + 1, (gp + 1) & 1);
+        else if (has_next) stage(nxt, 0, (gp + 1) & 1);
+        const float* buf = smem + (gp & 1) * BUF_F;
+        f32x4 rd[8];
+        xread(buf, 0, rd);
+#pragma unroll
+        for (int sp = 0; sp < PSUB / 2; ++sp) {
+          // chunk pair (2 sp, 2 sp + 1): lane half h holds channels 4h..4h+3 of both, i.e. the 8
+          // K values of a 32x32x16 f16 MFMA; transform both, split all four j, then fetch the next
+          // pair's first chunk so its LDS reads hide under this pair's MFMAs
+          f32x4 va[4], vb[4];
+          xform(rd, va);
+          xread(buf, 2 * sp + 1, rd);
+          xform(rd, vb);
+          const int q = p * (PSUB / 2) + sp;
+          const float* wq = wsl + (size_t)q * 16384;
+          const float* wq1 = q + 1 < NQ ? wq + 16384 : wnx;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            f16x8 ah, al;
+            split_f16x3(va[j], vb[j], ah, al);
+#if WINO_F16_XREAD_J >= 0
+            if (j == WINO_F16_XREAD_J && 2 * sp + 2 < PSUB) xread(buf, 2 * sp + 2, rd);
+#endif
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              if (last_half_pad && u == 1) continue;
+              acc[j][u] = mfma16h(ah, bh[j & 1][u], acc[j][u]);
+              acc[j][u] = mfma16h(ah, bl[j & 1][u], acc[j][u]);
+              acc[j][u] = mfma16h(al, bh[j & 1][u], acc[j][u]);
+            }
+            // refill the slot with block j + 2: (pair q, j + 2) or (pair q + 1, j - 2)
+            const float* wn = j < 2 ? wq + (j + 2) * 1024 : wq1 + (j - 2) * 1024;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              bh[j & 1][u] = ldh8(wn + (u * 2) * 256);
+              bl[j & 1][u] = ldh8(wn + (u * 2 + 1) * 256);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+        // every load older than the last two blocks' B refills (8) -- the phase's LDS-DMA among
+        // them -- has landed
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        __syncthreads();
+      }
+    } else
     for (int p = 0; p < NP; ++p, ++gp) {
       if (p + 1 < NP) stage(cur, p + 1, (gp + 1) & 1);
       else if (has_next) stage(nxt, 0, (gp + 1) & 1);
@@ -361,6 +430,7 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256) __attribute__((amdgpu_waves_per_
         const f32x4 p1 = ld4(rbase + 1 * 2048), p2 = ld4(rbase + 2 * 2048);
         const f32x4 pe = ld4(rbase + ((k & 1) ? 3 : 0) * 2048);
         f32x4 y = (k & 1) ? (p1 - p2 - pe) : (pe + p1 + p2);
+        if (F16) y *= F16X3_UNSCALE;   // exact power of two
         y += bv;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -724,13 +794,16 @@ int launch(const stif_conv_args& a, hipStream_t st) {
   if (tiles > 0x7fffffff) return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: too many tiles");
   if ((long long)a.H * a.W * std::max(a.C0, std::max(a.C1, a.cout)) * 4 >= 0x7fffffffLL)
     return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: item larger than 2 GB (buffer addressing)");
-  if (WINO_WS && (a.C0 + (a.in1_mode ? a.C1 : 0)) >= 16 * PSUB) {   // one warp-specialised workgroup per CU
+  if (WINO_WS && !(a.flags & STIF_CONV_F16X3) && (a.C0 + (a.in1_mode ? a.C1 : 0)) >= 16 * PSUB) {   // one warp-specialised workgroup per CU
     const int grid = 8 * (int)std::min<long long>((tiles + 7) / 8, (long long)num_cus() / 8);
     hipLaunchKernelGGL((k_wino_ws<IN1, EPI>), dim3(grid), dim3(512), 0, st, a, (int)tiles);
     return stif_check_launch("stif_conv3x3_wino");
   }
   const int grid = 8 * (int)std::min<long long>((tiles + 7) / 8, (long long)WG_PER_CU * num_cus() / 8);
-  hipLaunchKernelGGL((k_wino<IN1, EPI, WINO_SPLIT>), dim3(grid), dim3(WINO_SPLIT ? 512 : 256), 0, st, a, (int)tiles);
+  if (a.flags & STIF_CONV_F16X3)
+    hipLaunchKernelGGL((k_wino<IN1, EPI, 0, 1>), dim3(grid), dim3(256), 0, st, a, (int)tiles);
+  else
+    hipLaunchKernelGGL((k_wino<IN1, EPI, WINO_SPLIT, 0>), dim3(grid), dim3(WINO_SPLIT ? 512 : 256), 0, st, a, (int)tiles);
   return stif_check_launch("stif_conv3x3_wino");
 }
 

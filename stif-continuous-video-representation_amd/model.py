@@ -36,7 +36,8 @@ def _np(v):
 class LunaTokis:
     """STIF LunaTokis (Sakuya_arch_test.py:268) on MI355X."""
 
-    def __init__(self, nf=64, nframes=3, groups=8, front_RBs=5, back_RBs=10, device="cuda", winograd=True):
+    def __init__(self, nf=64, nframes=3, groups=8, front_RBs=5, back_RBs=10, device="cuda", winograd=True,
+                 mfma="f32"):
         if nf != 64 or groups != 8:
             raise ValueError("the gfx950 kernels implement nf=64, groups=8 (the shipped STIF configuration)")
         self.nf, self.groups = nf, groups
@@ -53,6 +54,11 @@ class LunaTokis:
         self.training = False
         # 3x3 convs by Winograd F(2x2,3x3) where the shape allows (fp32 throughout); False = direct
         self.winograd = bool(winograd)
+        # operand arithmetic of the Winograd convs: "f32" (fp32 MFMA) or "f16x3" (fp32 products
+        # from three fp16 MFMAs on split operands, ~22-bit operands, fp32 accumulation; stif.h)
+        if mfma not in ("f32", "f16x3"):
+            raise ValueError("mfma must be 'f32' or 'f16x3'")
+        self.mfma = mfma
 
     # ------------------------------------------------------------------ nn.Module-like API
     def eval(self):
@@ -123,7 +129,8 @@ class LunaTokis:
         # cat(., up(.)) ones on a materialised x2-upsampled second input), as do the offset/mask
         # (64 -> 216) and ConvLSTMCell (128 -> 256, gate epilogue) convs; the strided and 1x1
         # convs keep the direct kernel.
-        wino = L.PACK_WINO if self.winograd else L.PACK_PLAIN
+        f16 = L.PACK_F16X3 if self.mfma == "f16x3" else 0
+        wino = (L.PACK_WINO | f16) if self.winograd else L.PACK_PLAIN
 
         lay["conv_first.w"] = torch.from_numpy(h["conv_first.weight"]).to(dev)
         lay["conv_first.b"] = torch.from_numpy(h["conv_first.bias"]).to(dev)
@@ -141,13 +148,13 @@ class LunaTokis:
                     n = f"{prefix}{ln}_{d}"
                     if cin is None:
                         conv(n)
-                        conv(n + ".conv_offset_mask", L.PACK_WINO_OFFMASK if self.winograd else L.PACK_OFFMASK)
+                        conv(n + ".conv_offset_mask", (L.PACK_WINO_OFFMASK | f16) if self.winograd else L.PACK_OFFMASK)
                     else:
                         conv(n, wino)
 
         pcd("pcd_align.")
         conv("fusion")
-        conv("ConvBLSTM.forward_net.cell_list.0.conv", L.PACK_WINO_LSTM if self.winograd else L.PACK_LSTM)
+        conv("ConvBLSTM.forward_net.cell_list.0.conv", (L.PACK_WINO_LSTM | f16) if self.winograd else L.PACK_LSTM)
         for p in ("ConvBLSTM.forward_net.pcd_h.", "ConvBLSTM.forward_net.pcd_c."):
             for n in ("fea_L2_conv1", "fea_L3_conv1", "fusion"):
                 conv(p + n)

@@ -106,9 +106,11 @@ def conv2d(groups, *, epi=L.EPI_NONE, in1_mode=0, in1_scale=1.0, stride=None):
     a.in1_mode, a.in1_scale = in1_mode, in1_scale
     a.Ho, a.Wo, a.cout, a.ks, a.stride, a.epi = Ho, Wo, lay.cout, ks, stride, epi
     wmodes = (L.PACK_WINO, L.PACK_WINO_OFFMASK, L.PACK_WINO_LSTM)
-    wino = lay.mode in wmodes
-    if any((g["layer"].mode in wmodes) != wino for g in groups):
-        raise ValueError("conv2d: groups mix Winograd and direct packings")
+    wino = (lay.mode & ~L.PACK_F16X3) in wmodes
+    if any(((g["layer"].mode & ~L.PACK_F16X3) in wmodes) != wino or (g["layer"].mode ^ lay.mode) & L.PACK_F16X3
+           for g in groups):
+        raise ValueError("conv2d: groups mix Winograd / direct or f32 / f16x3 packings")
+    a.flags = L.CONV_F16X3 if lay.mode & L.PACK_F16X3 else 0
     tr = TRACE
     if tr is not None:
         # algorithmic (direct-convolution) FLOPs, whichever algorithm runs

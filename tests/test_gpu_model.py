@@ -188,3 +188,46 @@ def test_decoding_localensemble(latent16, golden, which):
     assert tuple(o.shape) == ref.shape
     ok, err, mx = close(o, ref)
     assert ok, (err, mx)
+
+
+@pytest.fixture(scope="module")
+def model_f16x3(stif, sd):
+    m = stif.LunaTokis(64, 6, 8, 5, 40, mfma="f16x3")
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    return m.eval()
+
+
+def test_f16x3_outputs_match_reference(model_f16x3, golden):
+    """mfma='f16x3' (Winograd convs on split-fp16 MFMA operands) against the reference's outputs,
+    at the same bar as the fp32-MFMA path."""
+    g = golden["model_16x20"]
+    with torch.no_grad():
+        outs = model_f16x3(torch.from_numpy(g["x"]).cuda(), [torch.tensor([[float(t)]]) for t in g["times"]])
+    ok, err, mx = close(model_f16x3.feat.detach().cpu().numpy()[0], g["feat"])
+    assert ok, (err, mx)
+    for i, o in enumerate(outs):
+        ok, err, mx = close(o[0], g["out"][i])
+        assert ok, (i, err, mx)
+
+
+def test_f16x3_window_and_psnr(model_f16x3, golden, sd):
+    """7-frame window against the reference, and the PSNR criterion (< 1e-3 dB)."""
+    g = golden["window_7x16x16"]
+    with torch.no_grad():
+        model_f16x3.gen_feat_window(torch.from_numpy(g["frames"]).cuda())
+        out = model_f16x3.decoding([torch.tensor([[0.5]])])[0]
+    ok, err, mx = close(out, g["out"])
+    assert ok, (err, mx)
+    gt = np.clip(g["out"] + 0.05 * np.random.default_rng(3).standard_normal(g["out"].shape), 0, 1)
+    d = abs(psnr(out.cpu().numpy(), gt) - psnr(g["out"], gt))
+    assert d < 1e-3, d
+
+
+def test_f16x3_larger_size_vs_oracle(model_f16x3, sd):
+    rng = np.random.default_rng(7)
+    x = rng.random((1, 2, 3, 32, 48)).astype(np.float32)
+    ref = O.forward(x, [0.3], sd)[0]
+    with torch.no_grad():
+        out = model_f16x3(torch.from_numpy(x).cuda(), [0.3])[0]
+    ok, err, mx = close(out, ref)
+    assert ok, (err, mx)

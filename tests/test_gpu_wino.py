@@ -7,7 +7,14 @@ from oracle import stif_oracle as O
 
 pytestmark = pytest.mark.gpu
 
-RTOL = 1e-5   # relative to max |ref|, same bar as the direct conv kernels
+RTOL = 1e-5   # relative to max |ref|, same bar as the direct conv kernels (both operand modes)
+
+
+@pytest.fixture(params=[0, 16], ids=["f32", "f16x3"])
+def pf(request):
+    """Winograd operand mode: fp32 MFMA, or fp32 products from 3 fp16 MFMAs on split operands
+    (STIF_PACK_F16X3 packing; ops.conv2d sets STIF_CONV_F16X3 from it)."""
+    return request.param
 
 
 def relmax(a, b):
@@ -28,7 +35,7 @@ def rnd(*shape, seed=0, scale=1.0):
 
 @pytest.mark.parametrize("epi", ["none", "lrelu", "relu", "res"])
 @pytest.mark.parametrize("hw", [(13, 37), (8, 32), (33, 70), (4, 4)])
-def test_wino_conv3x3(stif, epi, hw):
+def test_wino_conv3x3(stif, epi, hw, pf):
     L, ops = stif._lib, stif.ops
     H, W = hw
     x = rnd(3, 64, H, W, seed=1)
@@ -41,12 +48,12 @@ def test_wino_conv3x3(stif, epi, hw):
     if epi == "res":
         ref = ref + r
     out = torch.empty(3, H, W, 64, device="cuda")
-    layer = ops.pack_conv(w, b, L.PACK_WINO)
+    layer = ops.pack_conv(w, b, L.PACK_WINO | pf)
     ops.conv2d([dict(layer=layer, in0=nhwc(x), out=out, res=nhwc(r) if epi == "res" else None)], epi=e)
     assert relmax(to_nchw(out), ref) < RTOL
 
 
-def test_wino_residual_in_place(stif):
+def test_wino_residual_in_place(stif, pf):
     """out == res (the ResidualBlock_noBN in-place update the model uses)."""
     L, ops = stif._lib, stif.ops
     x = rnd(2, 64, 16, 64, seed=5)
@@ -54,12 +61,12 @@ def test_wino_residual_in_place(stif):
     w = rnd(64, 64, 3, 3, seed=7, scale=0.05)
     b = rnd(64, seed=8)
     xd = nhwc(x)
-    ops.conv2d([dict(layer=ops.pack_conv(w, b, L.PACK_WINO), in0=nhwc(t), out=xd, res=xd)], epi=L.EPI_RES)
+    ops.conv2d([dict(layer=ops.pack_conv(w, b, L.PACK_WINO | pf), in0=nhwc(t), out=xd, res=xd)], epi=L.EPI_RES)
     assert relmax(to_nchw(xd), x + O.conv2d(t, w, b)) < RTOL
 
 
 @pytest.mark.parametrize("cin1", [64, 32])
-def test_wino_two_inputs_groups(stif, cin1):
+def test_wino_two_inputs_groups(stif, cin1, pf):
     """cat(in0, in1) input (PCD offset convs) in two weight groups over strided item views."""
     L, ops = stif._lib, stif.ops
     H, W = 12, 40
@@ -71,25 +78,25 @@ def test_wino_two_inputs_groups(stif, cin1):
     t = nhwc(fr)
     in1 = t[1::2, :, :, :cin1].contiguous() if cin1 != 64 else t[1::2]
     out = torch.empty(2, 2, H, W, 64, device="cuda")
-    ops.conv2d([dict(layer=ops.pack_conv(wa, ba, L.PACK_WINO), in0=t[0::2], in1=in1, out=out[0]),
-                dict(layer=ops.pack_conv(wb, bb, L.PACK_WINO), in0=t[0::2], in1=in1, out=out[1])],
+    ops.conv2d([dict(layer=ops.pack_conv(wa, ba, L.PACK_WINO | pf), in0=t[0::2], in1=in1, out=out[0]),
+                dict(layer=ops.pack_conv(wb, bb, L.PACK_WINO | pf), in0=t[0::2], in1=in1, out=out[1])],
                epi=L.EPI_LRELU, in1_mode=1)
     cat = np.concatenate([f1n, f2n], 1)
     assert relmax(to_nchw(out[0]), O.lrelu(O.conv2d(cat, wa, ba))) < RTOL
     assert relmax(to_nchw(out[1]), O.lrelu(O.conv2d(cat, wb, bb))) < RTOL
 
 
-def test_wino_multi_slice(stif):
+def test_wino_multi_slice(stif, pf):
     L, ops = stif._lib, stif.ops
     x = rnd(1, 128, 10, 36, seed=14)
     w = rnd(128, 128, 3, 3, seed=15, scale=0.03)
     b = rnd(128, seed=16)
     out = torch.empty(1, 10, 36, 128, device="cuda")
-    ops.conv2d([dict(layer=ops.pack_conv(w, b, L.PACK_WINO), in0=nhwc(x), out=out)])
+    ops.conv2d([dict(layer=ops.pack_conv(w, b, L.PACK_WINO | pf), in0=nhwc(x), out=out)])
     assert relmax(to_nchw(out), O.conv2d(x, w, b)) < RTOL
 
 
-def test_wino_matches_direct_kernel(stif):
+def test_wino_matches_direct_kernel(stif, pf):
     """Winograd vs the direct implicit-GEMM kernel on the trunk shape: both fp32, both ~1e-7."""
     L, ops = stif._lib, stif.ops
     x = rnd(2, 64, 32, 64, seed=17)
@@ -97,17 +104,17 @@ def test_wino_matches_direct_kernel(stif):
     b = rnd(64, seed=19)
     o1 = torch.empty(2, 32, 64, 64, device="cuda")
     o2 = torch.empty_like(o1)
-    ops.conv2d([dict(layer=ops.pack_conv(w, b, L.PACK_WINO), in0=nhwc(x), out=o1)], epi=L.EPI_RELU)
+    ops.conv2d([dict(layer=ops.pack_conv(w, b, L.PACK_WINO | pf), in0=nhwc(x), out=o1)], epi=L.EPI_RELU)
     ops.conv2d([dict(layer=ops.pack_conv(w, b), in0=nhwc(x), out=o2)], epi=L.EPI_RELU)
     ref = O.relu(O.conv2d(x, w, b))
     e1, e2 = relmax(to_nchw(o1), ref), relmax(to_nchw(o2), ref)
     assert e1 < RTOL and e2 < RTOL, (e1, e2)
 
 
-def test_wino_rejects_bad_shapes(stif):
+def test_wino_rejects_bad_shapes(stif, pf):
     L, ops = stif._lib, stif.ops
     w = rnd(64, 64, 3, 3)
-    lay = ops.pack_conv(w, rnd(64), L.PACK_WINO)
+    lay = ops.pack_conv(w, rnd(64), L.PACK_WINO | pf)
     x = torch.zeros(1, 8, 8, 64, device="cuda")
     with pytest.raises(Exception):
         ops.conv2d([dict(layer=lay, in0=x, out=torch.empty(1, 4, 4, 64, device="cuda"))], stride=2)
@@ -124,7 +131,7 @@ def test_upsample2x(stif, scale):
     assert relmax(to_nchw(out), ref) < 1e-6
 
 
-def test_wino_cat_upsampled_matches_fused_direct(stif):
+def test_wino_cat_upsampled_matches_fused_direct(stif, pf):
     """cat(x, 2*up2(c)) conv: materialised upsample + Winograd == the direct kernel's fused path."""
     L, ops = stif._lib, stif.ops
     H, W = 12, 36
@@ -136,7 +143,7 @@ def test_wino_cat_upsampled_matches_fused_direct(stif):
     ops.upsample2x(nhwc(c), up, 2.0)
     o1 = torch.empty(2, H, W, 64, device="cuda")
     o2 = torch.empty_like(o1)
-    ops.conv2d([dict(layer=ops.pack_conv(w, b, L.PACK_WINO), in0=nhwc(x0), in1=up, out=o1)], epi=L.EPI_LRELU,
+    ops.conv2d([dict(layer=ops.pack_conv(w, b, L.PACK_WINO | pf), in0=nhwc(x0), in1=up, out=o1)], epi=L.EPI_LRELU,
                in1_mode=1)
     ops.conv2d([dict(layer=ops.pack_conv(w, b), in0=nhwc(x0), in1=nhwc(c), out=o2)], epi=L.EPI_LRELU,
                in1_mode=2, in1_scale=2.0)
@@ -144,7 +151,7 @@ def test_wino_cat_upsampled_matches_fused_direct(stif):
     assert relmax(to_nchw(o1), ref) < RTOL and relmax(to_nchw(o2), ref) < RTOL
 
 
-def test_wino_offmask_matches_direct(stif):
+def test_wino_offmask_matches_direct(stif, pf):
     """64 -> 216 offset/mask conv (permuted [group][tap][dy,dx,sigmoid(m)] rows, 4 cout slices with
     the last one partial) on the Winograd kernel == the direct kernel, and == the oracle."""
     L, ops = stif._lib, stif.ops
@@ -153,7 +160,7 @@ def test_wino_offmask_matches_direct(stif):
     b = rnd(216, seed=32)
     o1 = torch.empty(2, 10, 40, 216, device="cuda")
     o2 = torch.empty_like(o1)
-    ops.conv2d([dict(layer=ops.pack_conv(w, b, L.PACK_WINO_OFFMASK), in0=nhwc(x), out=o1)], epi=L.EPI_OFFMASK)
+    ops.conv2d([dict(layer=ops.pack_conv(w, b, L.PACK_WINO_OFFMASK | pf), in0=nhwc(x), out=o1)], epi=L.EPI_OFFMASK)
     ops.conv2d([dict(layer=ops.pack_conv(w, b, L.PACK_OFFMASK), in0=nhwc(x), out=o2)], epi=L.EPI_OFFMASK)
     a1, a2 = o1.cpu().numpy(), o2.cpu().numpy()
     assert np.abs(a1 - a2).max() < 1e-5 * np.abs(a2).max()
@@ -166,13 +173,13 @@ def test_wino_offmask_matches_direct(stif):
 
 
 @pytest.mark.parametrize("hw", [(6, 40), (13, 37), (32, 64)])
-def test_wino_lstm_cell_conv(stif, sd, hw):
+def test_wino_lstm_cell_conv(stif, sd, hw, pf):
     """ConvLSTMCell conv + gates (convlstm.py:42-58) on the Winograd path (STIF_PACK_WINO_LSTM),
     both BiConvLSTM directions as two launch groups, against the oracle cell."""
     L, ops = stif._lib, stif.ops
     H, W = hw
     p = "ConvBLSTM.forward_net.cell_list.0."
-    layer = ops.pack_conv(sd[p + "conv.weight"], sd[p + "conv.bias"], L.PACK_WINO_LSTM)
+    layer = ops.pack_conv(sd[p + "conv.weight"], sd[p + "conv.bias"], L.PACK_WINO_LSTM | pf)
     groups, refs = [], []
     for d in range(2):
         x, h, c = (rnd(2, 64, H, W, seed=30 + 3 * d + k) for k in range(3))

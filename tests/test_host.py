@@ -189,3 +189,35 @@ def test_resize_tables_match_reference(stif):
     h = np.load(os.path.join(REPO, "tests", "golden", "harness.npz"))
     w, i0, s0 = stif.video.resize_tables(37, 19, 0.5)
     assert np.array_equal(w, h["w_37_19"]) and np.array_equal(i0, h["i_37_19"][:, 0]) and s0 == h["sym_37_19"][0]
+
+
+def test_pack_wino_f16x3_layout(stif):
+    """STIF_PACK_WINO | STIF_PACK_F16X3: [slice][pair][i][j][nt][plane][lane][8] fp16 halves,
+    element e of lane l = input channel 16 q + 8 (e >> 2) + 4 (l >> 5) + (e & 3); h + l = U * 2^10
+    to ~2^-22 relative (fp32-class operands)."""
+    L = stif._lib
+    lib = L.lib()
+    rng = np.random.default_rng(2)
+    cout, cin = 96, 32
+    mode = L.PACK_WINO | L.PACK_F16X3
+    w = (rng.standard_normal((cout, cin, 3, 3)) * 0.05).astype(np.float32)
+    b = rng.standard_normal(cout).astype(np.float32)
+    wd = np.empty(lib.stif_conv_weight_floats(cout, cin, 3, mode), np.float32)
+    bd = np.empty(lib.stif_conv_bias_floats(cout, mode), np.float32)
+    assert wd.size == 128 * cin * 16
+    assert lib.stif_pack_conv_weight(w.ctypes.data, b.ctypes.data, cout, cin, 3, mode,
+                                     wd.ctypes.data, bd.ctypes.data) == 0
+    G = np.array([[1, 0, 0], [.5, .5, .5], [.5, -.5, .5], [0, 0, 1]])
+    U = np.zeros((128, cin, 4, 4))
+    U[:cout] = np.einsum("ap,oipq,bq->oiab", G, w.astype(np.float64), G)
+    hv = wd.view(np.float16).astype(np.float64).reshape(2, cin // 16, 4, 4, 2, 2, 2, 32, 2, 4)
+    # axes: [s][q][i][j][nt][plane][hf][l32][eh][e4]; channel 16 q + 8 eh + 4 hf + e4
+    full = hv[:, :, :, :, :, 0] + hv[:, :, :, :, :, 1]           # h + l
+    got = full.transpose(0, 4, 6, 1, 7, 5, 8, 2, 3).reshape(128, cin, 4, 4) / 1024.0
+    assert np.abs(got - U).max() <= 2.0 ** -21 * np.abs(U).max()
+    hi = hv[:, :, :, :, :, 0].transpose(0, 4, 6, 1, 7, 5, 8, 2, 3).reshape(128, cin, 4, 4)
+    assert np.array_equal(hi, (U * 1024).astype(np.float16).astype(np.float64))   # h = rne16(U 2^10)
+    assert np.array_equal(bd[:cout], b)
+    with pytest.raises(Exception):
+        L.check(lib.stif_pack_conv_weight(w.ctypes.data, b.ctypes.data, cout, cin, 3, L.PACK_PLAIN | L.PACK_F16X3,
+                                          wd.ctypes.data, bd.ctypes.data), "pack")

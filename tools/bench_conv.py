@@ -18,7 +18,7 @@ x = torch.randn(N, H, W, 64, device="cuda")
 r = torch.randn(N, H, W, 64, device="cuda")
 flop = 2.0 * 64 * 64 * 9 * N * H * W
 ONLY = os.environ.get("ONLY")
-for name, mode in (("direct", L.PACK_PLAIN), ("wino", L.PACK_WINO)):
+for name, mode in (("direct", L.PACK_PLAIN), ("wino", L.PACK_WINO), ("wino16", L.PACK_WINO | L.PACK_F16X3)):
     if ONLY and name != ONLY:
         continue
     lay = ops.pack_conv(w, b, mode)
