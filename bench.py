@@ -31,15 +31,22 @@ CONFIGS = {
     "c2": (7, 540, 960, 4, [0.25, 0.5, 0.75]),
 }
 FP32_PEAK_TFLOPS = 157.3   # MI355X dense fp32 MFMA (MI355X_MICROARCH.md, chip-level parameters)
+# f16x3 operand mode: one fp32-class product = 3 products on the dense fp16 MFMA pipe (~2.5 PF/s)
+F16X3_PEAK_TFLOPS = 2500.0 / 3.0
 WINO_GAIN = 36.0 / 16.0    # F(2x2,3x3): 16 transformed-domain MACs per 36 direct MACs
 EPI_NAMES = {0: "NONE", 1: "LRELU", 2: "RELU", 3: "RES", 4: "OFFMASK", 5: "LSTM"}
 
 
-def kernel_desc(kind):
+def kernel_desc(kind, mfma="f32"):
     """(kernel name as rocprof shows it, description, peak in algorithmic TFLOP/s) of a launch kind."""
+    f16 = mfma == "f16x3"
     if kind[0] == "wino":
         _, ks, s, epi, in1, cout = kind
-        return (f"k_wino<{in1}, {epi}>", f"3x3 {64 * (2 if in1 else 1)}->{cout} conv, EPI_{EPI_NAMES[epi]}, "
+        if f16:
+            return (f"k_wino<{in1}, {epi}, 0, 1>", f"3x3 {64 * (2 if in1 else 1)}->{cout} conv, EPI_{EPI_NAMES[epi]}, "
+                    "Winograd F(2x2,3x3) on split-fp16 MFMA (3 fp16 products per fp32-class product); algorithmic = "
+                    "direct-conv FLOPs, peak = fp16 MFMA dense peak / 3 x 36/16", F16X3_PEAK_TFLOPS * WINO_GAIN)
+        return (f"k_wino<{in1}, {epi}, 0, 0>", f"3x3 {64 * (2 if in1 else 1)}->{cout} conv, EPI_{EPI_NAMES[epi]}, "
                 f"Winograd F(2x2,3x3) on fp32 MFMA; algorithmic = direct-conv FLOPs, peak = fp32 MFMA peak x 36/16",
                 FP32_PEAK_TFLOPS * WINO_GAIN)
     if kind[0] == "conv":
@@ -47,7 +54,10 @@ def kernel_desc(kind):
         return (f"k_conv<{ks}, {s}, ...>", f"{ks}x{ks}/s{s} conv -> {cout}, in1 mode {in1}, EPI_{EPI_NAMES[epi]}, "
                 "direct implicit GEMM on fp32 MFMA", FP32_PEAK_TFLOPS)
     if kind[0] == "dcn":
-        return ("k_dcn", "fused modulated deformable conv", FP32_PEAK_TFLOPS)
+        if f16:
+            return (f"k_dcn<{kind[1]}, 1>", "fused modulated deformable conv, split-fp16 MFMA (peak = fp16 MFMA / 3)",
+                    F16X3_PEAK_TFLOPS)
+        return (f"k_dcn<{kind[1]}, 0>", "fused modulated deformable conv", FP32_PEAK_TFLOPS)
     return (f"k_{kind[0]}", "SIREN decoder stage", FP32_PEAK_TFLOPS)
 
 
@@ -148,7 +158,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_r01.json"),
                     help="PMC summary (tools/pmc_summary.py) giving the dominant kernel's HBM bytes/dispatch")
-    ap.add_argument("--mfma", default="f32", choices=["f32", "f16x3"],
+    ap.add_argument("--mfma", default="f16x3", choices=["f32", "f16x3"],
                     help="Winograd conv operand mode (model.LunaTokis mfma=)")
     ap.add_argument("--kernel-report", action="store_true", help="time every conv launch kind (stderr)")
     args = ap.parse_args()
@@ -220,7 +230,7 @@ def main():
     value = world * out_pix * args.steps / elapsed / 1e6
     if rank == 0:
         achieved = avg_flops / (avg_ms * 1e-3) / 1e12 if avg_ms else 0.0
-        kname, kdesc, peak = kernel_desc(dom)
+        kname, kdesc, peak = kernel_desc(dom, args.mfma)
         traffic = None
         # HBM bytes per dispatch of the same kernel from the committed PMC passes over this bench
         # (tools/pmc_summary.py); they were measured at C1, so only a C1 line carries them
@@ -244,6 +254,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
+            "mfma_operands": ("f16x3: Winograd convs and the DCN core run fp32 products as 3 fp16 MFMA products "
+                              "on split operands (x = h + l, ~22-bit operands, fp32 accumulation; accuracy "
+                              "equal to the fp32-MFMA path, DESIGN.md section 3)") if args.mfma == "f16x3" else
+                             "f32: every contraction on fp32 MFMA",
             "data": "synthetic (U[0,1) frames, seeded; deterministic generated weights: checkpoint not in tree)",
             "config": {"workload": f"{nframes}x3x{H}x{W} window ({pairs} pairs), {scale}x spatial, t={times}",
                        "frames_per_gpu": nframes, "lr_hw": [H, W], "scale": scale, "times": times,

@@ -111,6 +111,7 @@ typedef struct {
   long long in_item, om_item, out_item;
   int ngroups, nitems, H, W;
   int epi;                              /* STIF_EPI_NONE or STIF_EPI_LRELU */
+  int flags;                            /* STIF_CONV_F16X3: w packed STIF_PACK_PLAIN | STIF_PACK_F16X3 */
 } stif_dcn_args;
 
 int stif_dcn_nhwc(const stif_dcn_args* args, void* stream);
@@ -222,7 +223,10 @@ size_t stif_conv_bias_floats(int cout, int mode);
  * i, f, o, g; convlstm.py:49), so one 4-cout quad holds the four gates of hidden channel h.
  * STIF_PACK_WINO* | STIF_PACK_F16X3: U * 2^10 split into fp16 h = rne(U 2^10), l = rne(U 2^10 - h)
  * as [cout/64][cin/16][i 4][j 4][nt 2][plane h|l][lane 64][8 halves], lane l's element e holding
- * input channel 16 q + 8 (e >> 2) + 4 (l >> 5) + (e & 3) (the chunk pair of one f16 MFMA). */
+ * input channel 16 q + 8 (e >> 2) + 4 (l >> 5) + (e & 3) (the chunk pair of one f16 MFMA).
+ * STIF_PACK_PLAIN | STIF_PACK_F16X3 (64 -> 64 3x3 only: the stif_dcn_nhwc core with
+ * flags = STIF_CONV_F16X3): [group 8][tap pair 5][nt 2][plane h|l][lane 64][8 halves], element e
+ * of lane l holding tap 2p + (e >> 2) (tap 9 = 0), input channel 8 group + 4 (l >> 5) + (e & 3). */
 int stif_pack_conv_weight(const float* w_oihw, const float* b, int cout, int cin, int ks, int mode,
                           float* w_dst, float* b_dst);
 

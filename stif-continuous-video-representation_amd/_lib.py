@@ -39,6 +39,7 @@ class DcnArgs(C.Structure):
         ("inp", _PA), ("offmask", _PA), ("w", _PA), ("bias", _PA), ("out", _PA),
         ("in_item", C.c_longlong), ("om_item", C.c_longlong), ("out_item", C.c_longlong),
         ("ngroups", C.c_int), ("nitems", C.c_int), ("H", C.c_int), ("W", C.c_int), ("epi", C.c_int),
+        ("flags", C.c_int),
     ]
 
 

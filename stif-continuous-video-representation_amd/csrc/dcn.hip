@@ -42,14 +42,17 @@ STIF_DEV f32x4 dcn_sample4(const float* __restrict__ img, int H, int W, float h,
 // samples its own MFMA A-fragment (pixel = lane & 31, channels 4h..4h+3) tap by tap from the
 // tile -- falling back to global loads only when an offset leaves the margin -- so sampling
 // (VALU + LDS) interleaves with the MFMAs and no sampled A tile ever round-trips memory.
-template <int EPI>
+// F16: the contraction on split-fp16 MFMA (stif_common.h split_f16x3): two taps per 32x32x16 MFMA
+// (lane half h: channels 4h..4h+3 of tap 2p at elements 0..3, of tap 2p + 1 at 4..7; tap 9 = 0),
+// weights packed STIF_PACK_PLAIN | STIF_PACK_F16X3 ([group][pair][nt][plane][lane][8 halves]).
+template <int EPI, int F16>
 __global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
   constexpr int NW = 4, TH = 4, M = 4;
   constexpr int TR = TH + 2 + 2 * M, TC = 32 + 2 + 2 * M;   // tile rows / cols
   constexpr int T_EL = TR * 2 * TC;                          // 16-B elements
   constexpr int T_INST = (T_EL + 63) / 64;
   constexpr int T_F = T_INST * 256;
-  constexpr int W_F = 9 * 2 * 64 * 4;                        // packed B fragments: [tap][nt][lane][4]
+  constexpr int W_F = F16 ? 5 * 2 * 2 * 256 : 9 * 2 * 64 * 4;   // packed B fragments of one group
   constexpr int BUF_F = T_F + W_F;
   __shared__ __attribute__((aligned(16))) float smem[2 * BUF_F];
 
@@ -92,6 +95,7 @@ __global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
   for (int k = 0; k < 27; ++k) omc[k] = omp[k];
 
   f32x16 acc0 = f32x16{0}, acc1 = f32x16{0};
+  f32x4 avp = f32x4{0.f, 0.f, 0.f, 0.f};   // F16: the even tap of the current pair
   stage(0, 0);
   lds_dma_barrier();
   for (int dg = 0; dg < 8; ++dg) {
@@ -144,12 +148,30 @@ __global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
           av = w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4;
         }
       }
-      const f32x4 b0 = ld4(sw + ((tap * 2 + 0) * 64 + lane) * 4);
-      const f32x4 b1 = ld4(sw + ((tap * 2 + 1) * 64 + lane) * 4);
+      if constexpr (F16) {
+        if ((tap & 1) == 0 && tap < 8) {
+          avp = av;
+        } else {
+          f16x8 ah, al;
+          if (tap == 8) split_f16x3(av, f32x4{0.f, 0.f, 0.f, 0.f}, ah, al);
+          else split_f16x3(avp, av, ah, al);
+          const float* wp = sw + (tap >> 1) * 1024 + lane * 4;   // [pair][nt][plane][lane][8 halves]
+          const f16x8 bh0 = ldh8(wp), bl0 = ldh8(wp + 256), bh1 = ldh8(wp + 512), bl1 = ldh8(wp + 768);
+          acc0 = mfma16h(ah, bh0, acc0);
+          acc1 = mfma16h(ah, bh1, acc1);
+          acc0 = mfma16h(ah, bl0, acc0);
+          acc1 = mfma16h(ah, bl1, acc1);
+          acc0 = mfma16h(al, bh0, acc0);
+          acc1 = mfma16h(al, bh1, acc1);
+        }
+      } else {
+        const f32x4 b0 = ld4(sw + ((tap * 2 + 0) * 64 + lane) * 4);
+        const f32x4 b1 = ld4(sw + ((tap * 2 + 1) * 64 + lane) * 4);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        acc0 = mfma32(av[q], b0[q], acc0);
-        acc1 = mfma32(av[q], b1[q], acc1);
+        for (int q = 0; q < 4; ++q) {
+          acc0 = mfma32(av[q], b0[q], acc0);
+          acc1 = mfma32(av[q], b1[q], acc1);
+        }
       }
     }
     if (dg + 1 < 8) {
@@ -170,7 +192,7 @@ __global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
     f32x16 v;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      float t = (nt ? acc1[r] : acc0[r]) + bv;
+      float t = (nt ? acc1[r] : acc0[r]) * (F16 ? F16X3_UNSCALE : 1.f) + bv;
       if (EPI == STIF_EPI_LRELU) t = lrelu01(t);
       v[r] = t;
     }
@@ -273,10 +295,15 @@ extern "C" int stif_dcn_nhwc(const stif_dcn_args* pa, void* stream) {
   if (a.ngroups < 1 || a.ngroups > STIF_MAX_GROUPS || a.nitems < 1 || a.H < 1 || a.W < 1)
     return stif_fail(STIF_E_INVALID, "stif_dcn_nhwc: bad sizes");
   dim3 grid(((a.W + 31) / 32) * ((a.H + 3) / 4), 1, a.ngroups * a.nitems);
-  if (a.epi == STIF_EPI_LRELU)
-    hipLaunchKernelGGL(k_dcn<STIF_EPI_LRELU>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  const bool f16 = a.flags & STIF_CONV_F16X3;
+  if (a.epi == STIF_EPI_LRELU && f16)
+    hipLaunchKernelGGL((k_dcn<STIF_EPI_LRELU, 1>), grid, dim3(256), 0, (hipStream_t)stream, a);
+  else if (a.epi == STIF_EPI_NONE && f16)
+    hipLaunchKernelGGL((k_dcn<STIF_EPI_NONE, 1>), grid, dim3(256), 0, (hipStream_t)stream, a);
+  else if (a.epi == STIF_EPI_LRELU)
+    hipLaunchKernelGGL((k_dcn<STIF_EPI_LRELU, 0>), grid, dim3(256), 0, (hipStream_t)stream, a);
   else if (a.epi == STIF_EPI_NONE)
-    hipLaunchKernelGGL(k_dcn<STIF_EPI_NONE>, grid, dim3(256), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL((k_dcn<STIF_EPI_NONE, 0>), grid, dim3(256), 0, (hipStream_t)stream, a);
   else
     return stif_fail(STIF_E_INVALID, "stif_dcn_nhwc: epilogue must be NONE or LRELU");
   return stif_check_launch("stif_dcn_nhwc");

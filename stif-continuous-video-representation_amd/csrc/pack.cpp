@@ -96,7 +96,9 @@ std::vector<float> omega(const float* src, size_t n) {
 }  // namespace
 
 extern "C" size_t stif_conv_weight_floats(int cout, int cin, int ks, int mode) {
-  mode &= ~STIF_PACK_F16X3;   // same bytes: two fp16 planes per fp32 value
+  // PLAIN | F16X3 (the DCN core, 64 -> 64 3x3): 5 tap pairs x 2 nt x 2 planes x 1 KB per 8-channel group
+  if (mode == (STIF_PACK_PLAIN | STIF_PACK_F16X3)) return (size_t)(cin / 8) * 5 * 2 * 2 * 256;
+  mode &= ~STIF_PACK_F16X3;   // Winograd: same bytes, two fp16 planes per fp32 value
   if (mode == STIF_PACK_WINO || mode == STIF_PACK_WINO_OFFMASK || mode == STIF_PACK_WINO_LSTM)
     return (size_t)round64(cout) * cin * 16;
   return (size_t)cout_padded(cout, mode) * cin * ks * ks;
@@ -135,6 +137,33 @@ int pack_wino(const float* w, const float* b, int cout, int cin, int perm, float
       const int sr = src_row(j, cout, perm);
       b_dst[j] = (sr >= 0 && b) ? b[sr] : 0.f;
     }
+  return STIF_OK;
+}
+
+// x * 2^10 split into fp16 h = rne(x 2^10), l = rne(x 2^10 - h) (double arithmetic)
+void split_f16x3_host(double x, _Float16* h, _Float16* l) {
+  const double v = x * 1024.0;
+  *h = (_Float16)v;
+  *l = (_Float16)(v - (double)*h);
+}
+
+// PLAIN | F16X3, the fused DCN core (k_dcn<F16>): [group][tap pair p][nt][plane][lane][8 halves];
+// element e of lane l holds tap 2p + (e >> 2) (tap 9 = zero padding), input channel
+// 8 group + 4 (l >> 5) + (e & 3), cout nt * 32 + (l & 31)
+int pack_dcn_f16x3(const float* w, const float* b, int cout, int cin, float* w_dst, float* b_dst) {
+  _Float16* dst = reinterpret_cast<_Float16*>(w_dst);
+  for (int g = 0; g < cin / 8; ++g)
+    for (int p = 0; p < 5; ++p)
+      for (int nt = 0; nt < 2; ++nt)
+        for (int l = 0; l < 64; ++l)
+          for (int e = 0; e < 8; ++e) {
+            const int tap = 2 * p + (e >> 2), ci = 8 * g + 4 * (l >> 5) + (e & 3), co = nt * 32 + (l & 31);
+            const double x = tap < 9 ? (double)w[((size_t)co * cin + ci) * 9 + tap] : 0.0;
+            const size_t o = ((((size_t)g * 5 + p) * 2 + nt) * 2) * 512 + l * 8 + e;
+            split_f16x3_host(x, dst + o, dst + o + 512);
+          }
+  if (b_dst)
+    for (int j = 0; j < cout; ++j) b_dst[j] = b ? b[j] : 0.f;
   return STIF_OK;
 }
 
@@ -191,7 +220,12 @@ extern "C" int stif_pack_conv_weight(const float* w, const float* b, int cout, i
     const int perm = mode == STIF_PACK_WINO ? STIF_PACK_PLAIN : (mode == STIF_PACK_WINO_OFFMASK ? STIF_PACK_OFFMASK : mode);
     return f16x3 ? pack_wino_f16x3(w, b, cout, cin, perm, w_dst, b_dst) : pack_wino(w, b, cout, cin, perm, w_dst, b_dst);
   }
-  if (f16x3) return stif_fail(STIF_E_INVALID, "STIF_PACK_F16X3 applies to the Winograd packings only");
+  if (f16x3 && mode == STIF_PACK_PLAIN) {
+    if (ks != 3 || cout != 64 || cin != 64)
+      return stif_fail(STIF_E_INVALID, "PLAIN | F16X3 (DCN core) packing needs a 64 -> 64 3x3 weight");
+    return pack_dcn_f16x3(w, b, cout, cin, w_dst, b_dst);
+  }
+  if (f16x3) return stif_fail(STIF_E_INVALID, "STIF_PACK_F16X3 applies to the Winograd and DCN packings only");
   // layout [slice][chunk][tap][nt][lane][4]: the B fragments of one (slice, chunk) are one
   // contiguous block, copied to LDS by LDS-DMA; lane l of N-tile nt holds cout
   // slice*NJ + nt*32 + (l & 31), input channels chunk*8 + 4*(l >> 5) + e.

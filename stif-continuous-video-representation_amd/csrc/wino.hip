@@ -252,9 +252,14 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256) __attribute__((amdgpu_waves_per_
           // K values of a 32x32x16 f16 MFMA; transform both, split all four j, then fetch the next
           // pair's first chunk so its LDS reads hide under this pair's MFMAs
           f32x4 va[4], vb[4];
+#ifdef WINO_EXP_NOXF
+          va[0] = va[1] = va[2] = va[3] = f32x4{1.f * sp, 1.f, 1.f, (float)lane};
+          vb[0] = vb[1] = vb[2] = vb[3] = f32x4{1.f * sp, 1.f, 3.f, (float)lane};
+#else
           xform(rd, va);
           xread(buf, 2 * sp + 1, rd);
           xform(rd, vb);
+#endif
           const int q = p * (PSUB / 2) + sp;
           const float* wq = wsl + (size_t)q * 16384;
           const float* wq1 = q + 1 < NQ ? wq + 16384 : wnx;
@@ -274,18 +279,25 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256) __attribute__((amdgpu_waves_per_
             }
             // refill the slot with block j + 2: (pair q, j + 2) or (pair q + 1, j - 2)
             const float* wn = j < 2 ? wq + (j + 2) * 1024 : wq1 + (j - 2) * 1024;
+#ifndef WINO_EXP_NOB
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
               bh[j & 1][u] = ldh8(wn + (u * 2) * 256);
               bl[j & 1][u] = ldh8(wn + (u * 2 + 1) * 256);
             }
+#else
+            (void)wn;
+            for (int u = 0; u < 2; ++u) bh[j & 1][u] += (_Float16)1.f;
+#endif
             __builtin_amdgcn_sched_barrier(0);
           }
         }
         // every load older than the last two blocks' B refills (8) -- the phase's LDS-DMA among
         // them -- has landed
+        WTR(6);
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         __syncthreads();
+        WTR(2);
       }
     } else
     for (int p = 0; p < NP; ++p, ++gp) {

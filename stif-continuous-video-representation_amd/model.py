@@ -37,7 +37,7 @@ class LunaTokis:
     """STIF LunaTokis (Sakuya_arch_test.py:268) on MI355X."""
 
     def __init__(self, nf=64, nframes=3, groups=8, front_RBs=5, back_RBs=10, device="cuda", winograd=True,
-                 mfma="f32"):
+                 mfma="f16x3"):
         if nf != 64 or groups != 8:
             raise ValueError("the gfx950 kernels implement nf=64, groups=8 (the shipped STIF configuration)")
         self.nf, self.groups = nf, groups
@@ -147,7 +147,7 @@ class LunaTokis:
                 for ln, cin, _ in W._PCD_LAYERS:
                     n = f"{prefix}{ln}_{d}"
                     if cin is None:
-                        conv(n)
+                        conv(n, L.PACK_PLAIN | f16)     # the DCN core (k_dcn)
                         conv(n + ".conv_offset_mask", (L.PACK_WINO_OFFMASK | f16) if self.winograd else L.PACK_OFFMASK)
                     else:
                         conv(n, wino)

@@ -172,6 +172,10 @@ def dcn(groups, *, epi=L.EPI_NONE):
     a.om_item = _item_stride([g["offmask"] for g in groups], "dcn offmask")
     a.out_item = _item_stride([g["out"] for g in groups], "dcn out")
     a.ngroups, a.nitems, a.H, a.W, a.epi = len(groups), nitems, H, W, epi
+    f16 = g0["layer"].mode & L.PACK_F16X3
+    if any((g["layer"].mode & L.PACK_F16X3) != f16 for g in groups):
+        raise ValueError("dcn: groups mix f32 / f16x3 packings")
+    a.flags = L.CONV_F16X3 if f16 else 0
     tr = TRACE
     if tr is not None:
         tr.begin(("dcn", epi), 2.0 * 64 * 576 * H * W * nitems * len(groups),

@@ -191,31 +191,31 @@ def test_decoding_localensemble(latent16, golden, which):
 
 
 @pytest.fixture(scope="module")
-def model_f16x3(stif, sd):
-    m = stif.LunaTokis(64, 6, 8, 5, 40, mfma="f16x3")
+def model_f32(stif, sd):
+    m = stif.LunaTokis(64, 6, 8, 5, 40, mfma="f32")
     m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
     return m.eval()
 
 
-def test_f16x3_outputs_match_reference(model_f16x3, golden):
-    """mfma='f16x3' (Winograd convs on split-fp16 MFMA operands) against the reference's outputs,
-    at the same bar as the fp32-MFMA path."""
+def test_f32_mfma_outputs_match_reference(model_f32, golden):
+    """mfma='f32' (every contraction on fp32 MFMA; the default 'f16x3' runs the Winograd convs and
+    the DCN core on split-fp16 MFMA operands) against the reference's outputs, same bar."""
     g = golden["model_16x20"]
     with torch.no_grad():
-        outs = model_f16x3(torch.from_numpy(g["x"]).cuda(), [torch.tensor([[float(t)]]) for t in g["times"]])
-    ok, err, mx = close(model_f16x3.feat.detach().cpu().numpy()[0], g["feat"])
+        outs = model_f32(torch.from_numpy(g["x"]).cuda(), [torch.tensor([[float(t)]]) for t in g["times"]])
+    ok, err, mx = close(model_f32.feat.detach().cpu().numpy()[0], g["feat"])
     assert ok, (err, mx)
     for i, o in enumerate(outs):
         ok, err, mx = close(o[0], g["out"][i])
         assert ok, (i, err, mx)
 
 
-def test_f16x3_window_and_psnr(model_f16x3, golden, sd):
+def test_f32_mfma_window_and_psnr(model_f32, golden, sd):
     """7-frame window against the reference, and the PSNR criterion (< 1e-3 dB)."""
     g = golden["window_7x16x16"]
     with torch.no_grad():
-        model_f16x3.gen_feat_window(torch.from_numpy(g["frames"]).cuda())
-        out = model_f16x3.decoding([torch.tensor([[0.5]])])[0]
+        model_f32.gen_feat_window(torch.from_numpy(g["frames"]).cuda())
+        out = model_f32.decoding([torch.tensor([[0.5]])])[0]
     ok, err, mx = close(out, g["out"])
     assert ok, (err, mx)
     gt = np.clip(g["out"] + 0.05 * np.random.default_rng(3).standard_normal(g["out"].shape), 0, 1)
@@ -223,11 +223,11 @@ def test_f16x3_window_and_psnr(model_f16x3, golden, sd):
     assert d < 1e-3, d
 
 
-def test_f16x3_larger_size_vs_oracle(model_f16x3, sd):
+def test_f32_mfma_larger_size_vs_oracle(model_f32, sd):
     rng = np.random.default_rng(7)
     x = rng.random((1, 2, 3, 32, 48)).astype(np.float32)
     ref = O.forward(x, [0.3], sd)[0]
     with torch.no_grad():
-        out = model_f16x3(torch.from_numpy(x).cuda(), [0.3])[0]
+        out = model_f32(torch.from_numpy(x).cuda(), [0.3])[0]
     ok, err, mx = close(out, ref)
     assert ok, (err, mx)

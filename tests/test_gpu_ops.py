@@ -161,7 +161,8 @@ def _offsets(B, H, W, seed, scale=2.0):
 @pytest.mark.parametrize("epi", ["none", "lrelu"])
 @pytest.mark.parametrize("hw", [(9, 11), (16, 40), (21, 70)])
 @pytest.mark.parametrize("oscale", [0.7, 2.0, 7.0])   # 7.0: many samples leave the staged margin
-def test_dcn_fused(ops, L, epi, hw, oscale):
+@pytest.mark.parametrize("f16", [0, 1], ids=["f32", "f16x3"])
+def test_dcn_fused(ops, L, epi, hw, oscale, f16):
     H, W = hw
     B = 2
     x = rnd(B, 64, H, W, seed=30)
@@ -176,7 +177,8 @@ def test_dcn_fused(ops, L, epi, hw, oscale):
     m = mask.reshape(B, 8, 9, H, W).transpose(0, 3, 4, 1, 2)
     om = np.concatenate([o, m[..., None]], -1).reshape(B, H, W, 216)
     out = torch.empty(B, H, W, 64, device="cuda")
-    ops.dcn([dict(layer=ops.pack_conv(w, b), inp=nhwc(x), offmask=torch.from_numpy(np.ascontiguousarray(om)).cuda(),
+    lay = ops.pack_conv(w, b, L.PACK_PLAIN | (L.PACK_F16X3 if f16 else 0))
+    ops.dcn([dict(layer=lay, inp=nhwc(x), offmask=torch.from_numpy(np.ascontiguousarray(om)).cuda(),
                   out=out)], epi=L.EPI_LRELU if epi == "lrelu" else L.EPI_NONE)
     assert relmax(to_nchw(out), ref) < RTOL
 

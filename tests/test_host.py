@@ -219,5 +219,5 @@ def test_pack_wino_f16x3_layout(stif):
     assert np.array_equal(hi, (U * 1024).astype(np.float16).astype(np.float64))   # h = rne16(U 2^10)
     assert np.array_equal(bd[:cout], b)
     with pytest.raises(Exception):
-        L.check(lib.stif_pack_conv_weight(w.ctypes.data, b.ctypes.data, cout, cin, 3, L.PACK_PLAIN | L.PACK_F16X3,
+        L.check(lib.stif_pack_conv_weight(w.ctypes.data, b.ctypes.data, cout, cin, 3, L.PACK_OFFMASK | L.PACK_F16X3,
                                           wd.ctypes.data, bd.ctypes.data), "pack")

@@ -23,7 +23,7 @@ w = (rng.standard_normal((64, 64, 3, 3)) * 0.05).astype(np.float32)
 b = rng.standard_normal(64).astype(np.float32)
 x = torch.randn(N, H, W, 64, device="cuda")
 r = torch.randn(N, H, W, 64, device="cuda")
-lay = ops.pack_conv(w, b, L.PACK_WINO)
+lay = ops.pack_conv(w, b, L.PACK_WINO | (L.PACK_F16X3 if os.environ.get("F16") else 0))
 out = torch.empty(N, H, W, 64, device="cuda")
 for _ in range(3):
     ops.conv2d([dict(layer=lay, in0=x, out=out, res=r)], epi=EPI)
@@ -47,7 +47,7 @@ names = {1: "start", 6: "pre-bar", 2: "post-bar", 3: "xchg", 4: "comb", 5: "stor
 for k in sorted(seg):
     v = np.array(seg[k])
     print(f"wave {k[0]} {names[k[1]]:>8s} -> {names[k[2]]:<8s} n={len(v):5d} avg {v.mean():8.0f} med {np.median(v):8.0f} cyc")
-print("MFMA cycles per tile per wave at peak: 256 x 64 =", 256 * 64)
+print("MFMA cycles per tile per wave at peak:", 4 * 24 * 32 if os.environ.get("F16") else 256 * 64)
 
 
 def phase_intervals(blk, wv):
