@@ -58,6 +58,8 @@ def kernel_desc(kind, mfma="f32"):
             return (f"k_dcn<{kind[1]}, 1>", "fused modulated deformable conv, split-fp16 MFMA (peak = fp16 MFMA / 3)",
                     F16X3_PEAK_TFLOPS)
         return (f"k_dcn<{kind[1]}, 0>", "fused modulated deformable conv", FP32_PEAK_TFLOPS)
+    if f16:
+        return (f"k_{kind[0]}", "SIREN decoder stage, split-fp16 MFMA (peak = fp16 MFMA / 3)", F16X3_PEAK_TFLOPS)
     return (f"k_{kind[0]}", "SIREN decoder stage", FP32_PEAK_TFLOPS)
 
 
@@ -254,7 +256,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "mfma_operands": ("f16x3: Winograd convs and the DCN core run fp32 products as 3 fp16 MFMA products "
+            "mfma_operands": ("f16x3: Winograd convs, the DCN core and the SIREN decoder layers run fp32 products as 3 fp16 MFMA products "
                               "on split operands (x = h + l, ~22-bit operands, fp32 accumulation; accuracy "
                               "equal to the fp32-MFMA path, DESIGN.md section 3)") if args.mfma == "f16x3" else
                              "f32: every contraction on fp32 MFMA",

@@ -176,6 +176,14 @@ int stif_dec_stage1(const float* proj, const float* mlp, const stif_dec_tables* 
 int stif_dec_stage2(const float* proj, const float* mlp, const float* hrfeat, const float* flow,
                     const stif_dec_tables* tab, const stif_dec_image* img, const float* t, float* out_nchw,
                     int n, int h, int w, int HH, int WW, void* stream);
+/* The same stages with flags = STIF_CONV_F16X3: every SIREN layer on split-fp16 MFMA (mlp packed by
+ * stif_pack_dec_mlp_ex with the same flag); flags = 0 is stif_dec_stage1 / stif_dec_stage2. */
+int stif_dec_stage1_ex(const float* proj, const float* mlp, const stif_dec_tables* tab, const stif_dec_image* img,
+                       const float* t, float* hrfeat, float* flow, int n, int h, int w, int HH, int WW, int flags,
+                       void* stream);
+int stif_dec_stage2_ex(const float* proj, const float* mlp, const float* hrfeat, const float* flow,
+                       const stif_dec_tables* tab, const stif_dec_image* img, const float* t, float* out, int n, int h,
+                       int w, int HH, int WW, int flags, void* stream);
 
 /* out = sum_k pred_k * wgt_k (per HR pixel weights [HH*WW], shared by the n items): the
  * local ensemble's area blend (Sakuya_arch_test.py:1076-1084). pred_k / out: [n][3][HH][WW]. */
@@ -242,6 +250,11 @@ size_t stif_dec_mlp_floats(void);
  * feat: w0,b0,w1,b1,w2,b2,w3,b3; flow: same; enc: w0..w4, b0..b4 interleaved. */
 int stif_pack_dec_mlp(const float* const* feat, const float* const* flow, const float* const* enc,
                       float* dst);
+/* flags = STIF_CONV_F16X3: every 32x32 MFMA weight tile as a split-fp16 tile ([m 2][plane h|l][lane 64]
+ * [8 halves] of W * 2^10, element e of half-tile m = feature F(8m + e, lane >> 5)) and the image tiles
+ * scaled by 2^14, for stif_dec_stage1_ex / stif_dec_stage2_ex with the same flag. */
+int stif_pack_dec_mlp_ex(const float* const* feat, const float* const* flow, const float* const* enc,
+                         float* dst, int flags);
 
 const char* stif_last_error(void);
 const char* stif_version(void);

@@ -68,6 +68,10 @@ EXPORTS = {
                         + [_P]),
     "stif_dec_stage2": (C.c_int, [_P, _P, _P, _P, C.POINTER(DecTables), C.POINTER(DecImage), _P, _P]
                         + [C.c_int] * 5 + [_P]),
+    "stif_dec_stage1_ex": (C.c_int, [_P, _P, C.POINTER(DecTables), C.POINTER(DecImage), _P, _P, _P]
+                           + [C.c_int] * 6 + [_P]),
+    "stif_dec_stage2_ex": (C.c_int, [_P, _P, _P, _P, C.POINTER(DecTables), C.POINTER(DecImage), _P, _P]
+                           + [C.c_int] * 6 + [_P]),
     "stif_dec_blend4": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_int, _P]),
     "stif_upsample_image": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P]),
     "stif_resize_frames": (C.c_int, [_P, _P] + [C.c_int] * 5 + [_P, _P, C.c_int, C.c_int, _P, _P, C.c_int, C.c_int,
@@ -81,6 +85,7 @@ EXPORTS = {
     "stif_pack_dec_proj": (C.c_int, [_P] * 6),
     "stif_dec_mlp_floats": (C.c_size_t, []),
     "stif_pack_dec_mlp": (C.c_int, [C.POINTER(_P), C.POINTER(_P), C.POINTER(_P), _P]),
+    "stif_pack_dec_mlp_ex": (C.c_int, [C.POINTER(_P), C.POINTER(_P), C.POINTER(_P), _P, C.c_int]),
     "stif_last_error": (C.c_char_p, []),
     "stif_version": (C.c_char_p, []),
 }

@@ -26,24 +26,59 @@ namespace {
 
 using namespace stif_dec;
 
+// F16 (stif_pack_dec_mlp_ex with STIF_CONV_F16X3): every 32x32 weight tile is a split-fp16 tile
+// ([m][plane h|l][lane][8 halves], W * 2^10) and every register tile that feeds one is split too
+// (x * 2^4, split_f16x3), so MFMA accumulators hold values x 2^14 -- everything added into them
+// (gathered projections, bias terms, the fp32 image tiles, packed x 2^14) is scaled to match and
+// every consumer unscales (ACC_S).
+template <int F16>
+struct XT;   // a 32-feature register tile as an MFMA B operand
+template <>
+struct XT<0> {
+  f32x16 v;
+};
+template <>
+struct XT<1> {
+  f16x8 h[2], l[2];
+};
+template <int F16>
+STIF_DEV XT<F16> xop(const f32x16& x) {
+  XT<F16> o;
+  if constexpr (F16) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+      split_f16x3(f32x4{x[8 * m], x[8 * m + 1], x[8 * m + 2], x[8 * m + 3]},
+                  f32x4{x[8 * m + 4], x[8 * m + 5], x[8 * m + 6], x[8 * m + 7]}, o.h[m], o.l[m]);
+  } else {
+    o.v = x;
+  }
+  return o;
+}
+template <int F16>
+constexpr float ACC_S = F16 ? F16X3_UNSCALE : 1.f;   // accumulator -> value
+template <int F16>
+constexpr float ACC_IN = F16 ? 16384.f : 1.f;        // value -> accumulator
+
 // SineLayer: sin(30 * (z + b)) (SIREN.py:44-45, omega_0 = 30); the packed weights and biases of every
 // sine layer carry the factor 30 (pack.cpp), so the kernel evaluates sin(z + b)
+template <int F16>
 STIF_DEV f32x16 bias_sin(f32x16 z, const float* __restrict__ b, int hf) {
 #pragma unroll
   for (int v = 0; v < 4; ++v) {
     const f32x4 bb = ld4(b + 8 * v + 4 * hf);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) z[4 * v + e] = stif_sin(z[4 * v + e] + bb[e]);
+    for (int e = 0; e < 4; ++e) z[4 * v + e] = stif_sin(fmaf(z[4 * v + e], ACC_S<F16>, bb[e]));
   }
   return z;
 }
 
+template <int F16>
 STIF_DEV f32x16 bias_add(f32x16 z, const float* __restrict__ b, int hf) {
 #pragma unroll
   for (int v = 0; v < 4; ++v) {
     const f32x4 bb = ld4(b + 8 * v + 4 * hf);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) z[4 * v + e] += bb[e];
+    for (int e = 0; e < 4; ++e) z[4 * v + e] = fmaf(z[4 * v + e], ACC_S<F16>, bb[e]);
   }
   return z;
 }
@@ -142,17 +177,30 @@ STIF_DEV __amdgpu_buffer_rsrc_t mlp_rsrc(const float* mlp) {
 }
 
 // acc += W_tile . x, tile in LDS ([v][lane][4]), x = one 32-feature register tile
-STIF_DEV void tile_mma(f32x16& acc, const float* t, const f32x16& x, int lane) {
+template <int F16>
+STIF_DEV void tile_mma(f32x16& acc, const float* t, const XT<F16>& xt, int lane) {
   const float* b = t + lane * 4;
-  const f32x4 w0 = ld4(b), w1 = ld4(b + 256), w2 = ld4(b + 512), w3 = ld4(b + 768);
+  if constexpr (F16) {
+    // tile [m][plane][lane][8 halves]: element e of half-tile m = feature F(8m + e, lane >> 5)
 #pragma unroll
-  for (int e = 0; e < 4; ++e) acc = mfma32(w0[e], x[e], acc);
+    for (int m = 0; m < 2; ++m) {
+      const f16x8 ah = ldh8(b + (2 * m) * 256), al = ldh8(b + (2 * m + 1) * 256);
+      acc = mfma16h(ah, xt.h[m], acc);
+      acc = mfma16h(al, xt.h[m], acc);
+      acc = mfma16h(ah, xt.l[m], acc);
+    }
+  } else {
+    const f32x16& x = xt.v;
+    const f32x4 w0 = ld4(b), w1 = ld4(b + 256), w2 = ld4(b + 512), w3 = ld4(b + 768);
 #pragma unroll
-  for (int e = 0; e < 4; ++e) acc = mfma32(w1[e], x[4 + e], acc);
+    for (int e = 0; e < 4; ++e) acc = mfma32(w0[e], x[e], acc);
 #pragma unroll
-  for (int e = 0; e < 4; ++e) acc = mfma32(w2[e], x[8 + e], acc);
+    for (int e = 0; e < 4; ++e) acc = mfma32(w1[e], x[4 + e], acc);
 #pragma unroll
-  for (int e = 0; e < 4; ++e) acc = mfma32(w3[e], x[12 + e], acc);
+    for (int e = 0; e < 4; ++e) acc = mfma32(w2[e], x[8 + e], acc);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc = mfma32(w3[e], x[12 + e], acc);
+  }
   // keep the compiler from hoisting the LDS reads of many tiles ahead (VGPR budget)
   __builtin_amdgcn_sched_barrier(0);
 }
@@ -174,7 +222,7 @@ STIF_DEV void narrow_dot(float* o, const float* W, int kt, const f32x16& x, int 
 // MODE 0: feat_imnet + flow_imnet fused (the flow stage reads the pixel's own HRfeat);
 // MODE 1: feat_imnet only; MODE 2: flow_imnet only, reading HRfeat at (hr_y, hr_x) of the query
 // (local ensemble).  HRIMG: the flow stage's image input comes from the high-resolution image.
-template <int MODE, bool HRIMG>
+template <int MODE, bool HRIMG, int F16>
 __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))) void k_dec1(const float* __restrict__ proj, const float* __restrict__ mlp,
                                                      stif_dec_tables tb, stif_dec_image im,
                                                      const float* __restrict__ tq, float* __restrict__ hrfeat,
@@ -231,14 +279,18 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
   lds_dma_barrier();
   seg_feat23(B1, 0);
   // ---- layer 1: 64 -> 64
+  {
+    const XT<F16> xs[2] = {xop<F16>(x0[0]), xop<F16>(x0[1])};
 #pragma unroll
-  for (int ot = 0; ot < 2; ++ot) {
-    f32x16 acc = f32x16{0};
+    for (int ot = 0; ot < 2; ++ot) {
+      f32x16 acc = f32x16{0};
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) tile_mma(acc, B0 + (ot * 2 + kt) * T, x0[kt], lane);
-    x1[ot] = bias_sin(acc, mlp + F_B1 + ot * 32, hf);
+      for (int kt = 0; kt < 2; ++kt) tile_mma<F16>(acc, B0 + (ot * 2 + kt) * T, xs[kt], lane);
+      x1[ot] = bias_sin<F16>(acc, mlp + F_B1 + ot * 32, hf);
+    }
   }
   // ---- layer 2 (64 -> 256, sine) streamed into layer 3 (256 -> 64, linear)
+  const XT<F16> x1s[2] = {xop<F16>(x1[0]), xop<F16>(x1[1])};
 #pragma unroll 1
   for (int kt = 0; kt < 8; ++kt) {
     lds_dma_barrier();
@@ -250,14 +302,14 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
       dma_tiles<DEC_NW>(nxt + 4 * T, rm, L_W1, 4, wv, lane);
     }
     f32x16 acc = f32x16{0};
-    tile_mma(acc, cur, x1[0], lane);
-    tile_mma(acc, cur + T, x1[1], lane);
-    const f32x16 h2 = bias_sin(acc, mlp + F_B2 + kt * 32, hf);
-    tile_mma(hr[0], cur + 2 * T, h2, lane);
-    tile_mma(hr[1], cur + 3 * T, h2, lane);
+    tile_mma<F16>(acc, cur, x1s[0], lane);
+    tile_mma<F16>(acc, cur + T, x1s[1], lane);
+    const XT<F16> h2 = xop<F16>(bias_sin<F16>(acc, mlp + F_B2 + kt * 32, hf));
+    tile_mma<F16>(hr[0], cur + 2 * T, h2, lane);
+    tile_mma<F16>(hr[1], cur + 3 * T, h2, lane);
   }
 #pragma unroll
-  for (int ot = 0; ot < 2; ++ot) hr[ot] = bias_add(hr[ot], mlp + F_B3 + ot * 32, hf);
+  for (int ot = 0; ot < 2; ++ot) hr[ot] = bias_add<F16>(hr[ot], mlp + F_B3 + ot * 32, hf);
   if (valid) {
     float* o = hrfeat + (size_t)pc * 64;
 #pragma unroll
@@ -298,7 +350,7 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
         const int f = ot * 32 + 8 * v + 4 * hf;
         const f32x4 wt = ld4(mlp + L_WT + f), bb = ld4(mlp + L_B0 + f);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) z[ot][4 * v + e] += wt[e] * t + bb[e];
+        for (int e = 0; e < 4; ++e) z[ot][4 * v + e] = (z[ot][4 * v + e] + (wt[e] * t + bb[e])) * ACC_IN<F16>;
       }
     if constexpr (HRIMG) {   // q_inp from the high-resolution image (decoding_test :515-518)
       Bilin bi;
@@ -315,20 +367,27 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
     dma_tiles<DEC_NW>(dst, rm, L_W2 + kt * 2 * T, 2, wv, lane);
   };
   seg_flow23(B0, 0);
+  {
+    const XT<F16> hs[2] = {xop<F16>(hr[0]), xop<F16>(hr[1])};
 #pragma unroll
-  for (int ot = 0; ot < 2; ++ot) {
+    for (int ot = 0; ot < 2; ++ot) {
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) tile_mma(z[ot], B1 + (ot * 2 + kt) * T, hr[kt], lane);
+      for (int kt = 0; kt < 2; ++kt) tile_mma<F16>(z[ot], B1 + (ot * 2 + kt) * T, hs[kt], lane);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) z[ot][r] = stif_sin(z[ot][r]);
+      for (int r = 0; r < 16; ++r) z[ot][r] = stif_sin(z[ot][r] * ACC_S<F16>);
+    }
   }
+  {
+    const XT<F16> zs[2] = {xop<F16>(z[0]), xop<F16>(z[1])};
 #pragma unroll
-  for (int ot = 0; ot < 2; ++ot) {
-    f32x16 acc = f32x16{0};
+    for (int ot = 0; ot < 2; ++ot) {
+      f32x16 acc = f32x16{0};
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) tile_mma(acc, B1 + (4 + ot * 2 + kt) * T, z[kt], lane);
-    x1[ot] = bias_sin(acc, mlp + L_B1 + ot * 32, hf);
+      for (int kt = 0; kt < 2; ++kt) tile_mma<F16>(acc, B1 + (4 + ot * 2 + kt) * T, zs[kt], lane);
+      x1[ot] = bias_sin<F16>(acc, mlp + L_B1 + ot * 32, hf);
+    }
   }
+  const XT<F16> x1f[2] = {xop<F16>(x1[0]), xop<F16>(x1[1])};
   float fl[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
   for (int kt = 0; kt < 8; ++kt) {
@@ -337,9 +396,9 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
     float* nxt = (kt & 1) ? B0 : B1;
     if (kt < 7) seg_flow23(nxt, kt + 1);
     f32x16 acc = f32x16{0};
-    tile_mma(acc, cur, x1[0], lane);
-    tile_mma(acc, cur + T, x1[1], lane);
-    const f32x16 h2 = bias_sin(acc, mlp + L_B2 + kt * 32, hf);
+    tile_mma<F16>(acc, cur, x1f[0], lane);
+    tile_mma<F16>(acc, cur + T, x1f[1], lane);
+    const f32x16 h2 = bias_sin<F16>(acc, mlp + L_B2 + kt * 32, hf);
     narrow_dot<4>(fl, W3V, kt, h2, hf);   // flow_imnet.net.3 (256 -> 4, linear)
   }
 #pragma unroll
@@ -353,7 +412,7 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
   }
 }
 
-template <bool HRIMG>
+template <bool HRIMG, int F16>
 __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DEC2_WPE))) void k_dec2(const float* __restrict__ proj, const float* __restrict__ mlp,
                                                      const float* __restrict__ hrfeat, const float* __restrict__ flow,
                                                      stif_dec_tables tb, stif_dec_image im,
@@ -405,7 +464,7 @@ __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DE
         const int f = ot * 32 + 8 * v + 4 * hf;
         const f32x4 wt = ld4(mlp + E_WT + f), bb = ld4(mlp + E_B0 + f);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) z[ot][4 * v + e] += q[ot][4 * v + e] + wt[e] * t + bb[e];
+        for (int e = 0; e < 4; ++e) z[ot][4 * v + e] = (z[ot][4 * v + e] + (q[ot][4 * v + e] + wt[e] * t + bb[e])) * ACC_IN<F16>;
       }
     if constexpr (HRIMG) {   // q_img1 / q_img2 from the high-resolution image (decoding_test :558-583)
       const float* I = im.img + (size_t)item * im.ih * im.iw * IMG_C;
@@ -416,18 +475,22 @@ __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DE
     gather64(q, HRF, 64, 0, bilin(g1x, g1y, WW, HH), hf);   // q_feat1 -> W0 columns 0..63
     lds_dma_barrier();
     dma_tiles<DEC2_NW>(B1, rm, E_W1, 4, wv, lane);
+    {
+      const XT<F16> qs[2] = {xop<F16>(q[0]), xop<F16>(q[1])};
 #pragma unroll
-    for (int ot = 0; ot < 2; ++ot)
+      for (int ot = 0; ot < 2; ++ot)
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) tile_mma(z[ot], B0 + (ot * 4 + kt) * T, q[kt], lane);
+        for (int kt = 0; kt < 2; ++kt) tile_mma<F16>(z[ot], B0 + (ot * 4 + kt) * T, qs[kt], lane);
+    }
     asm volatile("" ::: "memory");
     gather64(q, HRF, 64, 0, bilin(g2x, g2y, WW, HH), hf);   // q_feat2 -> W0 columns 64..127
+    const XT<F16> qs[2] = {xop<F16>(q[0]), xop<F16>(q[1])};
 #pragma unroll
     for (int ot = 0; ot < 2; ++ot) {
 #pragma unroll
-      for (int kt = 2; kt < 4; ++kt) tile_mma(z[ot], B0 + (ot * 4 + kt) * T, q[kt - 2], lane);
+      for (int kt = 2; kt < 4; ++kt) tile_mma<F16>(z[ot], B0 + (ot * 4 + kt) * T, qs[kt - 2], lane);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) x0[ot][r] = stif_sin(z[ot][r]);
+      for (int r = 0; r < 16; ++r) x0[ot][r] = stif_sin(z[ot][r] * ACC_S<F16>);
     }
   }
   lds_dma_barrier();
@@ -438,13 +501,17 @@ __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DE
   };
   seg_l23_first(B0);
   f32x16 x1[2];
+  {
+    const XT<F16> xs[2] = {xop<F16>(x0[0]), xop<F16>(x0[1])};
 #pragma unroll
-  for (int ot = 0; ot < 2; ++ot) {
-    f32x16 acc = f32x16{0};
+    for (int ot = 0; ot < 2; ++ot) {
+      f32x16 acc = f32x16{0};
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) tile_mma(acc, B1 + (ot * 2 + kt) * T, x0[kt], lane);
-    x1[ot] = bias_sin(acc, mlp + E_B1 + ot * 32, hf);
+      for (int kt = 0; kt < 2; ++kt) tile_mma<F16>(acc, B1 + (ot * 2 + kt) * T, xs[kt], lane);
+      x1[ot] = bias_sin<F16>(acc, mlp + E_B1 + ot * 32, hf);
+    }
   }
+  const XT<F16> x1s[2] = {xop<F16>(x1[0]), xop<F16>(x1[1])};
   // layer 2 (64 -> 256, sine) streamed tile by tile into the 8 accumulators of layer 3 (256 -> 256):
   // segment kt = W2 rows of tile kt (2 tiles) + column kt of W3 (8 tiles)
   auto seg_l23 = [&](float* dst, int kt) {
@@ -463,11 +530,11 @@ __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DE
     if (kt < 7) seg_l23(nxt, kt + 1);
     else dma_tiles<DEC2_NW>(nxt, rm, E_W4V, 1, wv, lane);
     f32x16 acc = f32x16{0};
-    tile_mma(acc, cur, x1[0], lane);
-    tile_mma(acc, cur + T, x1[1], lane);
-    const f32x16 h2 = bias_sin(acc, mlp + E_B2 + kt * 32, hf);
+    tile_mma<F16>(acc, cur, x1s[0], lane);
+    tile_mma<F16>(acc, cur + T, x1s[1], lane);
+    const XT<F16> h2 = xop<F16>(bias_sin<F16>(acc, mlp + E_B2 + kt * 32, hf));
 #pragma unroll
-    for (int ot = 0; ot < 8; ++ot) tile_mma(a3[ot], cur + (2 + ot) * T, h2, lane);
+    for (int ot = 0; ot < 8; ++ot) tile_mma<F16>(a3[ot], cur + (2 + ot) * T, h2, lane);
   }
   // layer 3 sine streamed into layer 4 (256 -> 3, linear, VALU dot products); W4 sits in B0 as
   // plain rows (kt = 7 prefetch)
@@ -475,7 +542,7 @@ __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DE
   float o4[3] = {0.f, 0.f, 0.f};
 #pragma unroll
   for (int kt = 0; kt < 8; ++kt) {
-    const f32x16 h3 = bias_sin(a3[kt], mlp + E_B3 + kt * 32, hf);
+    const f32x16 h3 = bias_sin<F16>(a3[kt], mlp + E_B3 + kt * 32, hf);
     narrow_dot<3>(o4, B0, kt, h3, hf);
   }
 #pragma unroll
@@ -553,18 +620,23 @@ bool image_ok(const stif_dec_image* im) {
 }
 
 template <int MODE, bool HRIMG>
-void launch_dec1(long long blocks, hipStream_t st, const float* proj, const float* mlp, const stif_dec_tables& tb,
-                 const stif_dec_image& im, const float* t, float* hrfeat, float* flow, int n, int h, int w, int HH,
-                 int WW) {
-  hipLaunchKernelGGL((k_dec1<MODE, HRIMG>), dim3((unsigned)blocks), dim3(DEC_NW * 64), 0, st, proj, mlp, tb, im, t,
-                     hrfeat, flow, n, h, w, HH, WW);
+void launch_dec1(bool f16, long long blocks, hipStream_t st, const float* proj, const float* mlp,
+                 const stif_dec_tables& tb, const stif_dec_image& im, const float* t, float* hrfeat, float* flow, int n,
+                 int h, int w, int HH, int WW) {
+  if (f16)
+    hipLaunchKernelGGL((k_dec1<MODE, HRIMG, 1>), dim3((unsigned)blocks), dim3(DEC_NW * 64), 0, st, proj, mlp, tb, im,
+                       t, hrfeat, flow, n, h, w, HH, WW);
+  else
+    hipLaunchKernelGGL((k_dec1<MODE, HRIMG, 0>), dim3((unsigned)blocks), dim3(DEC_NW * 64), 0, st, proj, mlp, tb, im,
+                       t, hrfeat, flow, n, h, w, HH, WW);
 }
 
 }  // namespace
 
-extern "C" int stif_dec_stage1(const float* proj, const float* mlp, const stif_dec_tables* tab,
-                               const stif_dec_image* img, const float* t, float* hrfeat, float* flow, int n, int h,
-                               int w, int HH, int WW, void* stream) {
+extern "C" int stif_dec_stage1_ex(const float* proj, const float* mlp, const stif_dec_tables* tab,
+                                  const stif_dec_image* img, const float* t, float* hrfeat, float* flow, int n, int h,
+                                  int w, int HH, int WW, int flags, void* stream) {
+  const bool f16 = flags & STIF_CONV_F16X3;
   if (!proj || !mlp || !tables_ok(tab) || !image_ok(img) || !t || !hrfeat || !flow || n < 1 || h < 1 || w < 1 ||
       HH < 2 || WW < 2 || (!tab->hr_y) != (!tab->hr_x))
     return stif_fail(STIF_E_INVALID, "stif_dec_stage1: bad arguments");
@@ -573,33 +645,46 @@ extern "C" int stif_dec_stage1(const float* proj, const float* mlp, const stif_d
   hipStream_t st = (hipStream_t)stream;
   const stif_dec_image im = img ? *img : stif_dec_image{};
   if (tab->hr_y) {   // remapped HRfeat operand: the whole HRfeat map first, then the flow stage
-    launch_dec1<1, false>(blocks, st, proj, mlp, *tab, im, t, hrfeat, flow, n, h, w, HH, WW);
-    if (img) launch_dec1<2, true>(blocks, st, proj, mlp, *tab, im, t, hrfeat, flow, n, h, w, HH, WW);
-    else launch_dec1<2, false>(blocks, st, proj, mlp, *tab, im, t, hrfeat, flow, n, h, w, HH, WW);
+    launch_dec1<1, false>(f16, blocks, st, proj, mlp, *tab, im, t, hrfeat, flow, n, h, w, HH, WW);
+    if (img) launch_dec1<2, true>(f16, blocks, st, proj, mlp, *tab, im, t, hrfeat, flow, n, h, w, HH, WW);
+    else launch_dec1<2, false>(f16, blocks, st, proj, mlp, *tab, im, t, hrfeat, flow, n, h, w, HH, WW);
   } else if (img) {
-    launch_dec1<0, true>(blocks, st, proj, mlp, *tab, im, t, hrfeat, flow, n, h, w, HH, WW);
+    launch_dec1<0, true>(f16, blocks, st, proj, mlp, *tab, im, t, hrfeat, flow, n, h, w, HH, WW);
   } else {
-    launch_dec1<0, false>(blocks, st, proj, mlp, *tab, im, t, hrfeat, flow, n, h, w, HH, WW);
+    launch_dec1<0, false>(f16, blocks, st, proj, mlp, *tab, im, t, hrfeat, flow, n, h, w, HH, WW);
   }
   return stif_check_launch("stif_dec_stage1");
 }
 
-extern "C" int stif_dec_stage2(const float* proj, const float* mlp, const float* hrfeat, const float* flow,
-                               const stif_dec_tables* tab, const stif_dec_image* img, const float* t, float* out, int n,
-                               int h, int w, int HH, int WW, void* stream) {
+extern "C" int stif_dec_stage1(const float* proj, const float* mlp, const stif_dec_tables* tab,
+                               const stif_dec_image* img, const float* t, float* hrfeat, float* flow, int n, int h,
+                               int w, int HH, int WW, void* stream) {
+  return stif_dec_stage1_ex(proj, mlp, tab, img, t, hrfeat, flow, n, h, w, HH, WW, 0, stream);
+}
+
+extern "C" int stif_dec_stage2_ex(const float* proj, const float* mlp, const float* hrfeat, const float* flow,
+                                  const stif_dec_tables* tab, const stif_dec_image* img, const float* t, float* out,
+                                  int n, int h, int w, int HH, int WW, int flags, void* stream) {
+  const bool f16 = flags & STIF_CONV_F16X3;
   if (!proj || !mlp || !hrfeat || !flow || !tables_ok(tab) || !image_ok(img) || !t || !out || n < 1 || h < 1 ||
       w < 1 || HH < 2 || WW < 2)
     return stif_fail(STIF_E_INVALID, "stif_dec_stage2: bad arguments");
   const long long total = (long long)n * HH * WW;
   const long long blocks = (total + DEC2_NW * 32 - 1) / (DEC2_NW * 32);
   const stif_dec_image im = img ? *img : stif_dec_image{};
-  if (img)
-    hipLaunchKernelGGL((k_dec2<true>), dim3((unsigned)blocks), dim3(DEC2_NW * 64), 0, (hipStream_t)stream, proj, mlp,
-                       hrfeat, flow, *tab, im, t, out, n, h, w, HH, WW);
-  else
-    hipLaunchKernelGGL((k_dec2<false>), dim3((unsigned)blocks), dim3(DEC2_NW * 64), 0, (hipStream_t)stream, proj,
-                       mlp, hrfeat, flow, *tab, im, t, out, n, h, w, HH, WW);
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 g((unsigned)blocks), b(DEC2_NW * 64);
+  if (img && f16) hipLaunchKernelGGL((k_dec2<true, 1>), g, b, 0, st, proj, mlp, hrfeat, flow, *tab, im, t, out, n, h, w, HH, WW);
+  else if (img) hipLaunchKernelGGL((k_dec2<true, 0>), g, b, 0, st, proj, mlp, hrfeat, flow, *tab, im, t, out, n, h, w, HH, WW);
+  else if (f16) hipLaunchKernelGGL((k_dec2<false, 1>), g, b, 0, st, proj, mlp, hrfeat, flow, *tab, im, t, out, n, h, w, HH, WW);
+  else hipLaunchKernelGGL((k_dec2<false, 0>), g, b, 0, st, proj, mlp, hrfeat, flow, *tab, im, t, out, n, h, w, HH, WW);
   return stif_check_launch("stif_dec_stage2");
+}
+
+extern "C" int stif_dec_stage2(const float* proj, const float* mlp, const float* hrfeat, const float* flow,
+                               const stif_dec_tables* tab, const stif_dec_image* img, const float* t, float* out, int n,
+                               int h, int w, int HH, int WW, void* stream) {
+  return stif_dec_stage2_ex(proj, mlp, hrfeat, flow, tab, img, t, out, n, h, w, HH, WW, 0, stream);
 }
 
 extern "C" int stif_dec_blend4(const float* const* pred, const float* const* wgt, float* out, int n, int HH, int WW,

@@ -303,8 +303,28 @@ extern "C" size_t stif_dec_mlp_floats(void) { return stif_dec::MLP_FLOATS; }
 
 
 
-extern "C" int stif_pack_dec_mlp(const float* const* f, const float* const* l, const float* const* e,
-                                 float* d) {
+namespace {
+// fp32 tile [v][lane][4] -> split-fp16 tile [m][plane][lane][8 halves] in place (x 2^10): element
+// (m, e) of a lane = fp32 element (v = 2m + (e >> 2), e & 3), i.e. feature F(8m + e, lane >> 5)
+void tile_to_f16x3(float* t) {
+  std::vector<float> src(t, t + stif_dec::T);
+  _Float16* dst = reinterpret_cast<_Float16*>(t);
+  for (int m = 0; m < 2; ++m)
+    for (int l = 0; l < 64; ++l)
+      for (int e = 0; e < 8; ++e) {
+        const double x = src[((2 * m + (e >> 2)) * 64 + l) * 4 + (e & 3)];
+        const size_t o = ((size_t)(2 * m) * 64 + l) * 8 + e;
+        split_f16x3_host(x, dst + o, dst + o + 512);
+      }
+}
+}  // namespace
+
+extern "C" int stif_pack_dec_mlp(const float* const* f, const float* const* l, const float* const* e, float* d) {
+  return stif_pack_dec_mlp_ex(f, l, e, d, 0);
+}
+
+extern "C" int stif_pack_dec_mlp_ex(const float* const* f, const float* const* l, const float* const* e, float* d,
+                                    int flags) {
   using namespace stif_dec;
   if (!f || !l || !e || !d) return stif_fail(STIF_E_INVALID, "stif_pack_dec_mlp: null");
   for (int i = 0; i < 8; ++i)
@@ -375,5 +395,13 @@ extern "C" int stif_pack_dec_mlp(const float* const* f, const float* const* l, c
   // plain last layers for the VALU dot products
   memcpy(d + L_W3V, l[6], sizeof(float) * 4 * 256);
   memcpy(d + E_W4V, e[8], sizeof(float) * 3 * 256);
+  if (flags & STIF_CONV_F16X3) {
+    // every MFMA weight tile split; the fp32 image tiles (img_mma) scaled to the accumulators' 2^14
+    const int regions[][2] = {{F_W1, 4}, {F_W2, 16}, {F_W3, 16}, {L_W0, 4}, {L_W1, 4}, {L_W2, 16}, {L_W3, 8},
+                              {E_W0, 8}, {E_W1, 4}, {E_W2, 16}, {E_W3, 64}, {E_W4, 8}};
+    for (const auto& r : regions)
+      for (int k = 0; k < r[1]; ++k) tile_to_f16x3(d + r[0] + k * T);
+    for (int i = I_L; i < I_END; ++i) d[i] *= 16384.f;
+  }
   return STIF_OK;
 }

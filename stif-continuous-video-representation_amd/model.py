@@ -59,6 +59,7 @@ class LunaTokis:
         if mfma not in ("f32", "f16x3"):
             raise ValueError("mfma must be 'f32' or 'f16x3'")
         self.mfma = mfma
+        self._dec_flags = L.CONV_F16X3 if mfma == "f16x3" else 0   # decoder SIREN layers likewise
 
     # ------------------------------------------------------------------ nn.Module-like API
     def eval(self):
@@ -181,7 +182,7 @@ class LunaTokis:
         la, lp = siren_ptrs("flow_imnet.", 3)
         ea, ep = siren_ptrs("encode_imnet.", 4)
         mlp = np.empty(lib.stif_dec_mlp_floats(), np.float32)
-        L.check(lib.stif_pack_dec_mlp(fp, lp, ep, mlp.ctypes.data), "stif_pack_dec_mlp")
+        L.check(lib.stif_pack_dec_mlp_ex(fp, lp, ep, mlp.ctypes.data, self._dec_flags), "stif_pack_dec_mlp_ex")
         lay["dec.mlp"] = torch.from_numpy(mlp).to(dev)
         self.layers = lay
 
@@ -463,9 +464,9 @@ class LunaTokis:
         flow = self._empty(B, HH, WW, 4)
         for tq in times:
             t = self._time_vec(tq, B)
-            ops.dec_stage1(proj, mlp, tab, t, hrf, flow, image)
+            ops.dec_stage1(proj, mlp, tab, t, hrf, flow, image, flags=self._dec_flags)
             out = self._empty(B, 3, HH, WW)
-            ops.dec_stage2(proj, mlp, hrf, flow, tab, t, out, image)
+            ops.dec_stage2(proj, mlp, hrf, flow, tab, t, out, image, flags=self._dec_flags)
             preds.append(out)
         return preds
 

@@ -251,26 +251,27 @@ def dec_pack_lr(f0, f1, f2, x, out):
             "stif_dec_pack_lr")
 
 
-def dec_stage1(proj, mlp, tables: DecTablesDev, t, hrfeat, flow, image: "DecImageDev" = None):
+def dec_stage1(proj, mlp, tables: DecTablesDev, t, hrfeat, flow, image: "DecImageDev" = None, flags=0):
     n, h, w, _ = proj.shape
     HH, WW = hrfeat.shape[1:3]
     tr = TRACE
     if tr is not None:   # per HR px: feat_imnet layers 1-3 (36,864 MAC) + flow_imnet HRfeat/1-3 (25,600 MAC)
         tr.begin(("dec1",), 2.0 * 62464 * n * HH * WW)
-    L.check(L.lib().stif_dec_stage1(_vp(proj), _vp(mlp), C.byref(tables.c), C.byref(image.c) if image else None,
-                                    _vp(t), _vp(hrfeat), _vp(flow), n, h, w, HH, WW, _stream()), "stif_dec_stage1")
+    L.check(L.lib().stif_dec_stage1_ex(_vp(proj), _vp(mlp), C.byref(tables.c), C.byref(image.c) if image else None,
+                                       _vp(t), _vp(hrfeat), _vp(flow), n, h, w, HH, WW, flags, _stream()),
+            "stif_dec_stage1")
     if tr is not None:
         tr.end()
 
 
-def dec_stage2(proj, mlp, hrfeat, flow, tables: DecTablesDev, t, out, image: "DecImageDev" = None):
+def dec_stage2(proj, mlp, hrfeat, flow, tables: DecTablesDev, t, out, image: "DecImageDev" = None, flags=0):
     n, h, w, _ = proj.shape
     HH, WW = hrfeat.shape[1:3]
     tr = TRACE
     if tr is not None:   # per HR px: encode_imnet HRfeat part + layers 1-4 (94,976 MAC)
         tr.begin(("dec2",), 2.0 * 94976 * n * HH * WW)
-    L.check(L.lib().stif_dec_stage2(_vp(proj), _vp(mlp), _vp(hrfeat), _vp(flow), C.byref(tables.c),
-                                    C.byref(image.c) if image else None, _vp(t), _vp(out), n, h, w, HH, WW,
-                                    _stream()), "stif_dec_stage2")
+    L.check(L.lib().stif_dec_stage2_ex(_vp(proj), _vp(mlp), _vp(hrfeat), _vp(flow), C.byref(tables.c),
+                                       C.byref(image.c) if image else None, _vp(t), _vp(out), n, h, w, HH, WW, flags,
+                                       _stream()), "stif_dec_stage2")
     if tr is not None:
         tr.end()
