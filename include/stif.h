@@ -234,7 +234,7 @@ size_t stif_conv_bias_floats(int cout, int mode);
  * input channel 16 q + 8 (e >> 2) + 4 (l >> 5) + (e & 3) (the chunk pair of one f16 MFMA).
  * STIF_PACK_PLAIN | STIF_PACK_F16X3 (64 -> 64 3x3 only: the stif_dcn_nhwc core with
  * flags = STIF_CONV_F16X3): [group 8][tap pair 5][nt 2][plane h|l][lane 64][8 halves], element e
- * of lane l holding tap 2p + (e >> 2) (tap 9 = 0), input channel 8 group + 4 (l >> 5) + (e & 3). */
+ * of lane l holding tap 2p + (l >> 5) (tap 9 = 0), input channel 8 group + e. */
 int stif_pack_conv_weight(const float* w_oihw, const float* b, int cout, int cin, int ks, int mode,
                           float* w_dst, float* b_dst);
 

@@ -42,9 +42,10 @@ STIF_DEV f32x4 dcn_sample4(const float* __restrict__ img, int H, int W, float h,
 // samples its own MFMA A-fragment (pixel = lane & 31, channels 4h..4h+3) tap by tap from the
 // tile -- falling back to global loads only when an offset leaves the margin -- so sampling
 // (VALU + LDS) interleaves with the MFMAs and no sampled A tile ever round-trips memory.
-// F16: the contraction on split-fp16 MFMA (stif_common.h split_f16x3): two taps per 32x32x16 MFMA
-// (lane half h: channels 4h..4h+3 of tap 2p at elements 0..3, of tap 2p + 1 at 4..7; tap 9 = 0),
-// weights packed STIF_PACK_PLAIN | STIF_PACK_F16X3 ([group][pair][nt][plane][lane][8 halves]).
+// F16: the contraction on split-fp16 MFMA (stif_common.h split_f16x3): two taps per 32x32x16 MFMA,
+// lane half h sampling tap 2p + h (tap 9 = 0) for all 8 channels of the group (elements 0..7), so
+// each (pixel, tap) computes its bilinear weights once; weights packed STIF_PACK_PLAIN |
+// STIF_PACK_F16X3 ([group][pair][nt][plane][lane][8 halves]).
 template <int EPI, int F16>
 __global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
   constexpr int NW = 4, TH = 4, M = 4;
@@ -90,28 +91,84 @@ __global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
     for (int i = wv; i < W_F / 256; i += NW)
       __builtin_amdgcn_global_load_lds(wc + (i * 64 + lane) * 4, sw + i * 256, 16, 0, 0);
   };
-  float omc[27], omn[27];
+  // offset/mask values of a group: all 27 (fp32 path), or (F16) the 5 taps 2p + h of this lane half
+  // as [p][dy, dx, m] (tap 9 reads tap 8's values and is masked off)
+  constexpr int NOM = F16 ? 15 : 27;
+  auto om_load = [&](int dgi, float* o) {
 #pragma unroll
-  for (int k = 0; k < 27; ++k) omc[k] = omp[k];
+    for (int k = 0; k < NOM; ++k) {
+#ifdef DCN_EXP_NOOM
+      o[k] = 0.5f * k;
+#else
+      if constexpr (F16) o[k] = omp[dgi * 27 + min(2 * (k / 3) + hf, 8) * 3 + k % 3];
+      else o[k] = omp[dgi * 27 + k];
+#endif
+    }
+  };
+  float omc[NOM], omn[NOM];
+  om_load(0, omc);
 
   f32x16 acc0 = f32x16{0}, acc1 = f32x16{0};
-  f32x4 avp = f32x4{0.f, 0.f, 0.f, 0.f};   // F16: the even tap of the current pair
   stage(0, 0);
   lds_dma_barrier();
   for (int dg = 0; dg < 8; ++dg) {
     if (dg + 1 < 8) {
       stage(dg + 1, (dg + 1) & 1);
-#pragma unroll
-      for (int k = 0; k < 27; ++k) {
-#ifdef DCN_EXP_NOOM
-        omn[k] = omc[k] + 0.5f;
-#else
-        omn[k] = omp[(dg + 1) * 27 + k];
-#endif
-      }
+      om_load(dg + 1, omn);
     }
     const float* st = smem + (dg & 1) * BUF_F;
     const float* sw = st + T_F;
+    if constexpr (F16) {
+      // tap pair p: lane half h samples tap 2p + h for all 8 channels of the group -- one bilinear
+      // weight set per (pixel, tap) -- and supplies them as the 8 K values of its MFMA A operand
+#pragma unroll
+      for (int pp = 0; pp < 5; ++pp) {
+        const int tap = 2 * pp + hf;
+        const int ky = tap / 3, kx = tap - 3 * ky;
+        const float h_im = (float)(oy - 1 + ky) + omc[pp * 3];
+        const float w_im = (float)(ox - 1 + kx) + omc[pp * 3 + 1];
+        const bool valid =
+            pix_ok & (tap < 9) & (h_im > -1.f) & (w_im > -1.f) & (h_im < (float)H) & (w_im < (float)W);
+        const float fh = floorf(h_im), fw = floorf(w_im);
+        const float lh = h_im - fh, lw = w_im - fw, hh = 1.f - lh, hw = 1.f - lw;
+        const int h_low = (int)fh, w_low = (int)fw;
+        const int r0 = h_low - ty0, c0 = w_low - tx0;
+        const bool in_tile = ((unsigned)r0 < (unsigned)(TR - 1)) & ((unsigned)c0 < (unsigned)(TC - 1));
+        const float m = valid ? omc[pp * 3 + 2] : 0.f;
+        const float hm = hh * m, lm = lh * m;
+        const float w1 = hm * hw, w2 = hm * lw, w3 = lm * hw, w4 = lm * lw;
+        const float* p0 = st + (((in_tile ? r0 : 0) * 2) * TC + (in_tile ? c0 : 0)) * 4;   // channels 0-3
+        const float* p1 = p0 + 2 * TC * 4;                                                 // next row
+        f32x4 a0 = w1 * ld4(p0) + w2 * ld4(p0 + 4) + w3 * ld4(p1) + w4 * ld4(p1 + 4);
+        f32x4 a1 = w1 * ld4(p0 + TC * 4) + w2 * ld4(p0 + TC * 4 + 4) + w3 * ld4(p1 + TC * 4) + w4 * ld4(p1 + TC * 4 + 4);
+        const bool fb = valid & !in_tile;
+        if (__builtin_amdgcn_ballot_w64(fb)) {
+          if (fb) {
+            const int h_high = h_low + 1, w_high = w_low + 1, co = dg * 8;
+            const bool b1 = h_low >= 0 && w_low >= 0, b2 = h_low >= 0 && w_high <= W - 1;
+            const bool b3 = h_high <= H - 1 && w_low >= 0, b4 = h_high <= H - 1 && w_high <= W - 1;
+            const float* q1 = in + ((size_t)h_low * W + w_low) * 64 + co;
+            const float* q2 = in + ((size_t)h_low * W + w_high) * 64 + co;
+            const float* q3 = in + ((size_t)h_high * W + w_low) * 64 + co;
+            const float* q4 = in + ((size_t)h_high * W + w_high) * 64 + co;
+            const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+            a0 = w1 * (b1 ? ld4(q1) : z) + w2 * (b2 ? ld4(q2) : z) + w3 * (b3 ? ld4(q3) : z) + w4 * (b4 ? ld4(q4) : z);
+            a1 = w1 * (b1 ? ld4(q1 + 4) : z) + w2 * (b2 ? ld4(q2 + 4) : z) + w3 * (b3 ? ld4(q3 + 4) : z) +
+                 w4 * (b4 ? ld4(q4 + 4) : z);
+          }
+        }
+        f16x8 ah, al;
+        split_f16x3(a0, a1, ah, al);
+        const float* wp = sw + pp * 1024 + lane * 4;   // [pair][nt][plane][lane][8 halves]
+        const f16x8 bh0 = ldh8(wp), bl0 = ldh8(wp + 256), bh1 = ldh8(wp + 512), bl1 = ldh8(wp + 768);
+        acc0 = mfma16h(ah, bh0, acc0);
+        acc1 = mfma16h(ah, bh1, acc1);
+        acc0 = mfma16h(ah, bl0, acc0);
+        acc1 = mfma16h(ah, bl1, acc1);
+        acc0 = mfma16h(al, bh0, acc0);
+        acc1 = mfma16h(al, bh1, acc1);
+      }
+    } else {
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       // modulated_deformable_im2col (dcn_v2_im2col_cuda.cu:158-192) for this lane's pixel / tap.
@@ -148,35 +205,18 @@ __global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
           av = w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4;
         }
       }
-      if constexpr (F16) {
-        if ((tap & 1) == 0 && tap < 8) {
-          avp = av;
-        } else {
-          f16x8 ah, al;
-          if (tap == 8) split_f16x3(av, f32x4{0.f, 0.f, 0.f, 0.f}, ah, al);
-          else split_f16x3(avp, av, ah, al);
-          const float* wp = sw + (tap >> 1) * 1024 + lane * 4;   // [pair][nt][plane][lane][8 halves]
-          const f16x8 bh0 = ldh8(wp), bl0 = ldh8(wp + 256), bh1 = ldh8(wp + 512), bl1 = ldh8(wp + 768);
-          acc0 = mfma16h(ah, bh0, acc0);
-          acc1 = mfma16h(ah, bh1, acc1);
-          acc0 = mfma16h(ah, bl0, acc0);
-          acc1 = mfma16h(ah, bl1, acc1);
-          acc0 = mfma16h(al, bh0, acc0);
-          acc1 = mfma16h(al, bh1, acc1);
-        }
-      } else {
-        const f32x4 b0 = ld4(sw + ((tap * 2 + 0) * 64 + lane) * 4);
-        const f32x4 b1 = ld4(sw + ((tap * 2 + 1) * 64 + lane) * 4);
+      const f32x4 b0 = ld4(sw + ((tap * 2 + 0) * 64 + lane) * 4);
+      const f32x4 b1 = ld4(sw + ((tap * 2 + 1) * 64 + lane) * 4);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          acc0 = mfma32(av[q], b0[q], acc0);
-          acc1 = mfma32(av[q], b1[q], acc1);
-        }
+      for (int q = 0; q < 4; ++q) {
+        acc0 = mfma32(av[q], b0[q], acc0);
+        acc1 = mfma32(av[q], b1[q], acc1);
       }
+    }
     }
     if (dg + 1 < 8) {
 #pragma unroll
-      for (int k = 0; k < 27; ++k) omc[k] = omn[k];
+      for (int k = 0; k < NOM; ++k) omc[k] = omn[k];
     }
     lds_dma_barrier();
   }

@@ -148,8 +148,8 @@ void split_f16x3_host(double x, _Float16* h, _Float16* l) {
 }
 
 // PLAIN | F16X3, the fused DCN core (k_dcn<F16>): [group][tap pair p][nt][plane][lane][8 halves];
-// element e of lane l holds tap 2p + (e >> 2) (tap 9 = zero padding), input channel
-// 8 group + 4 (l >> 5) + (e & 3), cout nt * 32 + (l & 31)
+// element e of lane l holds tap 2p + (l >> 5) (tap 9 = zero padding), input channel 8 group + e,
+// cout nt * 32 + (l & 31)
 int pack_dcn_f16x3(const float* w, const float* b, int cout, int cin, float* w_dst, float* b_dst) {
   _Float16* dst = reinterpret_cast<_Float16*>(w_dst);
   for (int g = 0; g < cin / 8; ++g)
@@ -157,7 +157,7 @@ int pack_dcn_f16x3(const float* w, const float* b, int cout, int cin, float* w_d
       for (int nt = 0; nt < 2; ++nt)
         for (int l = 0; l < 64; ++l)
           for (int e = 0; e < 8; ++e) {
-            const int tap = 2 * p + (e >> 2), ci = 8 * g + 4 * (l >> 5) + (e & 3), co = nt * 32 + (l & 31);
+            const int tap = 2 * p + (l >> 5), ci = 8 * g + e, co = nt * 32 + (l & 31);
             const double x = tap < 9 ? (double)w[((size_t)co * cin + ci) * 9 + tap] : 0.0;
             const size_t o = ((((size_t)g * 5 + p) * 2 + nt) * 2) * 512 + l * 8 + e;
             split_f16x3_host(x, dst + o, dst + o + 512);
