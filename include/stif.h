@@ -232,8 +232,8 @@ size_t stif_conv_bias_floats(int cout, int mode);
  * STIF_PACK_WINO* | STIF_PACK_F16X3: U * 2^10 split into fp16 h = rne(U 2^10), l = rne(U 2^10 - h)
  * as [cout/64][cin/16][i 4][j 4][nt 2][plane h|l][lane 64][8 halves], lane l's element e holding
  * input channel 16 q + 8 (e >> 2) + 4 (l >> 5) + (e & 3) (the chunk pair of one f16 MFMA).
- * STIF_PACK_PLAIN | STIF_PACK_F16X3 (64 -> 64 3x3 only: the stif_dcn_nhwc core with
- * flags = STIF_CONV_F16X3): [group 8][tap pair 5][nt 2][plane h|l][lane 64][8 halves], element e
+ * STIF_PACK_PLAIN | STIF_PACK_F16X3 (64 -> 64 3x3 only: the stif_dcn_nhwc core, and the 3x3
+ * stride-2 convs of stif_conv2d_nhwc, with flags = STIF_CONV_F16X3): [group 8][tap pair 5][nt 2][plane h|l][lane 64][8 halves], element e
  * of lane l holding tap 2p + (l >> 5) (tap 9 = 0), input channel 8 group + e. */
 int stif_pack_conv_weight(const float* w_oihw, const float* b, int cout, int cin, int ks, int mode,
                           float* w_dst, float* b_dst);

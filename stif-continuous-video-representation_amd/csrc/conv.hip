@@ -21,7 +21,10 @@
 
 namespace {
 
-template <int KS, int S, int MT, int NT, int NW, int IN1, int EPI>
+// F16 (the 3x3 64 -> 64 convs with weights packed STIF_PACK_PLAIN | STIF_PACK_F16X3, as the DCN
+// core): split-fp16 MFMA with two taps per 32x32x16 MFMA, lane half h supplying tap 2p + h for the
+// chunk's 8 channels (tap 9 = zero weights).
+template <int KS, int S, int MT, int NT, int NW, int IN1, int EPI, int F16 = 0>
 __global__ __launch_bounds__(NW * 64) void k_conv(stif_conv_args a) {
   constexpr int TH = NW * MT;              // output rows per workgroup
   constexpr int HR = (TH - 1) * S + KS;    // halo rows
@@ -35,7 +38,8 @@ __global__ __launch_bounds__(NW * 64) void k_conv(stif_conv_args a) {
   constexpr int IN_EL = HR * 2 * HC;
   constexpr int IN_INST = (IN_EL + 63) / 64;
   constexpr int IN_F = IN_INST * 256;
-  constexpr int W_EL = T2 * NT * 64;       // weight fragments per chunk: [tap][nt][lane][4]
+  constexpr int W_EL = F16 ? 5 * NT * 2 * 64 : T2 * NT * 64;   // weight fragments per chunk: [tap][nt][lane][4]
+  static_assert(!F16 || (KS == 3 && IN1 == 0 && EPI != STIF_EPI_LSTM), "F16: 3x3 single-input convs");
   constexpr int W_F = W_EL * 4;
   constexpr int BUF_F = IN_F + W_F;
   constexpr int SM_F = (2 * BUF_F > NW * 1024) ? 2 * BUF_F : NW * 1024;
@@ -151,6 +155,31 @@ __global__ __launch_bounds__(NW * 64) void k_conv(stif_conv_args a) {
     }
     const float* si = smem + (c & 1) * BUF_F;
     const float* sw = si + IN_F;
+    if constexpr (F16) {
+#pragma unroll
+      for (int pp = 0; pp < 5; ++pp) {
+        const int tap = min(2 * pp + hf, 8);   // tap 9: any finite operand, its weights are zero
+        const int ky = tap / 3, kx = tap - 3 * ky;
+        f16x8 ah[MT], al[MT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const int oy = wv * MT + mt;
+          const float* pa = si + (((oy * S + ky) * 2) * HC + l32 * S + kx) * 4;
+          split_f16x3(ld4(pa), ld4(pa + HC * 4), ah[mt], al[mt]);
+        }
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const float* wp = sw + (pp * NT + nt) * 512 + lane * 4;   // [pair][nt][plane][lane][8 halves]
+          const f16x8 bh = ldh8(wp), bl = ldh8(wp + 256);
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            acc[mt][nt] = mfma16h(ah[mt], bh, acc[mt][nt]);
+            acc[mt][nt] = mfma16h(ah[mt], bl, acc[mt][nt]);
+            acc[mt][nt] = mfma16h(al[mt], bh, acc[mt][nt]);
+          }
+        }
+      }
+    } else
 #pragma unroll
     for (int tap = 0; tap < T2; ++tap) {
       const int ky = tap / KS, kx = tap % KS;
@@ -229,7 +258,7 @@ __global__ __launch_bounds__(NW * 64) void k_conv(stif_conv_args a) {
         f32x16 v;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float t = acc[mt][nt][r] + bv;
+          float t = acc[mt][nt][r] * (F16 ? F16X3_UNSCALE : 1.f) + bv;
           if (EPI == STIF_EPI_LRELU) t = lrelu01(t);
           if (EPI == STIF_EPI_RELU) t = fmaxf(t, 0.f);
           if (EPI == STIF_EPI_OFFMASK) {
@@ -259,13 +288,13 @@ __global__ __launch_bounds__(NW * 64) void k_conv(stif_conv_args a) {
   }
 }
 
-template <int KS, int S, int MT, int NT, int NW, int IN1, int EPI>
+template <int KS, int S, int MT, int NT, int NW, int IN1, int EPI, int F16 = 0>
 int launch(const stif_conv_args& a, hipStream_t st) {
   constexpr int TH = NW * MT;
   const int tiles = ((a.Wo + 31) / 32) * ((a.Ho + TH - 1) / TH);
   const int slices = ((a.cout + 31) / 32 + NT - 1) / NT;
   dim3 grid(tiles, slices, a.ngroups * a.nitems);
-  hipLaunchKernelGGL((k_conv<KS, S, MT, NT, NW, IN1, EPI>), grid, dim3(NW * 64), 0, st, a);
+  hipLaunchKernelGGL((k_conv<KS, S, MT, NT, NW, IN1, EPI, F16>), grid, dim3(NW * 64), 0, st, a);
   return stif_check_launch("stif_conv2d_nhwc");
 }
 
@@ -325,7 +354,9 @@ extern "C" int stif_conv2d_nhwc(const stif_conv_args* pa, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (a.ngroups < 1 || a.ngroups > STIF_MAX_GROUPS || a.nitems < 1)
     return stif_fail(STIF_E_INVALID, "stif_conv2d_nhwc: bad ngroups/nitems");
-  if (a.flags & STIF_CONV_F16X3) return stif_fail(STIF_E_INVALID, "stif_conv2d_nhwc: STIF_CONV_F16X3 is a Winograd-only mode");
+  const bool f16 = a.flags & STIF_CONV_F16X3;
+  if (f16 && !(a.ks == 3 && a.stride == 2 && a.cout == 64 && a.C0 == 64 && a.in1_mode == 0))
+    return stif_fail(STIF_E_INVALID, "stif_conv2d_nhwc: STIF_CONV_F16X3 takes the 3x3 stride-2 64 -> 64 convs only");
   if (a.C0 % 8 || a.C0 <= 0 || (a.in1_mode && (a.C1 % 8 || a.C1 <= 0)))
     return stif_fail(STIF_E_INVALID, "stif_conv2d_nhwc: channel counts must be multiples of 8");
   const int pad = a.ks / 2;
@@ -349,8 +380,10 @@ extern "C" int stif_conv2d_nhwc(const stif_conv_args* pa, void* stream) {
   if (a.ks == 3 && a.stride == 2) {
     if (a.in1_mode != 0) return stif_fail(STIF_E_INVALID, "strided conv takes one input");
     switch (a.epi) {
-      case STIF_EPI_LRELU: return launch<3, 2, 1, 2, 4, 0, STIF_EPI_LRELU>(a, st);
-      case STIF_EPI_NONE: return launch<3, 2, 1, 2, 4, 0, STIF_EPI_NONE>(a, st);
+      case STIF_EPI_LRELU:
+        return f16 ? launch<3, 2, 1, 2, 4, 0, STIF_EPI_LRELU, 1>(a, st) : launch<3, 2, 1, 2, 4, 0, STIF_EPI_LRELU>(a, st);
+      case STIF_EPI_NONE:
+        return f16 ? launch<3, 2, 1, 2, 4, 0, STIF_EPI_NONE, 1>(a, st) : launch<3, 2, 1, 2, 4, 0, STIF_EPI_NONE>(a, st);
       default: break;
     }
     return stif_fail(STIF_E_INVALID, "strided conv: unsupported epilogue");

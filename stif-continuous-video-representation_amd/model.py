@@ -138,8 +138,8 @@ class LunaTokis:
         for i in range(self.front_RBs):
             conv(f"feature_extraction.{i}.conv1", wino)
             conv(f"feature_extraction.{i}.conv2", wino)
-        for n in ("fea_L2_conv1", "fea_L3_conv1"):
-            conv(n)
+        for n in ("fea_L2_conv1", "fea_L3_conv1"):      # 3x3 stride-2 64 -> 64
+            conv(n, L.PACK_PLAIN | f16)
         for n in ("fea_L2_conv2", "fea_L3_conv2"):
             conv(n, wino)
 
@@ -157,8 +157,9 @@ class LunaTokis:
         conv("fusion")
         conv("ConvBLSTM.forward_net.cell_list.0.conv", (L.PACK_WINO_LSTM | f16) if self.winograd else L.PACK_LSTM)
         for p in ("ConvBLSTM.forward_net.pcd_h.", "ConvBLSTM.forward_net.pcd_c."):
-            for n in ("fea_L2_conv1", "fea_L3_conv1", "fusion"):
-                conv(p + n)
+            for n in ("fea_L2_conv1", "fea_L3_conv1"):
+                conv(p + n, L.PACK_PLAIN | f16)
+            conv(p + "fusion")
             for n in ("fea_L2_conv2", "fea_L3_conv2"):
                 conv(p + n, wino)
             pcd(p + "pcd_align.")

@@ -92,13 +92,24 @@ def test_conv_groups_and_strided_items(ops, L):
     assert relmax(to_nchw(out[1]), refb) < RTOL
 
 
-def test_conv_stride2(ops, L):
-    x = rnd(2, 64, 20, 36, seed=14)
+@pytest.mark.parametrize("f16", [0, 1], ids=["f32", "f16x3"])
+@pytest.mark.parametrize("hw", [(20, 36), (7, 13)])
+def test_conv_stride2(ops, L, f16, hw):
+    H, W = hw
+    x = rnd(2, 64, H, W, seed=14)
     w = rnd(64, 64, 3, 3, seed=15, scale=0.05)
     b = rnd(64, seed=16)
-    out = torch.empty(2, 10, 18, 64, device="cuda")
-    ops.conv2d([dict(layer=ops.pack_conv(w, b), in0=nhwc(x), out=out)], epi=L.EPI_LRELU, stride=2)
+    out = torch.empty(2, (H + 1) // 2, (W + 1) // 2, 64, device="cuda")
+    lay = ops.pack_conv(w, b, L.PACK_PLAIN | (L.PACK_F16X3 if f16 else 0))
+    ops.conv2d([dict(layer=lay, in0=nhwc(x), out=out)], epi=L.EPI_LRELU, stride=2)
     assert relmax(to_nchw(out), O.lrelu(O.conv2d(x, w, b, stride=2))) < RTOL
+
+
+def test_conv_f16x3_rejects_other_shapes(ops, L):
+    lay = ops.pack_conv(rnd(64, 64, 3, 3), rnd(64), L.PACK_PLAIN | L.PACK_F16X3)
+    x = torch.zeros(1, 8, 8, 64, device="cuda")
+    with pytest.raises(Exception):   # stride 1 direct conv has no f16x3 form
+        ops.conv2d([dict(layer=lay, in0=x, out=torch.empty(1, 8, 8, 64, device="cuda"))])
 
 
 def test_conv1x1_wide(ops, L):
