@@ -13,31 +13,28 @@
 namespace {
 
 // one thread = 4 channels of one output pixel
+// grid (x blocks over one output row's W * c/4 float4s, output row y, item): 32-bit index math only
+// (the flat 64-bit div/mod per element dominated the old mapping)
 __global__ __launch_bounds__(256) void k_up2(const float* __restrict__ in, float* __restrict__ out, int n, int h1,
                                              int w1, int c, float scale, long long in_item, long long out_item) {
   const int c4n = c >> 2;
-  const int H = 2 * h1, W = 2 * w1;
-  const long long total = (long long)n * H * W * c4n;
-  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
-    const int q = (int)(e % c4n);
-    long long r = e / c4n;
-    const int x = (int)(r % W);
-    r /= W;
-    const int y = (int)(r % H);
-    const int item = (int)(r / H);
-    // align_corners=False source coordinates (clamped at 0 like ATen's area_pixel_compute_source_index)
-    const float sy = fmaxf(0.5f * ((float)y + 0.5f) - 0.5f, 0.f);
-    const float sx = fmaxf(0.5f * ((float)x + 0.5f) - 0.5f, 0.f);
-    const int y0 = min((int)sy, h1 - 1), x0 = min((int)sx, w1 - 1);
-    const int y1 = y0 + (y0 < h1 - 1 ? 1 : 0), x1 = x0 + (x0 < w1 - 1 ? 1 : 0);
-    const float ly1 = sy - (float)y0, lx1 = sx - (float)x0;
-    const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
-    const float* src = in + (size_t)item * in_item + q * 4;
-    const f32x4 v00 = ld4(src + ((size_t)y0 * w1 + x0) * c), v01 = ld4(src + ((size_t)y0 * w1 + x1) * c);
-    const f32x4 v10 = ld4(src + ((size_t)y1 * w1 + x0) * c), v11 = ld4(src + ((size_t)y1 * w1 + x1) * c);
-    const f32x4 v = (ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11)) * scale;
-    st4(out + (size_t)item * out_item + ((size_t)y * W + x) * c + q * 4, v);
-  }
+  const int W = 2 * w1;
+  const int y = blockIdx.y, item = blockIdx.z;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= W * c4n) return;
+  const int x = t / c4n, q = t - x * c4n;
+  // align_corners=False source coordinates (clamped at 0 like ATen's area_pixel_compute_source_index)
+  const float sy = fmaxf(0.5f * ((float)y + 0.5f) - 0.5f, 0.f);
+  const float sx = fmaxf(0.5f * ((float)x + 0.5f) - 0.5f, 0.f);
+  const int y0 = min((int)sy, h1 - 1), x0 = min((int)sx, w1 - 1);
+  const int y1 = y0 + (y0 < h1 - 1 ? 1 : 0), x1 = x0 + (x0 < w1 - 1 ? 1 : 0);
+  const float ly1 = sy - (float)y0, lx1 = sx - (float)x0;
+  const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
+  const float* src = in + (size_t)item * in_item + q * 4;
+  const f32x4 v00 = ld4(src + ((size_t)y0 * w1 + x0) * c), v01 = ld4(src + ((size_t)y0 * w1 + x1) * c);
+  const f32x4 v10 = ld4(src + ((size_t)y1 * w1 + x0) * c), v11 = ld4(src + ((size_t)y1 * w1 + x1) * c);
+  const f32x4 v = (ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11)) * scale;
+  st4(out + (size_t)item * out_item + ((size_t)y * W + x) * c + q * 4, v);
 }
 
 }  // namespace
@@ -47,10 +44,10 @@ extern "C" int stif_upsample2x_nhwc(const float* in, float* out, int n, int h1, 
   if (!in || !out || n < 1 || h1 < 1 || w1 < 1 || c < 4 || c % 4 || in_item < (long long)h1 * w1 * c ||
       out_item < 4LL * h1 * w1 * c)
     return stif_fail(STIF_E_INVALID, "stif_upsample2x_nhwc: bad arguments");
-  const long long total = (long long)n * 4 * h1 * w1 * (c / 4);
-  const long long blocks = std::min<long long>((total + 255) / 256, 1 << 20);
-  hipLaunchKernelGGL(k_up2, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, in, out, n, h1, w1, c, scale,
-                     in_item, out_item);
+  if (2LL * h1 > 65535 || n > 65535 || 2LL * w1 * (c / 4) > 0x7fffffffLL)
+    return stif_fail(STIF_E_INVALID, "stif_upsample2x_nhwc: image too large for the row grid");
+  const dim3 grid((unsigned)((2 * w1 * (c / 4) + 255) / 256), (unsigned)(2 * h1), (unsigned)n);
+  hipLaunchKernelGGL(k_up2, grid, dim3(256), 0, (hipStream_t)stream, in, out, n, h1, w1, c, scale, in_item, out_item);
   return stif_check_launch("stif_upsample2x_nhwc");
 }
 
