@@ -17,10 +17,7 @@
 
 namespace {
 
-constexpr int OMC = 216;
-#ifndef DCN_F16_WPE
-#define DCN_F16_WPE 3   // k_dcn<F16>: waves per SIMD it is register-budgeted for
-#endif   // offmask channels per pixel: [group][tap][dy, dx, mask]
+constexpr int OMC = 216;   // offmask channels per pixel: [group][tap][dy, dx, mask]
 
 STIF_DEV f32x4 dcn_sample4(const float* __restrict__ img, int H, int W, float h, float w, int coff) {
   // dmcn_im2col_bilinear (dcn_v2_im2col_cuda.cu:25-54) on 4 channels of an NHWC 64-ch map.
@@ -50,17 +47,13 @@ STIF_DEV f32x4 dcn_sample4(const float* __restrict__ img, int H, int W, float h,
 // each (pixel, tap) computes its bilinear weights once; weights packed STIF_PACK_PLAIN |
 // STIF_PACK_F16X3 ([group][pair][nt][plane][lane][8 halves]).
 template <int EPI, int F16>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(F16 ? DCN_F16_WPE : 1))) void k_dcn(
-    stif_dcn_args a) {
+__global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
   constexpr int NW = 4, TH = 4, M = 4;
   constexpr int TR = TH + 2 + 2 * M, TC = 32 + 2 + 2 * M;   // tile rows / cols
   constexpr int T_EL = TR * 2 * TC;                          // 16-B elements
   constexpr int T_INST = (T_EL + 63) / 64;
   constexpr int T_F = T_INST * 256;
-  // packed B fragments of one group: staged in LDS (fp32), or (F16) read by every wave straight from
-  // L2 one tap pair ahead -- no weight staging, 39 KB of LDS per workgroup, 4 workgroups per CU
-  constexpr int W_F = F16 ? 0 : 9 * 2 * 64 * 4;
-  constexpr int WG_F = 5 * 2 * 2 * 256;   // F16: floats per group in global memory
+  constexpr int W_F = F16 ? 5 * 2 * 2 * 256 : 9 * 2 * 64 * 4;   // packed B fragments of one group
   constexpr int BUF_F = T_F + W_F;
   __shared__ __attribute__((aligned(16))) float smem[2 * BUF_F];
 
@@ -95,7 +88,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(F16 ? DCN_F
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, st + i * 256, 16, voff, 0, 0, 0);
     }
     const float* wc = wt + (size_t)dg * W_F;   // packed [chunk][tap][nt][lane][4]
-    if (!F16)
     for (int i = wv; i < W_F / 256; i += NW)
       __builtin_amdgcn_global_load_lds(wc + (i * 64 + lane) * 4, sw + i * 256, 16, 0, 0);
   };
@@ -117,25 +109,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(F16 ? DCN_F
   om_load(0, omc);
 
   f32x16 acc0 = f32x16{0}, acc1 = f32x16{0};
-  // F16: B fragments (h0, l0, h1, l1) of the next tap pair
-  f16x8 nb[4];
-  auto bload = [&](int dgi, int pp) {
-    const float* wp = wt + (size_t)dgi * WG_F + pp * 1024 + lane * 4;   // [pair][nt][plane][lane][8 halves]
-#pragma unroll
-    for (int k = 0; k < 4; ++k) nb[k] = ldh8(wp + k * 256);
-  };
-  if (F16) bload(0, 0);
   stage(0, 0);
   lds_dma_barrier();
   for (int dg = 0; dg < 8; ++dg) {
     if (dg + 1 < 8) {
-      // F16: the offset/mask loads go first, so the only vector-memory ops younger than the DMA are
-      // the 20 B-fragment prefetches of this group's pairs (the end-of-group wait leaves them in flight)
-      if (F16) om_load(dg + 1, omn);
-      asm volatile("" ::: "memory");   // keep the program order of the loads around the DMA
       stage(dg + 1, (dg + 1) & 1);
-      asm volatile("" ::: "memory");
-      if (!F16) om_load(dg + 1, omn);
+      om_load(dg + 1, omn);
     }
     const float* st = smem + (dg & 1) * BUF_F;
     const float* sw = st + T_F;
@@ -180,9 +159,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(F16 ? DCN_F
         }
         f16x8 ah, al;
         split_f16x3(a0, a1, ah, al);
-        const f16x8 bh0 = nb[0], bl0 = nb[1], bh1 = nb[2], bl1 = nb[3];
-        if (pp < 4) bload(dg, pp + 1);
-        else if (dg + 1 < 8) bload(dg + 1, 0);
+        const float* wp = sw + pp * 1024 + lane * 4;   // [pair][nt][plane][lane][8 halves]
+        const f16x8 bh0 = ldh8(wp), bl0 = ldh8(wp + 256), bh1 = ldh8(wp + 512), bl1 = ldh8(wp + 768);
         acc0 = mfma16h(ah, bh0, acc0);
         acc1 = mfma16h(ah, bh1, acc1);
         acc0 = mfma16h(ah, bl0, acc0);
@@ -240,13 +218,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(F16 ? DCN_F
 #pragma unroll
       for (int k = 0; k < NOM; ++k) omc[k] = omn[k];
     }
-    if constexpr (F16) {
-      // the next group's LDS-DMA has landed once at most the 20 younger B prefetches are in flight
-      asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
-      __syncthreads();
-    } else {
-      lds_dma_barrier();
-    }
+    lds_dma_barrier();
   }
   // epilogue through a per-wave LDS block -> coalesced 16-B stores (see tile_to_lds)
   float* out = a.out[g] + (size_t)n * a.out_item;
