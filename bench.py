@@ -130,7 +130,7 @@ def synth_frames(first, count, H, W, device):
     return out.to(device)
 
 
-def cpu_baseline(stif, sd, frames_cpu, times, scale, crop=88):
+def cpu_baseline(stif, sd, frames_cpu, times, scale, crop=128):
     """The numpy oracle (fp32) on a bounded sample of the same workload: one pair of the
     window, cropped to crop x crop LR pixels (FLOP per output pixel does not depend on the
     frame size), on all host BLAS threads."""
