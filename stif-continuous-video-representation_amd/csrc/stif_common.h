@@ -34,14 +34,29 @@ STIF_DEV f16x8 ldh8(const float* p) { return __builtin_bit_cast(f16x8, *reinterp
 #define F16X3_SCALE_A 16.0f
 #define F16X3_UNSCALE 0x1p-14f
 STIF_DEV void split_f16x3(f32x4 x0, f32x4 x1, f16x8& h, f16x8& l) {
+  // per pair (x, y): h = fp16(x * 2^4), fp16(y * 2^4); l = fp16(fma(x, 2^4, -h.lo)), ... -- all four
+  // as v_fma_mix{lo,hi}_f16 (fp32 multiply-add, fp16 operand read directly, fp16 result).  x * 2^4 - h
+  // is exact in fp32, so l equals fp16(x * 2^4 - float(h)) bit for bit, at 4 VALU ops per pair
+  // instead of ~7 (the compiler's lowering of the plain expression scales, converts h back to fp32
+  // and subtracts separately)
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 hv, lv;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    const float a = x0[e] * F16X3_SCALE_A, b = x1[e] * F16X3_SCALE_A;
-    h[e] = (_Float16)a;
-    h[e + 4] = (_Float16)b;
-    l[e] = (_Float16)(a - (float)h[e]);
-    l[e + 4] = (_Float16)(b - (float)h[e + 4]);
+    const float x = e < 2 ? x0[2 * e] : x1[2 * e - 4];
+    const float y = e < 2 ? x0[2 * e + 1] : x1[2 * e - 3];
+    unsigned hp, lp;
+    asm("v_fma_mixlo_f16 %0, %2, %4, 0\n\t"
+        "v_fma_mixhi_f16 %0, %3, %4, 0\n\t"
+        "v_fma_mixlo_f16 %1, %2, %4, -%0 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %1, %3, %4, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+        : "=&v"(hp), "=&v"(lp)
+        : "v"(x), "v"(y), "s"(F16X3_SCALE_A));
+    hv[e] = hp;
+    lv[e] = lp;
   }
+  h = __builtin_bit_cast(f16x8, hv);
+  l = __builtin_bit_cast(f16x8, lv);
 }
 
 STIF_DEV int mfma_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
