@@ -37,6 +37,60 @@ __global__ __launch_bounds__(256) void k_up2(const float* __restrict__ in, float
   st4(out + (size_t)item * out_item + ((size_t)y * W + x) * c + q * 4, v);
 }
 
+// one thread = 4 channels of the 2x2 output quad of input pixel (i, j): rows 2i, 2i+1, columns 2j,
+// 2j+1.  Every corner of those four outputs lies in the 3x3 input neighbourhood of (i, j), so the
+// thread loads 9 float4s for 4 outputs (16 with k_up2) and evaluates each output with k_up2's
+// coordinates, weights and expression (same rounding).  grid (x blocks over w1 * c/4, input row i, item)
+STIF_DEV f32x4 sel3(int s, f32x4 a, f32x4 b, f32x4 c) { return s == 0 ? a : (s == 1 ? b : c); }
+
+__global__ __launch_bounds__(256) void k_up2q(const float* __restrict__ in, float* __restrict__ out, int n, int h1,
+                                              int w1, int c, float scale, long long in_item, long long out_item) {
+  const int c4n = c >> 2;
+  const int W = 2 * w1;
+  const int i = blockIdx.y, item = blockIdx.z;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= w1 * c4n) return;
+  const int j = t / c4n, q = t - j * c4n;
+  const float* src = in + (size_t)item * in_item + q * 4;
+  float* dst = out + (size_t)item * out_item + q * 4;
+  // neighbourhood slot s holds input row / column (i|j) - 1 + s, clamped into the image (a clamped
+  // slot is never selected: every corner row / column lies inside the image)
+  const int r0 = max(i - 1, 0), r2 = min(i + 1, h1 - 1);
+  const int k0 = max(j - 1, 0), k2 = min(j + 1, w1 - 1);
+  f32x4 R[3][3];
+  const int rows[3] = {r0, i, r2}, cols[3] = {k0, j, k2};
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int b = 0; b < 3; ++b) R[a][b] = ld4(src + ((size_t)rows[a] * w1 + cols[b]) * c);
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const int y = 2 * i + a;
+    const float sy = fmaxf(0.5f * ((float)y + 0.5f) - 0.5f, 0.f);
+    const int y0 = min((int)sy, h1 - 1);
+    const int y1 = y0 + (y0 < h1 - 1 ? 1 : 0);
+    const float ly1 = sy - (float)y0, ly0 = 1.f - ly1;
+    const int sy0 = y0 - i + 1, sy1 = y1 - i + 1;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int x = 2 * j + b;
+      const float sx = fmaxf(0.5f * ((float)x + 0.5f) - 0.5f, 0.f);
+      const int x0 = min((int)sx, w1 - 1);
+      const int x1 = x0 + (x0 < w1 - 1 ? 1 : 0);
+      const float lx1 = sx - (float)x0, lx0 = 1.f - lx1;
+      const int sx0 = x0 - j + 1, sx1 = x1 - j + 1;
+      const f32x4 u0 = sel3(sy0, R[0][0], R[1][0], R[2][0]), u1 = sel3(sy0, R[0][1], R[1][1], R[2][1]),
+                  u2 = sel3(sy0, R[0][2], R[1][2], R[2][2]);
+      const f32x4 d0 = sel3(sy1, R[0][0], R[1][0], R[2][0]), d1 = sel3(sy1, R[0][1], R[1][1], R[2][1]),
+                  d2 = sel3(sy1, R[0][2], R[1][2], R[2][2]);
+      const f32x4 v00 = sel3(sx0, u0, u1, u2), v01 = sel3(sx1, u0, u1, u2);
+      const f32x4 v10 = sel3(sx0, d0, d1, d2), v11 = sel3(sx1, d0, d1, d2);
+      const f32x4 v = (ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11)) * scale;
+      st4(dst + ((size_t)y * W + x) * c, v);
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int stif_upsample2x_nhwc(const float* in, float* out, int n, int h1, int w1, int c, float scale,
@@ -46,8 +100,24 @@ extern "C" int stif_upsample2x_nhwc(const float* in, float* out, int n, int h1, 
     return stif_fail(STIF_E_INVALID, "stif_upsample2x_nhwc: bad arguments");
   if (2LL * h1 > 65535 || n > 65535 || 2LL * w1 * (c / 4) > 0x7fffffffLL)
     return stif_fail(STIF_E_INVALID, "stif_upsample2x_nhwc: image too large for the row grid");
-  const dim3 grid((unsigned)((2 * w1 * (c / 4) + 255) / 256), (unsigned)(2 * h1), (unsigned)n);
-  hipLaunchKernelGGL(k_up2, grid, dim3(256), 0, (hipStream_t)stream, in, out, n, h1, w1, c, scale, in_item, out_item);
+  // the 2x2-quad kernel reads 9 instead of 16 float4s per 4 outputs but runs 4x fewer threads: faster
+  // on large maps (48 x 128^2 -> 256^2: 282 -> 250 us), slower on small ones whose input stays in
+  // cache (48 x 64^2: 43 -> 47 us), so it takes launches of >= 8M quad threads
+  const long long quads = (long long)n * h1 * w1 * (c / 4);
+#ifdef UP2_PERPIXEL
+  const bool quad = false;
+#else
+  const bool quad = quads >= (8LL << 20);
+#endif
+  if (quad) {
+    const dim3 grid((unsigned)((w1 * (c / 4) + 255) / 256), (unsigned)h1, (unsigned)n);
+    hipLaunchKernelGGL(k_up2q, grid, dim3(256), 0, (hipStream_t)stream, in, out, n, h1, w1, c, scale, in_item,
+                       out_item);
+  } else {
+    const dim3 grid((unsigned)((2 * w1 * (c / 4) + 255) / 256), (unsigned)(2 * h1), (unsigned)n);
+    hipLaunchKernelGGL(k_up2, grid, dim3(256), 0, (hipStream_t)stream, in, out, n, h1, w1, c, scale, in_item,
+                       out_item);
+  }
   return stif_check_launch("stif_upsample2x_nhwc");
 }
 

@@ -120,15 +120,30 @@ def test_wino_rejects_bad_shapes(stif, pf):
         ops.conv2d([dict(layer=lay, in0=x, out=torch.empty(1, 4, 4, 64, device="cuda"))], stride=2)
 
 
-@pytest.mark.parametrize("scale", [1.0, 2.0])
-def test_upsample2x(stif, scale):
-    """stif_upsample2x_nhwc against the oracle's F.interpolate restatement, strided items."""
-    x = rnd(4, 64, 7, 9, seed=20)
+@pytest.mark.parametrize("scale,h,w", [(1.0, 7, 9), (2.0, 7, 9), (2.0, 1, 5), (1.0, 4, 1), (2.0, 1, 1)])
+def test_upsample2x(stif, scale, h, w):
+    """stif_upsample2x_nhwc against the oracle's F.interpolate restatement, strided items (incl. 1-row /
+    1-column / 1-pixel maps, where the 2x2-quad kernel's clamped neighbourhood slots matter)."""
+    x = rnd(4, 64, h, w, seed=20)
     t = nhwc(x)
-    out = torch.empty(2, 14, 18, 64, device="cuda")
+    out = torch.empty(2, 2 * h, 2 * w, 64, device="cuda")
     stif.ops.upsample2x(t[1::2], out, scale)
     ref = O.upsample2x(x[1::2].astype(np.float64)) * scale
     assert relmax(to_nchw(out), ref) < 1e-6
+
+
+@pytest.mark.parametrize("n,h,w", [(2, 512, 512), (1, 513, 1025)])
+def test_upsample2x_quad_kernel(stif, n, h, w):
+    """Launches of >= 8M quad threads take the 2x2-quad kernel (k_up2q): checked against torch's
+    F.interpolate(bilinear, x2, align_corners=False) on the GPU (fp32 reference of the same op;
+    tolerance 2e-6 of max |ref|), incl. an odd-sized map for the clamped border neighbourhoods."""
+    g = torch.Generator(device="cuda").manual_seed(7)
+    x = torch.randn(n, h, w, 64, device="cuda", generator=g)
+    out = torch.empty(n, 2 * h, 2 * w, 64, device="cuda")
+    stif.ops.upsample2x(x, out, 2.0)
+    ref = torch.nn.functional.interpolate(x.permute(0, 3, 1, 2), scale_factor=2, mode="bilinear",
+                                          align_corners=False).permute(0, 2, 3, 1) * 2.0
+    assert float((out - ref).abs().max()) <= 2e-6 * float(ref.abs().max())
 
 
 def test_wino_cat_upsampled_matches_fused_direct(stif, pf):
