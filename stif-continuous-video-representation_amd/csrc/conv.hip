@@ -52,8 +52,14 @@ __global__ __launch_bounds__(NW * 64) void k_conv(stif_conv_args a) {
   const int l32 = lane & 31;
   const int hf = lane >> 5;
   const int tiles_x = (a.Wo + 31) >> 5;
-  const int tx = blockIdx.x % tiles_x;
-  const int ty = blockIdx.x / tiles_x;
+  // XCD-aware tile order: workgroups b = x mod 8 run on XCD x, so XCD x takes a contiguous range of
+  // spatial tiles and vertically adjacent tiles (sharing halo rows and the 128-B pixel lines that
+  // successive 8-channel chunks re-touch) run under one L2 (stride-2 convs: 228 -> 196 us per C1
+  // dispatch; round-robin tiles put vertical neighbours on different XCDs)
+  const int nbx = gridDim.x;
+  const int bx = (nbx & 7) ? (int)blockIdx.x : (int)(blockIdx.x & 7) * (nbx >> 3) + (int)(blockIdx.x >> 3);
+  const int tx = bx % tiles_x;
+  const int ty = bx / tiles_x;
   const int slice = blockIdx.y;
   const int g = blockIdx.z / a.nitems;
   const int n = blockIdx.z - g * a.nitems;
