@@ -66,7 +66,14 @@ __global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l32 = lane & 31, hf = lane >> 5;
   const int H = a.H, W = a.W;
   const int tiles_x = (W + 31) >> 5;
-  const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+#ifdef DCN_XCD
+  // kernel experiment: XCD x (workgroups b = x mod 8) takes a contiguous range of spatial tiles
+  const int nbx = gridDim.x;
+  const int bx = (nbx & 7) ? (int)blockIdx.x : (int)(blockIdx.x & 7) * (nbx >> 3) + (int)(blockIdx.x >> 3);
+#else
+  const int bx = blockIdx.x;
+#endif
+  const int tx = bx % tiles_x, ty = bx / tiles_x;
   const int g = blockIdx.z / a.nitems, n = blockIdx.z - g * a.nitems;
   const float* in = a.in[g] + (size_t)n * a.in_item;
   const float* om = a.offmask[g] + (size_t)n * a.om_item;
