@@ -94,12 +94,14 @@ class KernelTimer:
             self._cur = None
 
     def per_kind(self):
+        """kind -> [launches, total ms, total FLOP, total algorithmic bytes]"""
         agg = {}
-        for (a, b, f), k in zip(self.rec, self.kinds):
-            d = agg.setdefault(k, [0, 0.0, 0.0])
+        for (a, b, f), k, nb in zip(self.rec, self.kinds, self.nbytes):
+            d = agg.setdefault(k, [0, 0.0, 0.0, 0.0])
             d[0] += 1
             d[1] += a.elapsed_time(b)
             d[2] += f
+            d[3] += nb
         return agg
 
     def dominant(self):
@@ -109,7 +111,7 @@ class KernelTimer:
     def report(self):
         """per-kind launches / avg us / TFLOP/s (all-kinds mode)"""
         agg = self.per_kind()
-        for k, (nl, ms, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+        for k, (nl, ms, fl, _) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
             print(f"  {str(k):40s} {nl:5d} launches {ms / nl * 1e3:9.1f} us avg {fl / (ms * 1e-3) / 1e12:7.1f} TFLOP/s"
                   f"  {ms:8.2f} ms total", file=sys.stderr)
 
@@ -119,6 +121,29 @@ class KernelTimer:
         nb = self.nbytes[:len(ms)]
         return (len(ms), float(np.mean(ms)) if ms else 0.0, float(np.mean(fl)) if fl else 0.0,
                 float(np.mean(nb)) if nb else 0.0)
+
+
+HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E (MI355X_MICROARCH.md)
+
+
+def hot_path_kernels(probe, mfma):
+    """The north star's DCNv2 + implicit-decoder kernels, from the last warm-up step (HIP events on
+    the launch stream): per kind avg time and TFLOP/s; for the DCN core also its algorithmic HBM
+    bytes (input + offset/mask + output per pixel) as GB/s and fraction of the HBM peak; for the
+    decoder stages the fraction of the MFMA peak of their operand mode."""
+    dec_peak = 2500.0 / 3 if mfma == "f16x3" else 157.3
+    out = {}
+    for k, (nl, ms, fl, nb) in probe.per_kind().items():
+        if k[0] not in ("dcn", "dec1", "dec2") or not ms:
+            continue
+        e = {"launches": nl, "avg_us": round(ms / nl * 1e3, 1), "tflops": round(fl / (ms * 1e-3) / 1e12, 1)}
+        if nb:
+            gbps = nb / (ms * 1e-3) / 1e9
+            e.update(hbm_gbps_algorithmic=round(gbps, 1), hbm_frac=round(gbps / HBM_PEAK_GBPS, 3))
+        if k[0] != "dcn":
+            e["mfma_frac"] = round(fl / (ms * 1e-3) / 1e12 / dec_peak, 3)
+        out["_".join(str(x) for x in k)] = e
+    return out
 
 
 def synth_frames(first, count, H, W, device):
@@ -200,6 +225,7 @@ def main():
         stif.ops.TRACE = None
         torch.cuda.synchronize()
         dom = probe.dominant()
+        hot = hot_path_kernels(probe, args.mfma)
         timer = KernelTimer(dom)
         stif.ops.TRACE = timer
         if dist:
@@ -272,6 +298,7 @@ def main():
                          "algorithmic_bytes_per_launch": round(avg_bytes),
                          "hbm_gbps_algorithmic": round(avg_bytes / (avg_ms * 1e-3) / 1e9, 1) if avg_ms else None},
         }
+        res["hot_path_kernels"] = hot
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(stif, sd, frames_cpu, times, scale)
         print(json.dumps(res), flush=True)
