@@ -1,15 +1,20 @@
 """Benchmark of the STIF LunaTokis forward on MI355X (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1]): a synthetic 7-frame 3x256x256 window = 6
-adjacent pairs, 4x spatial, one interpolated time t=0.5 -> 6 x 1024x1024 output
-pixels per GPU per step.  A step = gen_feat over the window (per-frame encoder,
-PCD alignment, Bi-Deformable-ConvLSTM, 40-block trunk) + the implicit decoder,
-with inputs already resident in HBM.  Multi-GPU: one process per GPU; rank r owns
-frames [6r, 6r+6] of a (6N+1)-frame sequence (the shared boundary frame is the
-temporal halo), so per-GPU work is fixed (weak scaling) and no collective is on
-the data path.  Rank 0 prints one JSON line.
+Workload (default c0 = the metric's own config, BASELINE.json "7x128x128 -> 4x"): a synthetic
+7-frame 3x128x128 window = 6 adjacent pairs, 4x spatial, one interpolated time t = 0.5 -> 6 x
+512x512 output pixels per GPU per step.  A step = the encoder over the window (per-frame encoder,
+PCD alignment, Bi-Deformable-ConvLSTM, 40-block trunk) + the implicit decoder, with inputs already
+resident in HBM.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c0|c2]
+Multi-GPU (one process per GPU, RCCL): c0-c2 are weak-scaled -- rank r owns frames [6r, 6r+6] of
+one (6N+1)-frame sequence -- and c3 / c4 strong-scaled -- one fixed sequence (64 frames at 720p /
+9 frames at 1080p) split into contiguous pair shards (8,8,...,7 at 8 ranks).  Neighbouring shards
+share one boundary frame; its per-frame encoder features come from rank r+1 by a point-to-point
+halo exchange inside the timed step (--halo recompute recomputes them instead).  Rank 0 prints one
+JSON line; at N = 1 it also carries the CPU baseline, a parity check of the same pair against the
+CPU oracle (max error, PSNR), the fp32-MFMA value and the C1 / C2 lines.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c0|c1|c2|c3|c4]
 """
 import argparse
 import json
@@ -25,11 +30,16 @@ sys.path.insert(0, REPO)
 
 BASE = json.load(open(os.path.join(REPO, "BASELINE.json")))
 CONFIGS = {
-    # name: (frames, H, W, scale, times)
-    "c0": (7, 128, 128, 4, [0.5]),
-    "c1": (7, 256, 256, 4, [0.5]),
-    "c2": (7, 540, 960, 4, [0.25, 0.5, 0.75]),
+    # name: (frames, H, W, (HH, WW) per LR (H, W), times, scaling); weak: frames per rank
+    "c0": (7, 128, 128, 4.0, [0.5], "weak"),
+    "c1": (7, 256, 256, 4.0, [0.5], "weak"),
+    "c2": (7, 540, 960, 4.0, [0.25, 0.5, 0.75], "weak"),
+    "c3": (64, 720, 1280, 4.0, [0.0, 0.5], "strong"),
+    "c4": (9, 1080, 1920, 2.5, [0.0, 0.25, 0.5, 0.75], "strong"),
 }
+# the reference's own CPU path (torch 2.10 + mkldnn, 8 threads, the survey container; BASELINE.md
+# section 2): one 128x128 pair -> 512x512 at one t in 3.69 s
+REF_TORCH_CPU_MPIX_S = 0.0711
 FP32_PEAK_TFLOPS = 157.3   # MI355X dense fp32 MFMA (MI355X_MICROARCH.md, chip-level parameters)
 # f16x3 operand mode: one fp32-class product = 3 products on the dense fp16 MFMA pipe (~2.5 PF/s)
 F16X3_PEAK_TFLOPS = 2500.0 / 3.0
@@ -155,116 +165,175 @@ def synth_frames(first, count, H, W, device):
     return out.to(device)
 
 
-def cpu_baseline(stif, sd, frames_cpu, times, scale, crop=128):
-    """The numpy oracle (fp32) on a bounded sample of the same workload: one pair of the
-    window, cropped to crop x crop LR pixels (FLOP per output pixel does not depend on the
-    frame size), on all host BLAS threads."""
-    from oracle import stif_oracle as O
+def _threads():
     try:
         from threadpoolctl import threadpool_info
-        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+        return max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
     except Exception:
-        threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    x = np.ascontiguousarray(frames_cpu[0:2, :, :crop, :crop].numpy()[None])
+        return int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+
+
+def cpu_baseline(sd, x, times, scale):
+    """The numpy oracle (fp32) on a bounded sample of the same workload: one pair of the window
+    cropped to 128 x 128 LR pixels (FLOP per output pixel does not depend on the frame size), on
+    all host BLAS threads.  Returns (baseline record, oracle output)."""
+    from oracle import stif_oracle as O
     t0 = time.perf_counter()
-    O.forward(x, times, sd, dtype=np.float32)
+    ref = O.forward(x, times, sd, dtype=np.float32)
     dt = time.perf_counter() - t0
     H, W = x.shape[-2:]
     mpix = len(times) * H * scale * W * scale / 1e6
-    return {"value": mpix / dt, "unit": "Mpix/s", "cores": threads, "kind": "port",
-            "sample": f"1 pair (frames 0-1) of the same window cropped to {H}x{W} -> {H * scale}x{W * scale}, "
-                      f"t={times}, numpy fp32 restatement (oracle/stif_oracle.py), {dt:.1f} s"}
+    rec = {"value": round(mpix / dt, 6), "unit": "Mpix/s", "cores": _threads(), "kind": "port",
+           "sample": f"1 pair (frames 0-1) of the same window cropped to {H}x{W} -> {int(H * scale)}x{int(W * scale)}, "
+                     f"t={times}, numpy fp32 restatement (oracle/stif_oracle.py), {dt:.1f} s",
+           "reference_torch_cpu": {"value": REF_TORCH_CPU_MPIX_S, "unit": "Mpix/s", "cores": 8,
+                                   "note": "the reference's own torch CPU path (Sakuya_arch_test.LunaTokis, torch 2.10 "
+                                           "+ mkldnn, 8 threads), one 128x128 pair -> 512x512 at t=0.5, measured in the "
+                                           "survey container (BASELINE.md section 2); not re-run on the GPU box, where "
+                                           "the reference is absent"}}
+    return rec, ref
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="c1", choices=sorted(CONFIGS))
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_r01.json"),
-                    help="PMC summary (tools/pmc_summary.py) giving the dominant kernel's HBM bytes/dispatch")
-    ap.add_argument("--mfma", default="f16x3", choices=["f32", "f16x3"],
-                    help="Winograd conv operand mode (model.LunaTokis mfma=)")
-    ap.add_argument("--kernel-report", action="store_true", help="time every conv launch kind (stderr)")
-    args = ap.parse_args()
+def parity_record(out, ref):
+    """GPU output vs the CPU oracle on the same pair: max errors, the north star's elementwise bar
+    (|a - b| <= 1e-4 |b| + 1e-6), PSNR vs the oracle, and the PSNR delta vs a ground truth."""
+    a = np.asarray(out, np.float64)
+    b = np.asarray(ref, np.float64)
+    d = np.abs(a - b)
+    ok = d <= 1e-4 * np.abs(b) + 1e-6
+    mse = float(np.mean(d ** 2))
+    # ground truth for the PSNR criterion (calc_psnr form, myutils.py:269-271, data range 1): the
+    # oracle's output rounded to 8-bit levels, the precision the harness writes frames in
+    gt = np.round(np.clip(b, 0, 1) * 255) / 255
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
-    if dist:
-        import torch.distributed as td
-        torch.cuda.set_device(local)
-        td.init_process_group("nccl")
-    device = torch.device("cuda", local)
-    torch.cuda.set_device(device)
+    def psnr(x):
+        m = float(np.mean((x - gt) ** 2))
+        return 10 * np.log10(1.0 / m) if m > 0 else float("inf")
+    return {"pair": "frames 0-1, 128x128 crop", "max_abs_err": float(d.max()),
+            "max_err_rel_to_max_ref": float(d.max() / np.abs(b).max()),
+            "elementwise_rtol1e-4_atol1e-6_frac": float(ok.mean()),
+            "psnr_vs_oracle_db": round(10 * np.log10(1.0 / mse), 2) if mse > 0 else None,
+            "psnr_gpu_vs_gt_db": round(psnr(a), 6), "psnr_oracle_vs_gt_db": round(psnr(b), 6),
+            "psnr_delta_db": abs(psnr(a) - psnr(b)),
+            "gt": "oracle output quantised to 8-bit levels (the harness's uint8 output precision)"}
 
-    import stif_pkg
-    stif = stif_pkg.load()
-    nframes, H, W, scale, times = CONFIGS[args.config]
-    pairs = nframes - 1
-    sd = stif.weights.make_state_dict(seed=0)
-    model = stif.LunaTokis(64, 6, 8, 5, 40, device=device, mfma=args.mfma)
+
+def run_config(stif, sd, cfg, args, world, rank, device, dist, mfma, trace_dom=True):
+    """Warm up, time args.steps steps of one config; returns (elapsed s, probe, timer, model, frames, tq,
+    out_pix per step over all ranks)."""
+    nframes, H, W, scale, times, scaling = CONFIGS[cfg]
+    P = stif.parallel
+    if scaling == "weak":
+        pairs = nframes - 1
+        total_frames = pairs * world + 1
+        shards = P.pair_shards(total_frames, world)
+    else:
+        total_frames = nframes
+        shards = P.pair_shards(total_frames, world)
+    a, b = shards[rank]
+    total_pairs = total_frames - 1
+    HH, WW = int(round(H * scale)), int(round(W * scale))
+    model = stif.LunaTokis(64, 6, 8, 5, 40, device=device, mfma=mfma)
     model.load_state_dict(sd, strict=True)
-    frames_cpu = synth_frames(rank * pairs, nframes, H, W, "cpu")
-    frames = frames_cpu.to(device)
+    frames = synth_frames(a, b - a, H, W, device) if b > a else None
     tq = [torch.tensor([[t]], device=device) for t in times]
+    exchange = args.halo == "exchange"
 
     def step():
-        model.gen_feat_window(frames)
-        return model.decoding(tq)
+        if frames is None:
+            return None
+        P.gen_feat_shard(model, frames, rank, world, shards=shards, exchange=exchange)
+        return model.decoding(tq, None if scale == 4.0 else (HH, WW))
 
     with torch.no_grad():
-        # warm-up; the last warm-up step times every launch to find the dominant kernel
         probe = KernelTimer(None)
         for i in range(max(1, args.warmup)):
-            stif.ops.TRACE = probe if i == max(1, args.warmup) - 1 else None
+            stif.ops.TRACE = probe if (trace_dom and i == max(1, args.warmup) - 1) else None
             step()
         stif.ops.TRACE = None
         torch.cuda.synchronize()
-        dom = probe.dominant()
-        hot = hot_path_kernels(probe, args.mfma)
-        timer = KernelTimer(dom)
-        stif.ops.TRACE = timer
+        timer = KernelTimer(probe.dominant() if (trace_dom and probe.rec) else ("none",))
+        stif.ops.TRACE = timer if trace_dom else None
         if dist:
-            td.barrier()
+            dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
             step()
         torch.cuda.synchronize()
         if dist:
-            td.barrier()
+            dist.barrier()
         elapsed = time.perf_counter() - t0
         stif.ops.TRACE = None
-    if dist:
+    out_pix = total_pairs * len(times) * HH * WW
+    return elapsed, probe, timer, model, frames, tq, out_pix
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c0", choices=sorted(CONFIGS))
+    ap.add_argument("--halo", default="exchange", choices=["exchange", "recompute"],
+                    help="boundary frame of a shard: features from rank r+1 (P2P) or recomputed")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="N=1: skip the fp32-MFMA and C1/C2 lines")
+    ap.add_argument("--traffic", default=None,
+                    help="PMC summary (tools/pmc_summary.py) giving the dominant kernel's HBM bytes/dispatch; "
+                         "default profiles/pmc_r02_<config>.json")
+    ap.add_argument("--mfma", default="f16x3", choices=["f32", "f16x3"],
+                    help="operand mode of the contractions (model.LunaTokis mfma=)")
+    ap.add_argument("--kernel-report", action="store_true", help="time every launch kind (stderr)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    td = None
+    if world > 1:
+        import torch.distributed as td
+        torch.cuda.set_device(local)
+        td.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    import stif_pkg
+    stif = stif_pkg.load()
+    sd = stif.weights.make_state_dict(seed=0)
+    nframes, H, W, scale, times, scaling = CONFIGS[args.config]
+    elapsed, probe, timer, model, frames, tq, out_pix = run_config(stif, sd, args.config, args, world, rank, device,
+                                                                   td, args.mfma)
+    dom = timer.kind
+    hot = hot_path_kernels(probe, args.mfma)
+    if td is not None:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         td.all_reduce(t, op=td.ReduceOp.MAX)
         elapsed = float(t.item())
     n_launch, avg_ms, avg_flops, avg_bytes = timer.summary()
-    if args.kernel_report and rank == 0:
+    if args.kernel_report and rank == 0 and frames is not None:
         with torch.no_grad():
             rep = KernelTimer(None)
             stif.ops.TRACE = rep
-            step()
+            model.gen_feat_window(frames)
+            model.decoding(tq)
             torch.cuda.synchronize()
             stif.ops.TRACE = None
-        print("conv launch report (one extra step, not timed):", file=sys.stderr)
+        print("launch report (one extra step, not timed):", file=sys.stderr)
         rep.report()
 
-    out_pix = pairs * len(times) * (H * scale) * (W * scale)
-    value = world * out_pix * args.steps / elapsed / 1e6
+    value = out_pix * args.steps / elapsed / 1e6
+    res = None
     if rank == 0:
         achieved = avg_flops / (avg_ms * 1e-3) / 1e12 if avg_ms else 0.0
         kname, kdesc, peak = kernel_desc(dom, args.mfma)
         traffic = None
-        # HBM bytes per dispatch of the same kernel from the committed PMC passes over this bench
-        # (tools/pmc_summary.py); they were measured at C1, so only a C1 line carries them
-        if args.config == "c1" and os.path.exists(args.traffic):
+        # HBM bytes per dispatch of the same kernel from the committed PMC passes over this bench at this
+        # config (tools/pmc_summary.py; FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md HBM section)
+        tpath = args.traffic or os.path.join(REPO, "profiles", f"pmc_r02_{args.config}.json")
+        if os.path.exists(tpath) and args.mfma == "f16x3":
             try:
-                pmc = json.load(open(args.traffic))["per_kernel"]
+                pmc = json.load(open(tpath))["per_kernel"]
                 hits = [v for k, v in pmc.items() if kname in k]
                 if len(hits) == 1:
                     traffic = round(hits[0]["hbm_bytes_per_dispatch"])
@@ -279,17 +348,22 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
-            "dtype": "f32",
-            "mfma_operands": ("f16x3: Winograd convs, the DCN core and the SIREN decoder layers run fp32 products as 3 fp16 MFMA products "
-                              "on split operands (x = h + l, ~22-bit operands, fp32 accumulation; accuracy "
-                              "equal to the fp32-MFMA path, DESIGN.md section 3)") if args.mfma == "f16x3" else
-                             "f32: every contraction on fp32 MFMA",
+            "dtype": args.mfma,
+            "mfma_operands": ("f16x3: every contraction (Winograd convs, stride-2 convs, the DCN core, the SIREN decoder "
+                              "layers) runs its fp32 products as 3 fp16 MFMA products on split operands (x = h + l, "
+                              "~22-bit operands, fp32 accumulation; outputs within 1e-4 of the fp32 reference, "
+                              "DESIGN.md section 3a); 1x1 convs and all elementwise/sampling math in fp32")
+                             if args.mfma == "f16x3" else "f32: every contraction on fp32 MFMA",
             "data": "synthetic (U[0,1) frames, seeded; deterministic generated weights: checkpoint not in tree)",
-            "config": {"workload": f"{nframes}x3x{H}x{W} window ({pairs} pairs), {scale}x spatial, t={times}",
-                       "frames_per_gpu": nframes, "lr_hw": [H, W], "scale": scale, "times": times,
-                       "parallelism": f"pair-sharded x{world} (1-frame halo, no collective)"},
+            "config": {"workload": f"{'per GPU ' if scaling == 'weak' else ''}{nframes}x3x{H}x{W} "
+                                   f"{'window' if scaling == 'weak' else 'sequence'} ({nframes - 1} pairs), "
+                                   f"{scale}x spatial, t={times}",
+                       "name": args.config, "frames": nframes, "lr_hw": [H, W], "scale": scale, "times": times,
+                       "parallelism": (f"sequence pair-sharded x{world}, boundary-frame features by "
+                                       f"{'RCCL P2P halo exchange' if args.halo == 'exchange' else 'recompute'}"
+                                       if world > 1 else "1 GPU")},
             "roofline": {"bound": "mfma", "kernel": f"{kname} ({kdesc})", "kind": list(dom),
                          "achieved": round(achieved, 3), "peak": round(peak, 2), "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4), "traffic": traffic,
@@ -297,12 +371,35 @@ def main():
                          "flops_per_launch": avg_flops,
                          "algorithmic_bytes_per_launch": round(avg_bytes),
                          "hbm_gbps_algorithmic": round(avg_bytes / (avg_ms * 1e-3) / 1e9, 1) if avg_ms else None},
+            "hot_path_kernels": hot,
         }
-        res["hot_path_kernels"] = hot
-        if not args.no_cpu_baseline and world == 1:
-            res["cpu_baseline"] = cpu_baseline(stif, sd, frames_cpu, times, scale)
+    if world == 1 and not args.no_extras:
+        # the same workload with every contraction on fp32 MFMA, then the C1 / C2 configs
+        extras = {}
+        runs = [(args.config, "f32" if args.mfma == "f16x3" else "f16x3")]
+        runs += [(c, args.mfma) for c in ("c1", "c2") if c != args.config and args.config in ("c0", "c1", "c2")]
+        for cfg, mf in runs:
+            a2 = argparse.Namespace(**vars(args))
+            a2.steps, a2.warmup = (3, 1) if cfg != "c2" else (2, 1)
+            del model
+            torch.cuda.empty_cache()
+            el, _, _, model, _, _, px = run_config(stif, sd, cfg, a2, 1, 0, device, None, mf, trace_dom=False)
+            extras[f"{cfg}_{mf}"] = {"value": round(px * a2.steps / el / 1e6, 4), "unit": "Mpix/s",
+                                     "ms_per_step": round(el / a2.steps * 1e3, 3), "steps": a2.steps}
+        res["extra_lines"] = extras
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        fr = synth_frames(0, 2, H, W, "cpu")[:, :, :128, :128]
+        x = np.ascontiguousarray(fr.numpy()[None])
+        rec, ref = cpu_baseline(sd, x, [0.5], 4)
+        res["cpu_baseline"] = rec
+        m = stif.LunaTokis(64, 6, 8, 5, 40, device=device, mfma=args.mfma)
+        m.load_state_dict(sd, strict=True)
+        with torch.no_grad():
+            out = m(torch.from_numpy(x).to(device), [0.5])[0].cpu().numpy()
+        res["parity"] = parity_record(out, ref)
+    if rank == 0:
         print(json.dumps(res), flush=True)
-    if dist:
+    if td is not None:
         td.destroy_process_group()
 
 

@@ -30,7 +30,8 @@ enum {
   STIF_OK = 0,
   STIF_E_INVALID = 1,   /* bad argument / unsupported shape */
   STIF_E_LAUNCH = 2,    /* kernel launch failed */
-  STIF_E_WORKSPACE = 3  /* workspace too small */
+  STIF_E_WORKSPACE = 3, /* workspace too small */
+  STIF_E_RANGE = 4      /* STIF_PACK_F16X3 packing: a weight exceeds the split-fp16 range (pack in fp32) */
 };
 
 /* activation / epilogue selector of stif_conv2d_nhwc and stif_dcn_nhwc */
@@ -70,11 +71,17 @@ typedef struct {
   int ks, stride;          /* 1 or 3; 1 or 2 (padding = ks/2) */
   int epi;                 /* STIF_EPI_* */
   int flags;               /* STIF_CONV_F16X3: weights packed with STIF_PACK_F16X3 (stif_conv3x3_wino only) */
+  int* status;             /* optional device word (NULL = none): with STIF_CONV_F16X3, set to 1 when an output
+                              element is not finite before its activation -- the signature of an activation
+                              outside the split-fp16 operand range (see STIF_CONV_F16X3) */
 } stif_conv_args;
 
 /* stif_conv_args.flags: fp32 products on the fp16 MFMA pipe by 3-term operand splitting (x = h + l,
  * a*b = ah*bh + ah*bl + al*bh, fp32 accumulation; ~22 significant bits per operand, see
- * stif_common.h).  Valid range: |activations| < 1024, |Winograd weights| < 64. */
+ * stif_common.h).  Valid range: |activations| < 1024 (Winograd: |transformed inputs| < 4096),
+ * |packed weights| < 64.  Both limits are enforced: the packers return STIF_E_RANGE for a weight
+ * outside it, and an activation outside it turns the outputs it feeds into NaN/inf, which the
+ * kernels report through the `status` word (the host then re-runs the call in fp32). */
 #define STIF_CONV_F16X3 1
 
 int stif_conv2d_nhwc(const stif_conv_args* args, void* stream);
@@ -112,6 +119,7 @@ typedef struct {
   int ngroups, nitems, H, W;
   int epi;                              /* STIF_EPI_NONE or STIF_EPI_LRELU */
   int flags;                            /* STIF_CONV_F16X3: w packed STIF_PACK_PLAIN | STIF_PACK_F16X3 */
+  int* status;                          /* optional device word, as stif_conv_args.status */
 } stif_dcn_args;
 
 int stif_dcn_nhwc(const stif_dcn_args* args, void* stream);
@@ -120,8 +128,12 @@ int stif_dcn_nhwc(const stif_dcn_args* args, void* stream);
  * weight [co,c,kh,kw], bias [co], offset [b, dg*2*kh*kw, ho, wo],
  * mask [b, dg*kh*kw, ho, wo]; output [b, co, ho, wo] (caller-allocated).
  * Any kernel/stride/pad/dilation/group combination of the reference is
- * accepted.  workspace: see stif_dcn_v2_workspace_size (0 bytes suffice for the
- * generic path). */
+ * accepted.  The STIF shape (c = co = 64, 3x3, stride 1, pad 1, dilation 1, 8 groups: every
+ * DCN_sep of LunaTokis) runs the fused im2col-free kernel of stif_dcn_nhwc (fp32 MFMA) between
+ * NCHW<->NHWC transposes, with the weights packed on the device -- workspace 344 floats per
+ * pixel (the reference's im2col path: 576); every other shape runs im2col + GEMM one sample at a
+ * time (workspace c*kh*kw*ho*wo floats, the reference's per-sample `columns`).
+ * workspace: at least stif_dcn_v2_workspace_size bytes, 16-B aligned. */
 size_t stif_dcn_v2_workspace_size(int batch, int channels, int height, int width, int channels_out,
                                   int kernel_h, int kernel_w, int stride_h, int stride_w, int pad_h,
                                   int pad_w, int dilation_h, int dilation_w, int deformable_group);
@@ -177,13 +189,16 @@ int stif_dec_stage2(const float* proj, const float* mlp, const float* hrfeat, co
                     const stif_dec_tables* tab, const stif_dec_image* img, const float* t, float* out_nchw,
                     int n, int h, int w, int HH, int WW, void* stream);
 /* The same stages with flags = STIF_CONV_F16X3: every SIREN layer on split-fp16 MFMA (mlp packed by
- * stif_pack_dec_mlp_ex with the same flag); flags = 0 is stif_dec_stage1 / stif_dec_stage2. */
+ * stif_pack_dec_mlp_ex with the same flag); flags = 0 is stif_dec_stage1 / stif_dec_stage2.
+ * status: optional device word (NULL = none), set to 1 by stage 2 when an RGB output is not finite
+ * in f16x3 mode (an HRfeat / hidden activation outside the split range propagates to the RGB:
+ * every split operand of both stages feeds encode_imnet). */
 int stif_dec_stage1_ex(const float* proj, const float* mlp, const stif_dec_tables* tab, const stif_dec_image* img,
                        const float* t, float* hrfeat, float* flow, int n, int h, int w, int HH, int WW, int flags,
-                       void* stream);
+                       int* status, void* stream);
 int stif_dec_stage2_ex(const float* proj, const float* mlp, const float* hrfeat, const float* flow,
                        const stif_dec_tables* tab, const stif_dec_image* img, const float* t, float* out, int n, int h,
-                       int w, int HH, int WW, int flags, void* stream);
+                       int w, int HH, int WW, int flags, int* status, void* stream);
 
 /* out = sum_k pred_k * wgt_k (per HR pixel weights [HH*WW], shared by the n items): the
  * local ensemble's area blend (Sakuya_arch_test.py:1076-1084). pred_k / out: [n][3][HH][WW]. */

@@ -6,10 +6,10 @@ Layout:
   _lib.py     ctypes binding of libstif_hip.so (no fallback: missing library -> error)
   ops.py      torch-buffer wrappers of the C ABI
   model.py    LunaTokis host (reference API: forward / gen_feat / decoding / load_state_dict)
-  dcn_v2.py   reference DCNv2 plugin API (dcn_v2_conv, DCN_sep, ...) on the drop-in op
   coords.py   fp32 query-grid tables of the decoder
   weights.py  state-dict spec + deterministic weight generator
   video.py    custom_video_test-style sliding-window driver
+(integration/_ext.py at the repo root is the DCNv2 `_ext` shim over ops.dcn_v2_forward)
   parallel.py frame-pair sharding over ranks
   serving.py  option files, define_G / load_network / VideoSRModel (checkpoint drop-in)
 """
@@ -19,7 +19,7 @@ from . import coords  # noqa: F401
 
 def __getattr__(name):
     # torch-dependent parts load lazily so that weight/coords utilities work without torch/GPU
-    if name in ("ops", "model", "dcn_v2", "video", "parallel", "_lib", "serving"):
+    if name in ("ops", "model", "video", "parallel", "_lib", "serving"):
         import importlib
         return importlib.import_module(f"{__name__}.{name}")
     if name == "LunaTokis":

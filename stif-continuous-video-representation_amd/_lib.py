@@ -30,7 +30,7 @@ class ConvArgs(C.Structure):
         ("H", C.c_int), ("W", C.c_int), ("C0", C.c_int),
         ("C1", C.c_int), ("in1_mode", C.c_int), ("in1_scale", C.c_float),
         ("Ho", C.c_int), ("Wo", C.c_int), ("cout", C.c_int), ("ks", C.c_int), ("stride", C.c_int),
-        ("epi", C.c_int), ("flags", C.c_int),
+        ("epi", C.c_int), ("flags", C.c_int), ("status", _P),
     ]
 
 
@@ -39,7 +39,7 @@ class DcnArgs(C.Structure):
         ("inp", _PA), ("offmask", _PA), ("w", _PA), ("bias", _PA), ("out", _PA),
         ("in_item", C.c_longlong), ("om_item", C.c_longlong), ("out_item", C.c_longlong),
         ("ngroups", C.c_int), ("nitems", C.c_int), ("H", C.c_int), ("W", C.c_int), ("epi", C.c_int),
-        ("flags", C.c_int),
+        ("flags", C.c_int), ("status", _P),
     ]
 
 
@@ -69,9 +69,9 @@ EXPORTS = {
     "stif_dec_stage2": (C.c_int, [_P, _P, _P, _P, C.POINTER(DecTables), C.POINTER(DecImage), _P, _P]
                         + [C.c_int] * 5 + [_P]),
     "stif_dec_stage1_ex": (C.c_int, [_P, _P, C.POINTER(DecTables), C.POINTER(DecImage), _P, _P, _P]
-                           + [C.c_int] * 6 + [_P]),
+                           + [C.c_int] * 6 + [_P, _P]),
     "stif_dec_stage2_ex": (C.c_int, [_P, _P, _P, _P, C.POINTER(DecTables), C.POINTER(DecImage), _P, _P]
-                           + [C.c_int] * 6 + [_P]),
+                           + [C.c_int] * 6 + [_P, _P]),
     "stif_dec_blend4": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_int, _P]),
     "stif_upsample_image": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P]),
     "stif_resize_frames": (C.c_int, [_P, _P] + [C.c_int] * 5 + [_P, _P, C.c_int, C.c_int, _P, _P, C.c_int, C.c_int,
@@ -93,8 +93,15 @@ EXPORTS = {
 _lib = None
 
 
+E_INVALID, E_LAUNCH, E_WORKSPACE, E_RANGE = 1, 2, 3, 4   # stif.h STIF_E_*
+
+
 class StifError(RuntimeError):
     """Raised for any non-zero status of the C ABI (the reference surfaces AT_ERROR as RuntimeError)."""
+
+    def __init__(self, msg, code=None):
+        super().__init__(msg)
+        self.code = code
 
 
 def lib():
@@ -114,4 +121,4 @@ def lib():
 def check(rc: int, what: str):
     if rc != 0:
         msg = lib().stif_last_error().decode(errors="replace")
-        raise StifError(f"{what} failed (code {rc}): {msg}")
+        raise StifError(f"{what} failed (code {rc}): {msg}", rc)

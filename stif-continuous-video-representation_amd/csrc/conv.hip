@@ -262,9 +262,11 @@ __global__ __launch_bounds__(NW * 64) void k_conv(stif_conv_args a) {
       for (int mt = 0; mt < MT; ++mt) {
         const int y = oy0 + wv * MT + mt;
         f32x16 v;
+        bool bad = false;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           float t = acc[mt][nt][r] * (F16 ? F16X3_UNSCALE : 1.f) + bv;
+          if (F16) bad |= not_finite(t);
           if (EPI == STIF_EPI_LRELU) t = lrelu01(t);
           if (EPI == STIF_EPI_RELU) t = fmaxf(t, 0.f);
           if (EPI == STIF_EPI_OFFMASK) {
@@ -272,6 +274,7 @@ __global__ __launch_bounds__(NW * 64) void k_conv(stif_conv_args a) {
           }
           v[r] = t;
         }
+        if (F16) report_range(a.status, bad && co < a.cout);
         tile_to_lds(blk, v, lane);
         f32x4 rv[4];
         if (EPI == STIF_EPI_RES) {

@@ -9,8 +9,9 @@
 //    modulated_deformable_im2col_gpu_kernel / dmcn_im2col_bilinear,
 //    dcn_v2_im2col_cuda.cu:25-54,125-195), stages the group's weight slice, and
 //    contracts with fp32 MFMA.  The columns buffer never exists.
-// 2. stif_dcn_v2_forward: drop-in for `_ext.dcn_v2_forward` (NCHW, any shape): an
-//    im2col kernel into a caller workspace + an fp32-MFMA GEMM with fused bias.
+// 2. stif_dcn_v2_forward: drop-in for `_ext.dcn_v2_forward` (NCHW, any shape): the STIF shape
+//    runs k_dcn between NCHW <-> NHWC transposes (weights packed on the device); any other shape
+//    an im2col kernel into a caller workspace + an fp32-MFMA GEMM with fused bias, per sample.
 #include "stif_common.h"
 #include "stif.h"
 #include "abi_util.h"
@@ -281,12 +282,15 @@ __global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
   for (int nt = 0; nt < 2; ++nt) {
     const float bv = bias[nt * 32 + l32];
     f32x16 v;
+    bool bad = false;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       float t = (nt ? acc1[r] : acc0[r]) * (F16 ? F16X3_UNSCALE : 1.f) + bv;
+      if (F16) bad |= not_finite(t);
       if (EPI == STIF_EPI_LRELU) t = lrelu01(t);
       v[r] = t;
     }
+    if (F16) report_range(a.status, bad);
     tile_to_lds(blk, v, lane);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -378,6 +382,70 @@ __global__ __launch_bounds__(256) void k_gemm_bias(const float* __restrict__ A, 
   }
 }
 
+// ------------------------------------------------------------------ drop-in, STIF shape
+// [R][Cc] -> [Cc][R] per batch item (NCHW <-> NHWC of one item), 32 x 32 tiles through LDS
+__global__ __launch_bounds__(256) void k_transpose(const float* __restrict__ src, float* __restrict__ dst, int R, int Cc) {
+  __shared__ float t[32][33];
+  const int b = blockIdx.z;
+  const float* s = src + (size_t)b * R * Cc;
+  float* d = dst + (size_t)b * R * Cc;
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int r = r0 + ty + 8 * k, c = c0 + tx;
+    t[ty + 8 * k][tx] = (r < R && c < Cc) ? s[(size_t)r * Cc + c] : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = c0 + ty + 8 * k, r = r0 + tx;
+    if (c < Cc && r < R) d[(size_t)c * R + r] = t[tx][ty + 8 * k];
+  }
+}
+
+// offset [b][8*18][HW] + mask [b][8*9][HW] (NCHW, reference channel order: offset (g, tap k) at
+// g*18 + 2k (+1 for w), mask at g*9 + k; dcn_v2_im2col_cuda.cu:160-167) -> the fused kernel's offmask
+// [b][HW][216] = [group][tap][dy, dx, mask], 64 pixels per workgroup through LDS
+__global__ __launch_bounds__(256) void k_offmask_nchw(const float* __restrict__ off, const float* __restrict__ msk,
+                                                      float* __restrict__ om, int HW) {
+  __shared__ float t[64 * 217];
+  const int b = blockIdx.y, p0 = blockIdx.x * 64;
+  const float* ob = off + (size_t)b * 144 * HW;
+  const float* mb = msk + (size_t)b * 72 * HW;
+  for (int i = threadIdx.x; i < 216 * 64; i += 256) {
+    const int j = i >> 6, px = i & 63, p = p0 + px;   // packed channel j, pixel
+    const int g = j / 27, k = (j % 27) / 3, e = j % 3;
+    float v = 0.f;
+    if (p < HW) v = e < 2 ? ob[(size_t)(g * 18 + 2 * k + e) * HW + p] : mb[(size_t)(g * 9 + k) * HW + p];
+    t[px * 217 + j] = v;
+  }
+  __syncthreads();
+  float* ow = om + ((size_t)b * HW + p0) * 216;
+  const int npx = min(64, HW - p0);
+  for (int i = threadIdx.x; i < npx * 216; i += 256) ow[i] = t[(i / 216) * 217 + i % 216];
+}
+
+// nn.Conv2d weight [64][64][3][3] + bias -> the STIF_PACK_PLAIN layout k_dcn<.., 0> reads:
+// [chunk 8][tap 9][nt 2][lane 64][4], lane l of nt = cout nt*32 + (l & 31), channels chunk*8 + 4(l >> 5) + e
+__global__ __launch_bounds__(256) void k_pack_dcn_w(const float* __restrict__ w, const float* __restrict__ b,
+                                                    float* __restrict__ wp, float* __restrict__ bp) {
+  const int i = blockIdx.x * 256 + threadIdx.x;   // 8 * 9 * 2 * 64 * 4 = 36864
+  if (i < 36864) {
+    const int e = i & 3, l = (i >> 2) & 63, nt = (i >> 8) & 1, t = (i >> 9) % 9, c = (i >> 9) / 9;
+    const int co = nt * 32 + (l & 31), ci = c * 8 + 4 * (l >> 5) + e;
+    wp[i] = w[(co * 64 + ci) * 9 + t];
+  }
+  if (i < 64) bp[i] = b[i];
+}
+
+bool stif_dcn_shape(int channels, int channels_out, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw,
+                    int dg, int height, int width) {
+  return channels == 64 && channels_out == 64 && kh == 3 && kw == 3 && sh == 1 && sw == 1 && ph == 1 && pw == 1 &&
+         dh == 1 && dw == 1 && dg == 8 && (long long)height * width * 216 * 4 < 0x7fffffffLL;
+}
+constexpr size_t DCN_WPACK = 36864, DCN_BPACK = 64;
+
 }  // namespace
 
 extern "C" int stif_dcn_nhwc(const stif_dcn_args* pa, void* stream) {
@@ -410,13 +478,15 @@ static bool dcn_dims(int H, int W, int kh, int kw, int sh, int sw, int ph, int p
 extern "C" size_t stif_dcn_v2_workspace_size(int batch, int channels, int height, int width, int channels_out,
                                              int kernel_h, int kernel_w, int stride_h, int stride_w, int pad_h,
                                              int pad_w, int dilation_h, int dilation_w, int deformable_group) {
-  (void)channels_out;
-  (void)deformable_group;
   int Ho, Wo;
   if (!dcn_dims(height, width, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w, dilation_h, dilation_w, &Ho,
                 &Wo))
     return 0;
-  return (size_t)batch * channels * kernel_h * kernel_w * Ho * Wo * sizeof(float);
+  if (stif_dcn_shape(channels, channels_out, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w, dilation_h,
+                     dilation_w, deformable_group, height, width))
+    return ((size_t)batch * height * width * (64 + 216 + 64) + DCN_WPACK + DCN_BPACK) * sizeof(float);
+  // generic: the reference's per-sample columns buffer [c * kh * kw][ho * wo] (dcn_v2_cuda.cu:90, one sample)
+  return (size_t)channels * kernel_h * kernel_w * Ho * Wo * sizeof(float);
 }
 
 extern "C" int stif_dcn_v2_forward(const float* input, const float* weight, const float* bias, const float* offset,
@@ -439,18 +509,63 @@ extern "C" int stif_dcn_v2_forward(const float* input, const float* weight, cons
                                                  deformable_group);
   if (!workspace || workspace_bytes < need)
     return stif_fail(STIF_E_WORKSPACE, "dcn_v2_forward: workspace too small");
-  float* cols = (float*)workspace;
   hipStream_t st = (hipStream_t)stream;
-  const long long n = (long long)batch * channels * Ho * Wo;
+  if (stif_dcn_shape(channels, channels_out, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w, dilation_h,
+                     dilation_w, deformable_group, height, width)) {
+    // every DCN_sep of LunaTokis: NCHW -> NHWC, offset/mask -> offmask, weights packed on the device,
+    // the fused im2col-free kernel (fp32 MFMA), NHWC -> NCHW
+    const int HW = height * width;
+    float* in_nhwc = (float*)workspace;
+    float* om = in_nhwc + (size_t)batch * HW * 64;
+    float* out_nhwc = om + (size_t)batch * HW * 216;
+    float* wp = out_nhwc + (size_t)batch * HW * 64;
+    float* bp = wp + DCN_WPACK;
+    hipLaunchKernelGGL(k_transpose, dim3((HW + 31) / 32, 2, batch), dim3(256), 0, st, input, in_nhwc, 64, HW);
+    hipLaunchKernelGGL(k_offmask_nchw, dim3((HW + 63) / 64, batch), dim3(256), 0, st, offset, mask, om, HW);
+    hipLaunchKernelGGL(k_pack_dcn_w, dim3((unsigned)(DCN_WPACK / 256)), dim3(256), 0, st, weight, bias, wp, bp);
+    int rc = stif_check_launch("dcn_v2_forward/layout");
+    if (rc) return rc;
+    stif_dcn_args a{};
+    a.in[0] = in_nhwc;
+    a.offmask[0] = om;
+    a.w[0] = wp;
+    a.bias[0] = bp;
+    a.out[0] = out_nhwc;
+    a.in_item = (long long)HW * 64;
+    a.om_item = (long long)HW * 216;
+    a.out_item = (long long)HW * 64;
+    a.ngroups = 1;
+    a.nitems = batch;
+    a.H = height;
+    a.W = width;
+    a.epi = STIF_EPI_NONE;
+    a.flags = 0;
+    a.status = nullptr;
+    rc = stif_dcn_nhwc(&a, stream);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_transpose, dim3(2, (HW + 31) / 32, batch), dim3(256), 0, st, out_nhwc, output, HW, 64);
+    return stif_check_launch("dcn_v2_forward/out");
+  }
+  // any other shape: im2col + GEMM one sample at a time (dcn_v2_cuda_forward's per-sample columns)
+  float* cols = (float*)workspace;
+  const int K = channels * kernel_h * kernel_w, N = Ho * Wo;
+  const long long n = (long long)channels * Ho * Wo;
   long long blocks = (n + 255) / 256;
   if (blocks > 1 << 20) blocks = 1 << 20;
-  hipLaunchKernelGGL(k_im2col, dim3((unsigned)blocks), dim3(256), 0, st, input, offset, mask, cols, batch, channels,
-                     height, width, Ho, Wo, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w, dilation_h,
-                     dilation_w, deformable_group);
-  int rc = stif_check_launch("dcn_v2_forward/im2col");
-  if (rc) return rc;
-  const int K = channels * kernel_h * kernel_w, N = Ho * Wo;
-  dim3 grid((N + 63) / 64, (channels_out + 63) / 64, batch);
-  hipLaunchKernelGGL(k_gemm_bias, grid, dim3(256), 0, st, weight, cols, bias, output, channels_out, K, N);
-  return stif_check_launch("dcn_v2_forward/gemm");
+  for (int b = 0; b < batch; ++b) {
+    hipLaunchKernelGGL(k_im2col, dim3((unsigned)blocks), dim3(256), 0, st,
+                       input + (size_t)b * channels * height * width,
+                       offset + (size_t)b * deformable_group * 2 * kernel_h * kernel_w * N,
+                       mask + (size_t)b * deformable_group * kernel_h * kernel_w * N, cols, 1, channels, height, width,
+                       Ho, Wo, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w, dilation_h, dilation_w,
+                       deformable_group);
+    int rc = stif_check_launch("dcn_v2_forward/im2col");
+    if (rc) return rc;
+    dim3 grid((N + 63) / 64, (channels_out + 63) / 64, 1);
+    hipLaunchKernelGGL(k_gemm_bias, grid, dim3(256), 0, st, weight, cols, bias, output + (size_t)b * channels_out * N,
+                       channels_out, K, N);
+    rc = stif_check_launch("dcn_v2_forward/gemm");
+    if (rc) return rc;
+  }
+  return STIF_OK;
 }

@@ -417,7 +417,7 @@ __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DE
                                                      const float* __restrict__ hrfeat, const float* __restrict__ flow,
                                                      stif_dec_tables tb, stif_dec_image im,
                                                      const float* __restrict__ tq, float* __restrict__ out, int n,
-                                                     int h, int w, int HH, int WW) {
+                                                     int h, int w, int HH, int WW, int* status) {
   __shared__ __attribute__((aligned(16))) float wbuf[2 * SEG * T];
   const int lane = threadIdx.x & 63, hf = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
@@ -550,8 +550,14 @@ __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DE
   if (valid && hf == 0) {
     const size_t plane = (size_t)HH * WW;
     float* o = out + (size_t)item * 3 * plane + (size_t)py * WW + px;
+    bool bad = false;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) o[c * plane] = o4[c] + mlp[E_B4 + c];
+    for (int c = 0; c < 3; ++c) {
+      const float v = o4[c] + mlp[E_B4 + c];
+      bad |= not_finite(v);
+      o[c * plane] = v;
+    }
+    if (F16) report_range(status, bad);
   }
 }
 
@@ -635,7 +641,8 @@ void launch_dec1(bool f16, long long blocks, hipStream_t st, const float* proj, 
 
 extern "C" int stif_dec_stage1_ex(const float* proj, const float* mlp, const stif_dec_tables* tab,
                                   const stif_dec_image* img, const float* t, float* hrfeat, float* flow, int n, int h,
-                                  int w, int HH, int WW, int flags, void* stream) {
+                                  int w, int HH, int WW, int flags, int* status, void* stream) {
+  (void)status;   // stage 1's split operands all feed stage 2 (see stif.h)
   const bool f16 = flags & STIF_CONV_F16X3;
   if (!proj || !mlp || !tables_ok(tab) || !image_ok(img) || !t || !hrfeat || !flow || n < 1 || h < 1 || w < 1 ||
       HH < 2 || WW < 2 || (!tab->hr_y) != (!tab->hr_x))
@@ -659,12 +666,12 @@ extern "C" int stif_dec_stage1_ex(const float* proj, const float* mlp, const sti
 extern "C" int stif_dec_stage1(const float* proj, const float* mlp, const stif_dec_tables* tab,
                                const stif_dec_image* img, const float* t, float* hrfeat, float* flow, int n, int h,
                                int w, int HH, int WW, void* stream) {
-  return stif_dec_stage1_ex(proj, mlp, tab, img, t, hrfeat, flow, n, h, w, HH, WW, 0, stream);
+  return stif_dec_stage1_ex(proj, mlp, tab, img, t, hrfeat, flow, n, h, w, HH, WW, 0, nullptr, stream);
 }
 
 extern "C" int stif_dec_stage2_ex(const float* proj, const float* mlp, const float* hrfeat, const float* flow,
                                   const stif_dec_tables* tab, const stif_dec_image* img, const float* t, float* out,
-                                  int n, int h, int w, int HH, int WW, int flags, void* stream) {
+                                  int n, int h, int w, int HH, int WW, int flags, int* status, void* stream) {
   const bool f16 = flags & STIF_CONV_F16X3;
   if (!proj || !mlp || !hrfeat || !flow || !tables_ok(tab) || !image_ok(img) || !t || !out || n < 1 || h < 1 ||
       w < 1 || HH < 2 || WW < 2)
@@ -674,17 +681,17 @@ extern "C" int stif_dec_stage2_ex(const float* proj, const float* mlp, const flo
   const stif_dec_image im = img ? *img : stif_dec_image{};
   hipStream_t st = (hipStream_t)stream;
   const dim3 g((unsigned)blocks), b(DEC2_NW * 64);
-  if (img && f16) hipLaunchKernelGGL((k_dec2<true, 1>), g, b, 0, st, proj, mlp, hrfeat, flow, *tab, im, t, out, n, h, w, HH, WW);
-  else if (img) hipLaunchKernelGGL((k_dec2<true, 0>), g, b, 0, st, proj, mlp, hrfeat, flow, *tab, im, t, out, n, h, w, HH, WW);
-  else if (f16) hipLaunchKernelGGL((k_dec2<false, 1>), g, b, 0, st, proj, mlp, hrfeat, flow, *tab, im, t, out, n, h, w, HH, WW);
-  else hipLaunchKernelGGL((k_dec2<false, 0>), g, b, 0, st, proj, mlp, hrfeat, flow, *tab, im, t, out, n, h, w, HH, WW);
+  if (img && f16) hipLaunchKernelGGL((k_dec2<true, 1>), g, b, 0, st, proj, mlp, hrfeat, flow, *tab, im, t, out, n, h, w, HH, WW, status);
+  else if (img) hipLaunchKernelGGL((k_dec2<true, 0>), g, b, 0, st, proj, mlp, hrfeat, flow, *tab, im, t, out, n, h, w, HH, WW, status);
+  else if (f16) hipLaunchKernelGGL((k_dec2<false, 1>), g, b, 0, st, proj, mlp, hrfeat, flow, *tab, im, t, out, n, h, w, HH, WW, status);
+  else hipLaunchKernelGGL((k_dec2<false, 0>), g, b, 0, st, proj, mlp, hrfeat, flow, *tab, im, t, out, n, h, w, HH, WW, status);
   return stif_check_launch("stif_dec_stage2");
 }
 
 extern "C" int stif_dec_stage2(const float* proj, const float* mlp, const float* hrfeat, const float* flow,
                                const stif_dec_tables* tab, const stif_dec_image* img, const float* t, float* out, int n,
                                int h, int w, int HH, int WW, void* stream) {
-  return stif_dec_stage2_ex(proj, mlp, hrfeat, flow, tab, img, t, out, n, h, w, HH, WW, 0, stream);
+  return stif_dec_stage2_ex(proj, mlp, hrfeat, flow, tab, img, t, out, n, h, w, HH, WW, 0, nullptr, stream);
 }
 
 extern "C" int stif_dec_blend4(const float* const* pred, const float* const* wgt, float* out, int n, int HH, int WW,

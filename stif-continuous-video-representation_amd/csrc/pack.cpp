@@ -147,10 +147,19 @@ void split_f16x3_host(double x, _Float16* h, _Float16* l) {
   *l = (_Float16)(v - (double)*h);
 }
 
+// split range of a packed weight: |x 2^10| must round to a finite fp16 (|x| < 64 less half an fp16 ulp)
+constexpr double F16X3_WMAX = 65504.0 / 1024.0;
+bool f16x3_ok(double x) { return x >= -F16X3_WMAX && x <= F16X3_WMAX; }
+int range_fail(const char* what) {
+  return stif_fail(STIF_E_RANGE, what);
+}
+
 // PLAIN | F16X3, the fused DCN core (k_dcn<F16>): [group][tap pair p][nt][plane][lane][8 halves];
 // element e of lane l holds tap 2p + (l >> 5) (tap 9 = zero padding), input channel 8 group + e,
 // cout nt * 32 + (l & 31)
 int pack_dcn_f16x3(const float* w, const float* b, int cout, int cin, float* w_dst, float* b_dst) {
+  for (size_t i = 0; i < (size_t)cout * cin * 9; ++i)
+    if (!f16x3_ok(w[i])) return range_fail("stif_pack_conv_weight: a weight is outside the f16x3 range (|w| < 64); pack it without STIF_PACK_F16X3");
   _Float16* dst = reinterpret_cast<_Float16*>(w_dst);
   for (int g = 0; g < cin / 8; ++g)
     for (int p = 0; p < 5; ++p)
@@ -174,6 +183,14 @@ int pack_dcn_f16x3(const float* w, const float* b, int cout, int cin, float* w_d
 int pack_wino_f16x3(const float* w, const float* b, int cout, int cin, int perm, float* w_dst, float* b_dst) {
   if (cin % 16) return stif_fail(STIF_E_INVALID, "f16x3 winograd pack needs cin % 16 == 0");
   const int cp = round64(cout), NS = cp / 64, NQ = cin / 16;
+  // |U| <= 9/4 max|g| (G g G^T, rows of G sum to <= 1.5 in magnitude): checked on U itself
+  for (size_t i = 0; i < (size_t)cout * cin; ++i) {
+    double u[4][4];
+    wino_u(w + i * 9, u);
+    for (int a = 0; a < 16; ++a)
+      if (!f16x3_ok(u[a / 4][a % 4]))
+        return range_fail("stif_pack_conv_weight: a Winograd weight G g G^T is outside the f16x3 range (|U| < 64); pack it without STIF_PACK_F16X3");
+  }
   _Float16* dst = reinterpret_cast<_Float16*>(w_dst);
   for (int s = 0; s < NS; ++s)
     for (int nt = 0; nt < 2; ++nt)
@@ -304,6 +321,12 @@ extern "C" size_t stif_dec_mlp_floats(void) { return stif_dec::MLP_FLOATS; }
 
 
 namespace {
+bool tile_f16x3_ok(const float* t) {
+  for (int i = 0; i < stif_dec::T; ++i)
+    if (!f16x3_ok(t[i])) return false;
+  return true;
+}
+
 // fp32 tile [v][lane][4] -> split-fp16 tile [m][plane][lane][8 halves] in place (x 2^10): element
 // (m, e) of a lane = fp32 element (v = 2m + (e >> 2), e & 3), i.e. feature F(8m + e, lane >> 5)
 void tile_to_f16x3(float* t) {
@@ -399,6 +422,11 @@ extern "C" int stif_pack_dec_mlp_ex(const float* const* f, const float* const* l
     // every MFMA weight tile split; the fp32 image tiles (img_mma) scaled to the accumulators' 2^14
     const int regions[][2] = {{F_W1, 4}, {F_W2, 16}, {F_W3, 16}, {L_W0, 4}, {L_W1, 4}, {L_W2, 16}, {L_W3, 8},
                               {E_W0, 8}, {E_W1, 4}, {E_W2, 16}, {E_W3, 64}, {E_W4, 8}};
+    // sine-layer tiles carry omega_0 = 30: their reference weights must stay below 64 / 30
+    for (const auto& r : regions)
+      for (int k = 0; k < r[1]; ++k)
+        if (!tile_f16x3_ok(d + r[0] + k * T))
+          return range_fail("stif_pack_dec_mlp_ex: a SIREN weight (times omega_0 for sine layers) is outside the f16x3 range (|w| < 64); pack with flags = 0");
     for (const auto& r : regions)
       for (int k = 0; k < r[1]; ++k) tile_to_f16x3(d + r[0] + k * T);
     for (int i = I_L; i < I_END; ++i) d[i] *= 16384.f;

@@ -59,6 +59,15 @@ STIF_DEV void split_f16x3(f32x4 x0, f32x4 x1, f16x8& h, f16x8& l) {
   l = __builtin_bit_cast(f16x8, lv);
 }
 
+// f16x3 operand-range report.  An operand outside the split range (|A * 2^4| > 65504) becomes an fp16
+// infinity, and every product it enters turns into inf or NaN (h = inf, l = -inf: inf - inf), so the
+// outputs it feeds are not finite.  The kernels test their pre-activation outputs with this and set
+// the caller's optional status word (a plain vector store; concurrent writers all store 1).
+STIF_DEV bool not_finite(float x) { return !(__builtin_fabsf(x) <= 3.40282347e38f); }
+STIF_DEV void report_range(int* status, bool bad) {
+  if (status != nullptr && bad) *status = 1;
+}
+
 STIF_DEV int mfma_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
 STIF_DEV f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }

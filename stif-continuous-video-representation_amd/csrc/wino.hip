@@ -444,6 +444,9 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256) __attribute__((amdgpu_waves_per_
         f32x4 y = (k & 1) ? (p1 - p2 - pe) : (pe + p1 + p2);
         if (F16) y *= F16X3_UNSCALE;   // exact power of two
         y += bv;
+        if (F16)
+          report_range(a.status, (cob < a.cout) & (not_finite(y[0]) | not_finite(y[1]) | not_finite(y[2]) |
+                                                   not_finite(y[3])));
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           if (EPI == STIF_EPI_LRELU) y[e] = lrelu01(y[e]);

@@ -4,8 +4,9 @@ Mirrors ``codes/models/modules/Sakuya_arch_test.py:LunaTokis`` -- constructor
 ``LunaTokis(nf, nframes, groups, front_RBs, back_RBs)`` (:268-311),
 ``forward(x, times, scale=None, test=False)`` (:1222-1231), ``gen_feat`` (:313-362),
 ``decoding`` (:364-459), ``load_state_dict(sd, strict=True)`` over the reference's
-442 keys -- but holds repacked device weights and runs every layer through
-libstif_hip.so (see ops.py); no torch.nn module is on the path.
+442 keys -- as an ``nn.Module`` whose parameters are those 442 tensors, but every layer
+runs through libstif_hip.so on repacked copies (see ops.py); no torch.nn layer is on
+the path.
 
 Work is batched across everything the reference runs sequentially but that is
 independent: both PCD_Align directions (different weights -> launch groups), both
@@ -16,10 +17,13 @@ the reconstruction trunk.  Per-frame encoder features are computed once per fram
 """
 from __future__ import annotations
 
+import math
+import warnings
 from collections import OrderedDict
 
 import numpy as np
 import torch
+from torch import nn
 
 from . import _lib as L
 from . import ops
@@ -33,67 +37,94 @@ def _np(v):
     return v.detach().cpu().numpy().astype(np.float32, copy=False)
 
 
-class LunaTokis:
-    """STIF LunaTokis (Sakuya_arch_test.py:268) on MI355X."""
+class _Container(nn.Module):
+    """A plain node of the reference's module tree (holds the reference parameters by their key)."""
+
+
+class LunaTokis(nn.Module):
+    """STIF LunaTokis (Sakuya_arch_test.py:268) on MI355X.
+
+    An ``nn.Module`` whose parameters are exactly the reference's 442 state-dict tensors (same keys,
+    shapes and registration order; ``requires_grad=False``: inference engine), so ``state_dict``,
+    ``load_state_dict``, ``.to()`` / ``.cuda()`` and ``nn.DataParallel`` (VideoSR_base_model.py:29-32)
+    behave as on the reference module.  The kernels read repacked copies of those weights
+    (non-persistent buffers under ``_pk``, derived at ``load_state_dict``; they move and replicate with
+    the module), never the parameters themselves."""
 
     def __init__(self, nf=64, nframes=3, groups=8, front_RBs=5, back_RBs=10, device="cuda", winograd=True,
-                 mfma="f16x3"):
+                 mfma="f16x3", range_check="rerun", chunk_px=2 ** 21):
+        super().__init__()
         if nf != 64 or groups != 8:
             raise ValueError("the gfx950 kernels implement nf=64, groups=8 (the shipped STIF configuration)")
         self.nf, self.groups = nf, groups
         self.in_frames = 1 + nframes // 2        # unused attributes kept for API parity (:272-273)
         self.ot_frames = nframes
         self.front_RBs, self.back_RBs = front_RBs, back_RBs
-        self.device = torch.device(device)
         self._spec = W.state_dict_spec(nf, front_RBs, back_RBs, groups)
+        dev = torch.device(device)
+        # the reference module tree: one parameter per state-dict key, registered in key order
+        for key, shape in self._spec.items():
+            *path, leaf = key.split(".")
+            node = self
+            for name in path:
+                if name not in node._modules:
+                    node.add_module(name, _Container())
+                node = node._modules[name]
+            node.register_parameter(leaf, nn.Parameter(torch.zeros(shape, device=dev), requires_grad=False))
+        self._pk = _Container()                   # packed kernel weights (non-persistent buffers)
+        self._meta = {}                           # layer name -> (buffer index, cout, cin, ks, mode)
+        self._meta32 = None                       # fp32 re-packing of the f16x3 layers (range fallback)
+        self.register_buffer("_range_status", torch.zeros(1, dtype=torch.int32, device=dev), persistent=False)
         self._host = None
+        self._layers_key = None
         self.layers = {}
-        self.feat = None
+        self._feat = None
         self.inp = None
         self._tables = {}
         self.training = False
         # 3x3 convs by Winograd F(2x2,3x3) where the shape allows (fp32 throughout); False = direct
         self.winograd = bool(winograd)
-        # operand arithmetic of the Winograd convs: "f32" (fp32 MFMA) or "f16x3" (fp32 products
-        # from three fp16 MFMAs on split operands, ~22-bit operands, fp32 accumulation; stif.h)
+        # operand arithmetic: "f32" (fp32 MFMA) or "f16x3" (fp32 products from three fp16 MFMAs on split
+        # operands, ~22-bit operands, fp32 accumulation; stif.h)
         if mfma not in ("f32", "f16x3"):
             raise ValueError("mfma must be 'f32' or 'f16x3'")
         self.mfma = mfma
         self._dec_flags = L.CONV_F16X3 if mfma == "f16x3" else 0   # decoder SIREN layers likewise
+        # f16x3 activations outside the split range: "rerun" the call in fp32 (warning), "raise", or "off"
+        if range_check not in ("rerun", "raise", "off"):
+            raise ValueError("range_check must be 'rerun', 'raise' or 'off'")
+        self.range_check = range_check
+        self.range_reruns = 0
+        # pairs per encoder pass: a window is processed in chunks of about chunk_px LR pixels, which
+        # bounds the PCD / BiConvLSTM working set (~20 KB per pair-pixel) at large frames
+        self.chunk_px = int(chunk_px)
+        self._active = False
 
-    # ------------------------------------------------------------------ nn.Module-like API
-    def eval(self):
-        return self
+    # ------------------------------------------------------------------ nn.Module API
+    @property
+    def device(self):
+        return self.conv_first.weight.device
 
     def train(self, mode=True):
         if mode:
             raise NotImplementedError("training (DCNv2 backward) is out of scope; inference only")
-        return self
+        return super().train(False)
 
-    def to(self, device):
-        device = torch.device(device)
-        if device.type != "cuda":
-            raise RuntimeError("LunaTokis (stif_amd) runs on the GPU only")
-        if self._host is not None and device != self.device:
-            self.device = device
-            self._pack()
-        self.device = device
-        return self
+    def to(self, *args, **kwargs):
+        device, dtype, _, _ = torch._C._nn._parse_to(*args, **kwargs)
+        if dtype is not None and dtype != torch.float32:
+            raise NotImplementedError("LunaTokis (stif_amd) computes in fp32 (operand modes: mfma='f32'|'f16x3')")
+        return super().to(*args, **kwargs)
 
-    def cuda(self, device=None):
-        return self.to("cuda" if device is None else torch.device("cuda", device))
+    def half(self):
+        raise NotImplementedError("LunaTokis (stif_amd) computes in fp32")
 
-    def __call__(self, *a, **k):
-        return self.forward(*a, **k)
+    bfloat16 = double = half
 
-    def state_dict(self):
-        if self._host is None:
-            raise RuntimeError("no weights loaded")
-        return OrderedDict((k, torch.from_numpy(v.copy())) for k, v in self._host.items())
-
-    def load_state_dict(self, state_dict, strict=True):
-        """Same key contract as nn.Module.load_state_dict on the reference module; a
-        'module.' prefix (DataParallel/DDP checkpoints) is stripped as base_model.py:93-98 does."""
+    def load_state_dict(self, state_dict, strict=True, assign=False):
+        """Same key contract as nn.Module.load_state_dict on the reference module; a 'module.' prefix
+        (DataParallel/DDP checkpoints) is stripped as base_model.py:93-98 does.  Repacks the kernel
+        weights on the parameters' device."""
         sd = OrderedDict()
         for k, v in state_dict.items():
             sd[k[7:] if k.startswith("module.") else k] = v
@@ -102,6 +133,7 @@ class LunaTokis:
         if strict and (missing or unexpected):
             raise RuntimeError("Error(s) in loading state_dict for LunaTokis:\n"
                                f"\tMissing key(s): {missing}\n\tUnexpected key(s): {unexpected}")
+        params = dict(self.named_parameters())
         host = OrderedDict()
         for k, shape in self._spec.items():
             if k in sd:
@@ -110,21 +142,30 @@ class LunaTokis:
                     raise RuntimeError(f"size mismatch for {k}: copying a param with shape {tuple(a.shape)}, "
                                        f"the shape in current model is {tuple(shape)}")
                 host[k] = np.ascontiguousarray(a)
+                params[k].data.copy_(torch.from_numpy(host[k]))
             elif self._host is not None:
                 host[k] = self._host[k]
             else:
-                host[k] = np.zeros(shape, np.float32)
+                host[k] = params[k].detach().cpu().numpy().astype(np.float32)
         self._host = host
         self._pack()
         return type("IncompatibleKeys", (), {"missing_keys": missing, "unexpected_keys": unexpected})()
 
     # ------------------------------------------------------------------ weight packing
     def _pack(self):
+        """Pack every layer for the kernels into non-persistent buffers of ``_pk`` (on the parameters'
+        device).  f16x3 packings whose weights leave the split range fall back to fp32 per layer."""
         h, dev = self._host, self.device
-        lay = {}
+        meta = {}
+        bufs = []
+
+        def put(name, pc, extra=None):
+            meta[name] = (len(bufs), pc.cout, pc.cin, pc.ks, pc.mode) if extra is None else (len(bufs),) + extra
+            bufs.append(pc.w)
+            bufs.append(pc.b if pc.b is not None else torch.zeros(1, device=dev))
 
         def conv(name, mode=L.PACK_PLAIN):
-            lay[name] = ops.pack_conv(h[name + ".weight"], h[name + ".bias"], mode, dev)
+            put(name, ops.pack_conv(h[name + ".weight"], h[name + ".bias"], mode, dev))
 
         # 3x3 / stride-1 / 64-cout convs run by Winograd F(2x2,3x3) (stif_conv3x3_wino; the
         # cat(., up(.)) ones on a materialised x2-upsampled second input), as do the offset/mask
@@ -133,8 +174,8 @@ class LunaTokis:
         f16 = L.PACK_F16X3 if self.mfma == "f16x3" else 0
         wino = (L.PACK_WINO | f16) if self.winograd else L.PACK_PLAIN
 
-        lay["conv_first.w"] = torch.from_numpy(h["conv_first.weight"]).to(dev)
-        lay["conv_first.b"] = torch.from_numpy(h["conv_first.bias"]).to(dev)
+        put("conv_first", ops.PackedConv(torch.from_numpy(h["conv_first.weight"]).to(dev),
+                                         torch.from_numpy(h["conv_first.bias"]).to(dev), 64, 3, 3, L.PACK_PLAIN))
         for i in range(self.front_RBs):
             conv(f"feature_extraction.{i}.conv1", wino)
             conv(f"feature_extraction.{i}.conv2", wino)
@@ -167,10 +208,25 @@ class LunaTokis:
         for i in range(self.back_RBs):
             conv(f"recon_trunk.{i}.conv1", wino)
             conv(f"recon_trunk.{i}.conv2", wino)
-        # decoder
-        lib = L.lib()
-        self.layers = lay
-        self._pack_proj(lr_image=True)
+        # decoder: LR projections + the SIREN MLPs
+        for lr_image in (True, False):
+            put("dec.proj" if lr_image else "dec.proj_hrimg", self._pack_proj(lr_image))
+        mlp, flags = self._pack_mlp(self._dec_flags)
+        self._dec_flags = flags
+        meta["dec.mlp"] = (len(bufs), flags)
+        bufs.append(mlp)
+        bufs.append(torch.zeros(1, device=dev))
+        self._pk = _Container()
+        for i, b in enumerate(bufs):
+            self._pk.register_buffer(f"b{i}", b, persistent=False)
+        self._meta = meta
+        self._meta32 = None
+        self._layers_key = None
+        self._tables = {}
+
+    def _pack_mlp(self, flags):
+        """All SIREN layers (stif_pack_dec_mlp_ex); an out-of-range weight for f16x3 -> fp32 packing."""
+        h, lib = self._host, L.lib()
 
         def siren_ptrs(prefix, n_sine):
             arrs = []
@@ -183,9 +239,14 @@ class LunaTokis:
         la, lp = siren_ptrs("flow_imnet.", 3)
         ea, ep = siren_ptrs("encode_imnet.", 4)
         mlp = np.empty(lib.stif_dec_mlp_floats(), np.float32)
-        L.check(lib.stif_pack_dec_mlp_ex(fp, lp, ep, mlp.ctypes.data, self._dec_flags), "stif_pack_dec_mlp_ex")
-        lay["dec.mlp"] = torch.from_numpy(mlp).to(dev)
-        self.layers = lay
+        try:
+            L.check(lib.stif_pack_dec_mlp_ex(fp, lp, ep, mlp.ctypes.data, flags), "stif_pack_dec_mlp_ex")
+        except L.StifError as e:
+            if e.code != L.E_RANGE or not flags:
+                raise
+            flags = 0
+            L.check(lib.stif_pack_dec_mlp_ex(fp, lp, ep, mlp.ctypes.data, 0), "stif_pack_dec_mlp_ex")
+        return torch.from_numpy(mlp).to(self.device), flags
 
     def _pack_proj(self, lr_image=True):
         """LR projection of the decoder's first layers (stif_pack_dec_proj_ex); lr_image=False leaves
@@ -198,10 +259,81 @@ class LunaTokis:
                                           h["flow_imnet.net.0.linear.weight"].ctypes.data,
                                           h["encode_imnet.net.0.linear.weight"].ctypes.data, int(lr_image),
                                           wd.ctypes.data, bd.ctypes.data), "stif_pack_dec_proj_ex")
-        self.layers["dec.proj" if lr_image else "dec.proj_hrimg"] = ops.PackedConv(
-            torch.from_numpy(wd).to(dev), torch.from_numpy(bd).to(dev), 256, 200, 1, L.PACK_PLAIN)
+        return ops.PackedConv(torch.from_numpy(wd).to(dev), torch.from_numpy(bd).to(dev), 256, 200, 1, L.PACK_PLAIN)
+
+    def _build_layers(self, pk, meta):
+        bufs = pk._buffers
+        lay = {}
+        for name, m in meta.items():
+            w, b = bufs[f"b{m[0]}"], bufs[f"b{m[0] + 1}"]
+            lay[name] = w if name == "dec.mlp" else ops.PackedConv(w, b, *m[1:])
+        return lay
+
+    def _layers_fp32(self):
+        """The f16x3 layers re-packed in fp32 (range fallback), as non-persistent buffers of ``_pk32``."""
+        if self._meta32 is None or self._pk32.b0.device != self.device:
+            keep = (self.mfma, self._dec_flags, self._pk, self._meta)
+            self.mfma, self._dec_flags = "f32", 0
+            try:
+                self._pack()
+                self._pk32, self._meta32 = self._pk, self._meta
+            finally:
+                self.mfma, self._dec_flags, self._pk, self._meta = keep
+                self._layers_key = None
+        return self._build_layers(self._pk32, self._meta32)
+
+    # ------------------------------------------------------------------ call wrapper
+    def _call(self, fn, *args, **kwargs):
+        """Run a public entry point on the module's device (its current stream), with the packed
+        layers of this module (or replica).  With f16x3 operands the kernels report non-finite
+        outputs in ``_range_status``; the call is then re-run in fp32 (range_check='rerun') or
+        raises (range_check='raise')."""
+        if self._host is None:
+            raise RuntimeError("LunaTokis: call load_state_dict first")
+        dev = self.device
+        if dev.type != "cuda":
+            raise L.StifError("LunaTokis (stif_amd) runs on the GPU only: move it with .to('cuda')")
+        if self._active:                       # nested entry (e.g. decoding_fasttest -> decoding)
+            return fn(*args, **kwargs)
+        with torch.cuda.device(dev):
+            key = self._pk.b0.data_ptr()
+            if self._layers_key != key:
+                self.layers = self._build_layers(self._pk, self._meta)
+                self._layers_key = key
+            check = self.range_check != "off" and (self.mfma == "f16x3")
+            self._active = True
+            try:
+                if check:
+                    self._range_status.zero_()
+                out = fn(*args, **kwargs)
+                if check and int(self._range_status.item()):
+                    if self.range_check == "raise":
+                        raise L.StifError("f16x3 operand outside the split-fp16 range (|activation| >= 1024): "
+                                          "use LunaTokis(mfma='f32') or range_check='rerun'", L.E_RANGE)
+                    warnings.warn("LunaTokis: an f16x3 operand left the split-fp16 range; re-running this call "
+                                  "with fp32 MFMA operands", RuntimeWarning, stacklevel=3)
+                    self.range_reruns += 1
+                    keep = (self.layers, self._dec_flags, self._layers_key)
+                    self.layers, self._dec_flags = self._layers_fp32(), 0
+                    try:
+                        out = fn(*args, **kwargs)
+                    finally:
+                        self.layers, self._dec_flags, self._layers_key = keep
+            finally:
+                self._active = False
+        return out
+
+    @property
+    def _status(self):
+        return self._range_status if self.range_check != "off" else None
 
     # ------------------------------------------------------------------ encoder pieces
+    def _conv(self, groups, **kw):
+        ops.conv2d(groups, status=self._status, **kw)
+
+    def _dcn(self, groups, **kw):
+        ops.dcn(groups, status=self._status, **kw)
+
     def _empty(self, *shape):
         return torch.empty(*shape, device=self.device, dtype=torch.float32)
 
@@ -209,7 +341,7 @@ class LunaTokis:
         """conv_first + feature_extraction + pyramid (:318-325) for frames [n,3,H,W] (NCHW)."""
         n, _, H, Wd = frames.shape
         l1 = self._empty(n, H, Wd, 64)
-        ops.conv_first(frames, self.layers["conv_first.w"], self.layers["conv_first.b"], l1)
+        ops.conv_first(frames, self.layers["conv_first"].w, self.layers["conv_first"].b, l1)
         tmp = self._empty(n, H, Wd, 64)
         for i in range(self.front_RBs):
             self._resblock(l1, tmp, f"feature_extraction.{i}")
@@ -218,8 +350,8 @@ class LunaTokis:
 
     def _resblock(self, x, tmp, name):
         """ResidualBlock_noBN (module_util.py:48-52), x updated in place."""
-        ops.conv2d([dict(layer=self.layers[name + ".conv1"], in0=x, out=tmp)], epi=L.EPI_RELU)
-        ops.conv2d([dict(layer=self.layers[name + ".conv2"], in0=tmp, out=x, res=x)], epi=L.EPI_RES)
+        self._conv([dict(layer=self.layers[name + ".conv1"], in0=x, out=tmp)], epi=L.EPI_RELU)
+        self._conv([dict(layer=self.layers[name + ".conv2"], in0=tmp, out=x, res=x)], epi=L.EPI_RES)
 
     def _pyramid(self, srcs):
         """fea_L2_conv1/2, fea_L3_conv1/2 with lrelu for a list of (L1 map, weight prefix)."""
@@ -230,13 +362,13 @@ class LunaTokis:
         a3 = self._empty(G, n, H // 4, Wd // 4, 64)
         b3 = self._empty(G, n, H // 4, Wd // 4, 64)
         lay = self.layers
-        ops.conv2d([dict(layer=lay[p + "fea_L2_conv1"], in0=s, out=a2[i]) for i, (s, p) in enumerate(srcs)],
+        self._conv([dict(layer=lay[p + "fea_L2_conv1"], in0=s, out=a2[i]) for i, (s, p) in enumerate(srcs)],
                    epi=L.EPI_LRELU, stride=2)
-        ops.conv2d([dict(layer=lay[p + "fea_L2_conv2"], in0=a2[i], out=b2[i]) for i, (s, p) in enumerate(srcs)],
+        self._conv([dict(layer=lay[p + "fea_L2_conv2"], in0=a2[i], out=b2[i]) for i, (s, p) in enumerate(srcs)],
                    epi=L.EPI_LRELU)
-        ops.conv2d([dict(layer=lay[p + "fea_L3_conv1"], in0=b2[i], out=a3[i]) for i, (s, p) in enumerate(srcs)],
+        self._conv([dict(layer=lay[p + "fea_L3_conv1"], in0=b2[i], out=a3[i]) for i, (s, p) in enumerate(srcs)],
                    epi=L.EPI_LRELU, stride=2)
-        ops.conv2d([dict(layer=lay[p + "fea_L3_conv2"], in0=a3[i], out=b3[i]) for i, (s, p) in enumerate(srcs)],
+        self._conv([dict(layer=lay[p + "fea_L3_conv2"], in0=a3[i], out=b3[i]) for i, (s, p) in enumerate(srcs)],
                    epi=L.EPI_LRELU)
         return b2, b3
 
@@ -258,7 +390,7 @@ class LunaTokis:
         def LO(u, name):
             return lay[f"{u[0]}{name}_{u[1]}.conv_offset_mask"]
 
-        conv, dcn = ops.conv2d, ops.dcn
+        conv, dcn = self._conv, self._dcn
         E = enumerate
 
         def conv_up(make, coarse, scale, epi):
@@ -345,36 +477,56 @@ class LunaTokis:
                     units.append((pcds[p] + "pcd_align.", 2, f2, f1, Y[p, d, 1]))
             self._pcd_align(units)
             T = self._empty(2, 2, B, H, Wd, 64)          # Easy_PCD.fusion outputs: (pcd, dir)
-            ops.conv2d([dict(layer=lay[pcds[p] + "fusion"], in0=Y[p, d, 0], in1=Y[p, d, 1], out=T[p, d])
+            self._conv([dict(layer=lay[pcds[p] + "fusion"], in0=Y[p, d, 0], in1=Y[p, d, 1], out=T[p, d])
                         for p in range(2) for d in range(2)], in1_mode=1)
             # ConvLSTMCell (convlstm.py:42-58): combined = cat(x, h~); c_next = f*c~ + i*g
-            ops.conv2d([dict(layer=lay[pf + "cell_list.0.conv"], in0=xin[d], in1=T[0, d], res=T[1, d],
+            self._conv([dict(layer=lay[pf + "cell_list.0.conv"], in0=xin[d], in1=T[0, d], res=T[1, d],
                              out=hs[d, t], out2=cs[d]) for d in range(2)], epi=L.EPI_LSTM, in1_mode=1)
         feats = self._empty(3, B, H, Wd, 64)
-        ops.conv2d([dict(layer=lay["ConvBLSTM.conv_1x1"], in0=hs[0, t], in1=hs[1, 2 - t], out=feats[t])
+        self._conv([dict(layer=lay["ConvBLSTM.conv_1x1"], in0=hs[0, t], in1=hs[1, 2 - t], out=feats[t])
                     for t in range(3)], in1_mode=1)
         return feats
 
-    def _gen_feat_core(self, fea1, fea2):
-        """Everything after the per-frame features: PCD + fusion, BiConvLSTM, recon trunk."""
+    def _gen_feat_core(self, fea1, fea2, out=None):
+        """Everything after the per-frame features: PCD + fusion, BiConvLSTM, recon trunk.
+        fea1 / fea2: [L1, L2, L3] of the pairs' first / second frames (item = pair)."""
         B, H, Wd, _ = fea1[0].shape
         X = self._empty(3, B, H, Wd, 64)
         X[0].copy_(fea1[0])
         X[2].copy_(fea2[0])
         Y = self._empty(2, B, H, Wd, 64)
         self._pcd_align([("pcd_align.", 1, fea1, fea2, Y[0]), ("pcd_align.", 2, fea2, fea1, Y[1])])
-        ops.conv2d([dict(layer=self.layers["fusion"], in0=Y[0], in1=Y[1], out=X[1])], in1_mode=1)
+        self._conv([dict(layer=self.layers["fusion"], in0=Y[0], in1=Y[1], out=X[1])], in1_mode=1)
+        del Y
         feats = self._bilstm(X)
+        del X
         trunk = feats.view(3 * B, H, Wd, 64)
         tmp = self._empty(3 * B, H, Wd, 64)
         for i in range(self.back_RBs):
             self._resblock(trunk, tmp, f"recon_trunk.{i}")
+        if out is not None:
+            out.copy_(feats)
+            return out
         return feats
+
+    def _gen_feat_pairs(self, fea1, fea2):
+        """_gen_feat_core over chunks of about ``chunk_px`` LR pixels of pairs (balanced), so the
+        working set stays bounded at large frames; pairs are independent, so chunking does not
+        change a bit of the result."""
+        B, H, Wd, _ = fea1[0].shape
+        per = max(1, self.chunk_px // (H * Wd))
+        if B <= per:
+            return self._gen_feat_core(fea1, fea2)
+        nch = math.ceil(B / per)
+        per = math.ceil(B / nch)
+        out = self._empty(3, B, H, Wd, 64)
+        for c0 in range(0, B, per):
+            c1 = min(B, c0 + per)
+            self._gen_feat_core([t[c0:c1] for t in fea1], [t[c0:c1] for t in fea2], out[:, c0:c1])
+        return out
 
     # ------------------------------------------------------------------ reference API
     def _check_input(self, x):
-        if self._host is None:
-            raise RuntimeError("LunaTokis: call load_state_dict first")
         x = x.to(self.device, torch.float32).contiguous()
         if x.dim() != 5 or x.shape[1] != 2 or x.shape[2] != 3:
             raise ValueError(f"x must be [B, 2, 3, H, W], got {tuple(x.shape)}")
@@ -384,42 +536,53 @@ class LunaTokis:
 
     def gen_feat(self, x):
         """LunaTokis.gen_feat (:313-362): x [B,2,3,H,W] -> self.feat (NHWC [3,B,H,W,64] on device)."""
+        return self._call(self._gen_feat, x)
+
+    def _gen_feat(self, x):
         x = self._check_input(x)
         self.inp = x
         B, N, C, H, Wd = x.shape
         l1, l2, l3 = self._frame_features(x.view(B * N, C, H, Wd))
         fea1 = [l1[0::2], l2[0::2], l3[0::2]]
         fea2 = [l1[1::2], l2[1::2], l3[1::2]]
-        self._feat = self._gen_feat_core(fea1, fea2)
+        self._feat = self._gen_feat_pairs(fea1, fea2)
         return None
 
     def frame_features(self, frames):
         """Per-frame encoder (conv_first + feature_extraction + pyramid, :318-325) of frames
-        [F,3,H,W] -> NHWC (L1, L2, L3); used for sliding windows and halo exchange."""
-        frames = frames.to(self.device, torch.float32).contiguous()
-        return self._frame_features(frames)
+        [F,3,H,W] -> NHWC (L1, L2, L3); used for sliding windows and the halo exchange."""
+        return self._call(lambda f: self._frame_features(f.to(self.device, torch.float32).contiguous()), frames)
 
-    def gen_feat_window(self, frames, last_frame_feats=None):
+    def gen_feat_window(self, frames, last_frame_feats=None, frame_feats=None):
         """Sliding-window gen_feat: frames [F,3,H,W] -> latents of the F-1 adjacent pairs, with the
         per-frame encoder run once per frame (the reference harness runs it twice per inner frame,
-        custom_video_test.py:81-97).  ``last_frame_feats`` = (L1, L2, L3) of the last frame computed
-        elsewhere (parallel.halo_exchange); its encoder is then not recomputed here."""
+        custom_video_test.py:81-97).  ``frame_feats`` = (L1, L2, L3) of all F frames computed
+        beforehand (frame_features + parallel.halo_exchange); ``last_frame_feats`` = those of the
+        last frame only (the others are computed here)."""
+        return self._call(self._gen_feat_window, frames, last_frame_feats, frame_feats)
+
+    def _gen_feat_window(self, frames, last_frame_feats=None, frame_feats=None):
         frames = frames.to(self.device, torch.float32).contiguous()
         x = torch.stack([frames[:-1], frames[1:]], dim=1).contiguous()
-        self._check_input(x)
-        self.inp = x
-        if last_frame_feats is None:
+        self.inp = self._check_input(x)
+        F_ = frames.shape[0]
+        if frame_feats is not None:
+            l1, l2, l3 = frame_feats
+            if l1.shape[0] != F_:
+                raise ValueError(f"frame_feats hold {l1.shape[0]} frames, the window {F_}")
+        elif last_frame_feats is None:
             l1, l2, l3 = self._frame_features(frames)
         else:
             a1, a2, a3 = self._frame_features(frames[:-1].contiguous())
-            l1, l2, l3 = (torch.cat([a, b.reshape(1, *a.shape[1:])]) for a, b in zip((a1, a2, a3), last_frame_feats))
-        self._feat = self._gen_feat_core([l1[:-1], l2[:-1], l3[:-1]], [l1[1:], l2[1:], l3[1:]])
+            l1, l2, l3 = (torch.cat([a, b.reshape(1, *a.shape[1:]).to(a.device)])
+                          for a, b in zip((a1, a2, a3), last_frame_feats))
+        self._feat = self._gen_feat_pairs([l1[:-1], l2[:-1], l3[:-1]], [l1[1:], l2[1:], l3[1:]])
         return None
 
     @property
     def feat(self):
         """Latent video as the reference's [B, 3, 64, H, W] (a permuted view of the NHWC buffer)."""
-        f = getattr(self, "_feat", None)
+        f = self.__dict__.get("_feat")
         return None if f is None else f.permute(1, 0, 4, 2, 3)
 
     @feat.setter
@@ -440,7 +603,7 @@ class LunaTokis:
         return t.contiguous()
 
     def _tab(self, H, Wd, HH, WW, shift=None):
-        key = (H, Wd, HH, WW, shift)
+        key = (str(self.device), H, Wd, HH, WW, shift)
         if key not in self._tables:
             self._tables[key] = ops.DecTablesDev(H, Wd, HH, WW, self.device, shift)
         return self._tables[key]
@@ -454,7 +617,7 @@ class LunaTokis:
         src = self._empty(B, H, Wd, 200)
         ops.dec_pack_lr(feats[0], feats[1], feats[2], x, src)
         proj = self._empty(B, H, Wd, 256)
-        ops.conv2d([dict(layer=self.layers["dec.proj" if lr_image else "dec.proj_hrimg"], in0=src, out=proj)])
+        self._conv([dict(layer=self.layers["dec.proj" if lr_image else "dec.proj_hrimg"], in0=src, out=proj)])
         return proj
 
     def _decode(self, proj, times, HH, WW, tab, image=None):
@@ -465,14 +628,17 @@ class LunaTokis:
         flow = self._empty(B, HH, WW, 4)
         for tq in times:
             t = self._time_vec(tq, B)
-            ops.dec_stage1(proj, mlp, tab, t, hrf, flow, image, flags=self._dec_flags)
+            ops.dec_stage1(proj, mlp, tab, t, hrf, flow, image, flags=self._dec_flags, status=self._status)
             out = self._empty(B, 3, HH, WW)
-            ops.dec_stage2(proj, mlp, hrf, flow, tab, t, out, image, flags=self._dec_flags)
+            ops.dec_stage2(proj, mlp, hrf, flow, tab, t, out, image, flags=self._dec_flags, status=self._status)
             preds.append(out)
         return preds
 
     def decoding(self, times=None, scale=None):
         """LunaTokis.decoding (:364-459): list over times of [B,3,HH,WW] (unclamped)."""
+        return self._call(self._decoding, times, scale)
+
+    def _decoding(self, times=None, scale=None):
         if times is None:
             raise ValueError("times must be a list of query times")
         proj = self._projection()
@@ -484,10 +650,11 @@ class LunaTokis:
         """LunaTokis.decoding_test (:461-598), what forward(test=True) returns: the flow and encode
         stages sample HRinp = F.upsample(inp, x4, bilinear) instead of the LR frames; HH = H * scale
         (integer scale, default 4).  The reference's q/3 chunking only bounds its memory."""
+        return self._call(self._decoding_test, times, scale)
+
+    def _decoding_test(self, times=None, scale=None):
         if times is None:
             raise ValueError("times must be a list of query times")
-        if "dec.proj_hrimg" not in self.layers:
-            self._pack_proj(lr_image=False)
         proj = self._projection(lr_image=False)
         _, H, Wd, _ = proj.shape
         s = 4 if scale is None else int(scale)
@@ -498,17 +665,23 @@ class LunaTokis:
     def decoding_fasttest(self, times=None, scale=None):
         """LunaTokis.decoding_fasttest (:863-960): `times` is a list of floats, the latent a batch of
         one; all times come back as one batch [len(times), 3, HH, WW]."""
+        return self._call(self._decoding_fasttest, times, scale)
+
+    def _decoding_fasttest(self, times=None, scale=None):
         if self._feat is None:
             raise RuntimeError("decoding needs gen_feat first")
         if self._feat.shape[1] != 1:
             raise ValueError("decoding_fasttest batches the query times: the latent must have batch 1")
         tq = [torch.tensor([[float(t)]]) for t in times]
-        return torch.cat(self.decoding(tq, scale), 0)
+        return torch.cat(self._decoding(tq, scale), 0)
 
     def decoding_localensemble(self, times=None, scale=None):
         """LunaTokis.decoding_localensemble (:962-1085): four decodes with the query shifted by
         (+-1/H, +-1/W), blended per HR pixel by the diagonally opposite |rel_y rel_x| area; batch-1
         latent, `times` a list of floats -> [len(times), 3, HH, WW]."""
+        return self._call(self._decoding_localensemble, times, scale)
+
+    def _decoding_localensemble(self, times=None, scale=None):
         if self._feat is None:
             raise RuntimeError("decoding needs gen_feat first")
         if self._feat.shape[1] != 1:
@@ -516,12 +689,11 @@ class LunaTokis:
         proj = self._projection()
         _, H, Wd, _ = proj.shape
         HH, WW = (H * 4, Wd * 4) if scale is None else (int(scale[0]), int(scale[1]))
-        key = ("ens", H, Wd, HH, WW)
+        key = ("ens", str(self.device), H, Wd, HH, WW)
         if key not in self._tables:
             self._tables[key] = [torch.from_numpy(a).to(self.device) for a in ensemble_weights(H, Wd, HH, WW)]
         wts = self._tables[key]
         tq = [torch.tensor([[float(t)]]) for t in times]
-        outs = []
         decs = [torch.cat(self._decode(proj, tq, HH, WW, self._tab(H, Wd, HH, WW, (vx, vy))), 0)
                 for vx in (-1, 1) for vy in (-1, 1)]
         out = self._empty(len(times), 3, HH, WW)
@@ -530,7 +702,10 @@ class LunaTokis:
 
     def forward(self, x, times=None, scale=None, test=False, center=None, index=0):
         """LunaTokis.forward (:1222-1231): decoding, or decoding_test with test=True."""
-        self.gen_feat(x)
+        return self._call(self._forward, x, times, scale, test)
+
+    def _forward(self, x, times, scale, test):
+        self._gen_feat(x)
         if test:
-            return self.decoding_test(times, scale)
-        return self.decoding(times, scale)
+            return self._decoding_test(times, scale)
+        return self._decoding(times, scale)

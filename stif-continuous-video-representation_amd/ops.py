@@ -55,23 +55,44 @@ class PackedConv:
     mode: int
 
 
-def pack_conv(weight: np.ndarray, bias: np.ndarray, mode: int = L.PACK_PLAIN, device="cuda") -> PackedConv:
+def pack_conv(weight: np.ndarray, bias: np.ndarray, mode: int = L.PACK_PLAIN, device="cuda",
+              range_fallback: bool = True) -> PackedConv:
+    """Pack one conv layer.  A STIF_PACK_F16X3 packing whose weights leave the split-fp16 range
+    (stif_pack_conv_weight -> STIF_E_RANGE) is re-packed in fp32 (same kernel family, fp32 MFMA)
+    when ``range_fallback``; otherwise the StifError propagates."""
     weight = np.ascontiguousarray(weight, np.float32)
     bias = np.ascontiguousarray(bias, np.float32)
     cout, cin, ks, _ = weight.shape
     lib = L.lib()
     wd = np.empty(lib.stif_conv_weight_floats(cout, cin, ks, mode), np.float32)
     bd = np.empty(lib.stif_conv_bias_floats(cout, mode), np.float32)
-    L.check(lib.stif_pack_conv_weight(weight.ctypes.data, bias.ctypes.data, cout, cin, ks, mode,
-                                      wd.ctypes.data, bd.ctypes.data), "stif_pack_conv_weight")
+    try:
+        L.check(lib.stif_pack_conv_weight(weight.ctypes.data, bias.ctypes.data, cout, cin, ks, mode,
+                                          wd.ctypes.data, bd.ctypes.data), "stif_pack_conv_weight")
+    except L.StifError as e:
+        if e.code != L.E_RANGE or not range_fallback or not mode & L.PACK_F16X3:
+            raise
+        return pack_conv(weight, bias, mode & ~L.PACK_F16X3, device, False)
     return PackedConv(torch.from_numpy(wd).to(device), torch.from_numpy(bd).to(device), cout, cin, ks, mode)
 
 
-def conv2d(groups, *, epi=L.EPI_NONE, in1_mode=0, in1_scale=1.0, stride=None):
+def _split_by_mode(groups, key):
+    """Launch groups by operand mode: layers that fell back to fp32 packing run in their own launch."""
+    f16 = [g for g in groups if g[key].mode & L.PACK_F16X3]
+    return [f16, [g for g in groups if not g[key].mode & L.PACK_F16X3]] if 0 < len(f16) < len(groups) else None
+
+
+def conv2d(groups, *, epi=L.EPI_NONE, in1_mode=0, in1_scale=1.0, stride=None, status=None):
     """groups: list of dicts {layer: PackedConv, in0, [in1], out, [res], [out2]} with tensors
-    [nitems, H, W, C].  All groups share shapes and item strides."""
+    [nitems, H, W, C].  All groups share shapes and item strides.  status: optional int32 device
+    word that f16x3 kernels set on a non-finite output (operand out of the split range)."""
     if not 1 <= len(groups) <= L.MAXG:
         raise ValueError("conv2d: 1..8 groups")
+    parts = _split_by_mode(groups, "layer")
+    if parts:
+        for part in parts:
+            conv2d(part, epi=epi, in1_mode=in1_mode, in1_scale=in1_scale, stride=stride, status=status)
+        return
     g0 = groups[0]
     lay: PackedConv = g0["layer"]
     in0 = g0["in0"]
@@ -111,6 +132,7 @@ def conv2d(groups, *, epi=L.EPI_NONE, in1_mode=0, in1_scale=1.0, stride=None):
            for g in groups):
         raise ValueError("conv2d: groups mix Winograd / direct or f32 / f16x3 packings")
     a.flags = L.CONV_F16X3 if lay.mode & L.PACK_F16X3 else 0
+    a.status = _vp(status)
     tr = TRACE
     if tr is not None:
         # algorithmic (direct-convolution) FLOPs, whichever algorithm runs
@@ -158,8 +180,13 @@ def conv_first(x_nchw: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: torc
     L.check(L.lib().stif_conv_first(_vp(x_nchw), _vp(w), _vp(b), _vp(out), n, h, wd, _stream()), "stif_conv_first")
 
 
-def dcn(groups, *, epi=L.EPI_NONE):
+def dcn(groups, *, epi=L.EPI_NONE, status=None):
     """Fused DCN_sep core. groups: list of {layer: PackedConv (64->64 3x3), inp, offmask, out}."""
+    parts = _split_by_mode(groups, "layer")
+    if parts:
+        for part in parts:
+            dcn(part, epi=epi, status=status)
+        return
     g0 = groups[0]
     nitems, H, W, Cc = g0["inp"].shape
     assert Cc == 64
@@ -175,9 +202,8 @@ def dcn(groups, *, epi=L.EPI_NONE):
     a.out_item = _item_stride([g["out"] for g in groups], "dcn out")
     a.ngroups, a.nitems, a.H, a.W, a.epi = len(groups), nitems, H, W, epi
     f16 = g0["layer"].mode & L.PACK_F16X3
-    if any((g["layer"].mode & L.PACK_F16X3) != f16 for g in groups):
-        raise ValueError("dcn: groups mix f32 / f16x3 packings")
     a.flags = L.CONV_F16X3 if f16 else 0
+    a.status = _vp(status)
     tr = TRACE
     if tr is not None:
         tr.begin(("dcn", epi), 2.0 * 64 * 576 * H * W * nitems * len(groups),
@@ -253,20 +279,21 @@ def dec_pack_lr(f0, f1, f2, x, out):
             "stif_dec_pack_lr")
 
 
-def dec_stage1(proj, mlp, tables: DecTablesDev, t, hrfeat, flow, image: "DecImageDev" = None, flags=0):
+def dec_stage1(proj, mlp, tables: DecTablesDev, t, hrfeat, flow, image: "DecImageDev" = None, flags=0, status=None):
     n, h, w, _ = proj.shape
     HH, WW = hrfeat.shape[1:3]
     tr = TRACE
     if tr is not None:   # per HR px: feat_imnet layers 1-3 (36,864 MAC) + flow_imnet HRfeat/1-3 (25,600 MAC)
         tr.begin(("dec1",), 2.0 * 62464 * n * HH * WW)
     L.check(L.lib().stif_dec_stage1_ex(_vp(proj), _vp(mlp), C.byref(tables.c), C.byref(image.c) if image else None,
-                                       _vp(t), _vp(hrfeat), _vp(flow), n, h, w, HH, WW, flags, _stream()),
+                                       _vp(t), _vp(hrfeat), _vp(flow), n, h, w, HH, WW, flags, _vp(status), _stream()),
             "stif_dec_stage1")
     if tr is not None:
         tr.end()
 
 
-def dec_stage2(proj, mlp, hrfeat, flow, tables: DecTablesDev, t, out, image: "DecImageDev" = None, flags=0):
+def dec_stage2(proj, mlp, hrfeat, flow, tables: DecTablesDev, t, out, image: "DecImageDev" = None, flags=0,
+               status=None):
     n, h, w, _ = proj.shape
     HH, WW = hrfeat.shape[1:3]
     tr = TRACE
@@ -274,6 +301,6 @@ def dec_stage2(proj, mlp, hrfeat, flow, tables: DecTablesDev, t, out, image: "De
         tr.begin(("dec2",), 2.0 * 94976 * n * HH * WW)
     L.check(L.lib().stif_dec_stage2_ex(_vp(proj), _vp(mlp), _vp(hrfeat), _vp(flow), C.byref(tables.c),
                                        C.byref(image.c) if image else None, _vp(t), _vp(out), n, h, w, HH, WW, flags,
-                                       _stream()), "stif_dec_stage2")
+                                       _vp(status), _stream()), "stif_dec_stage2")
     if tr is not None:
         tr.end()

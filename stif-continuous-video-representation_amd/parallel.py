@@ -19,7 +19,8 @@ import torch.distributed as dist
 
 def pair_shards(num_frames: int, world: int) -> List[Tuple[int, int]]:
     """Frame ranges [start, stop) per rank; consecutive ranges overlap by one frame.
-    Pairs are split as evenly as possible (the first `rem` ranks take one more)."""
+    Pairs are split as evenly as possible (the first `rem` ranks take one more); with more ranks
+    than pairs the surplus ranks get an empty range (start == stop)."""
     pairs = num_frames - 1
     if pairs < 1 or world < 1:
         raise ValueError("need >= 2 frames and >= 1 rank")
@@ -37,16 +38,44 @@ def shard_for_rank(num_frames: int, world: int, rank: int) -> Tuple[int, int]:
     return pair_shards(num_frames, world)[rank]
 
 
-def halo_exchange(first_frame_feats: Sequence[torch.Tensor], rank: int, world: int, group=None):
-    """Send this rank's first-frame features to rank-1 and receive rank+1's (which is this
-    rank's last frame).  Returns the received tensors (None on the last rank)."""
-    reqs = []
+def halo_exchange(first_frame_feats: Sequence[torch.Tensor], rank: int, world: int, group=None,
+                  shards: Sequence[Tuple[int, int]] = None):
+    """Send this rank's first-frame features to rank-1 and receive rank+1's (which is this rank's
+    last frame): one neighbour exchange per rank, issued as one batched P2P group (RCCL over xGMI
+    with the nccl backend, gloo on CPU).  Returns the received tensors, or None when this rank has
+    no right neighbour with frames.  ``shards`` (pair_shards) lets ranks whose shard is empty --
+    more ranks than pairs -- drop out of the exchange instead of waiting on a peer that sends
+    nothing."""
+    def has(r):
+        return 0 <= r < world and (shards is None or shards[r][1] > shards[r][0])
+
+    if not has(rank):
+        return None
+    ops = []
     recv = None
-    if rank + 1 < world:
+    if has(rank + 1):
         recv = [torch.empty_like(t) for t in first_frame_feats]
-        reqs += [dist.irecv(t, src=rank + 1, group=group) for t in recv]
-    if rank > 0:
-        reqs += [dist.isend(t.contiguous(), dst=rank - 1, group=group) for t in first_frame_feats]
-    for q in reqs:
-        q.wait()
+        ops += [dist.P2POp(dist.irecv, t, rank + 1, group) for t in recv]
+    if has(rank - 1):
+        ops += [dist.P2POp(dist.isend, t.contiguous(), rank - 1, group) for t in first_frame_feats]
+    if ops:
+        for q in dist.batch_isend_irecv(ops):
+            q.wait()
     return recv
+
+
+def gen_feat_shard(model, frames: torch.Tensor, rank: int, world: int, group=None, shards=None,
+                   exchange: bool = True):
+    """Encoder of this rank's shard of one sequence.  ``frames``: the shard's frames [a, b) (its
+    pairs' frames, boundary frame included).  With ``exchange``, the boundary frame's per-frame
+    features (L1/L2/L3 of conv_first + feature_extraction + pyramid, 336 B per LR pixel) come from
+    rank r+1 by ``halo_exchange`` instead of being recomputed; ``exchange=False`` recomputes them.
+    Leaves the latents of the shard's pairs in ``model.feat``."""
+    if not exchange or world == 1:
+        model.gen_feat_window(frames)
+        return
+    has_right = rank + 1 < world and (shards is None or shards[rank + 1][1] > shards[rank + 1][0])
+    own = model.frame_features(frames[:-1] if has_right else frames)
+    recv = halo_exchange([t[:1] for t in own], rank, world, group, shards)
+    feats = own if recv is None else tuple(torch.cat([a, b]) for a, b in zip(own, recv))
+    model.gen_feat_window(frames, frame_feats=feats)

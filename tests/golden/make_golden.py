@@ -22,6 +22,8 @@ with ``load_state_dict(strict=True)``.
 Usage:  python tests/golden/make_golden.py             (model, window and per-op fixtures)
         python tests/golden/make_golden.py decoders    (decoding_test / _fasttest / _localensemble)
         python tests/golden/make_golden.py harness     (custom_video_test's imresize_np input resize)
+        python tests/golden/make_golden.py single      (custom_video_test's single_forward, 11x13 pair)
+        python tests/golden/make_golden.py c0          (BASELINE config C0: one full 128x128 pair, t=0.5)
 """
 import json
 import os
@@ -311,7 +313,68 @@ def harness():
     print("harness:", {k: v.shape for k, v in res.items()})
 
 
+def _reference_model():
+    install_shims()
+    sys.path.insert(0, REPO)
+    import stif_pkg
+    stif = stif_pkg.load()
+    import models.modules.Sakuya_arch_test as S
+    torch.set_num_threads(8)
+    sd_np = stif.weights.make_state_dict(seed=0)
+    model = S.LunaTokis(64, 6, 8, 5, 40)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd_np.items()}, strict=True)
+    return model.eval()
+
+
+def single():
+    """custom_video_test.py:41-54 (single_forward) on an 11x13 pair: zero-pad bottom/right to 12x16,
+    the eight times i/8, outputs not cropped -> single_11x13.npz.  The script itself cannot be
+    imported (cv2, module-level file I/O), so its five lines are restated here around the reference
+    model call."""
+    if not os.path.isdir(REF):
+        print("reference absent; nothing to do")
+        return
+    model = _reference_model()
+    g = torch.Generator().manual_seed(2024)
+    imgs_in = torch.rand(1, 2, 3, 11, 13, generator=g)
+    with torch.no_grad():
+        b, n, c, h, w = imgs_in.size()
+        h_n, w_n = int(4 * np.ceil(h / 4)), int(4 * np.ceil(w / 4))
+        imgs_temp = imgs_in.new_zeros(b, n, c, h_n, w_n)
+        imgs_temp[:, :, :, 0:h, 0:w] = imgs_in
+        time_Tensors = [torch.tensor([i / 8])[None] for i in range(8)]
+        outs = model(imgs_temp, time_Tensors)
+    np.savez_compressed(os.path.join(HERE, "single_11x13.npz"), x=f32(imgs_in),
+                        out=np.stack([f32(o[0]) for o in outs]))
+    print("single_forward:", tuple(outs[0].shape), len(outs))
+
+
+def c0():
+    """BASELINE.json configs[0] (C0): one full 128x128 pair of bench.py's synthetic window (frames 0
+    and 1, torch.Generator seeds 1234 / 1235, torch.rand(3, 128, 128)), 4x, t = 0.5, through the
+    reference model -> c0_pair_128.npz (output [3, 512, 512] float32)."""
+    if not os.path.isdir(REF):
+        print("reference absent; nothing to do")
+        return
+    model = _reference_model()
+    fr = []
+    for i in range(2):
+        g = torch.Generator().manual_seed(1234 + i)
+        fr.append(torch.rand(3, 128, 128, generator=g))
+    x = torch.stack(fr)[None]
+    with torch.no_grad():
+        out = model(x, [torch.tensor([[0.5]])])[0]
+    np.savez_compressed(os.path.join(HERE, "c0_pair_128.npz"), x=f32(x), out=f32(out[0]))
+    print("c0 pair:", tuple(out.shape), float(out.min()), float(out.max()))
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["single"]:
+        single()
+        sys.exit(0)
+    if sys.argv[1:] == ["c0"]:
+        c0()
+        sys.exit(0)
     if sys.argv[1:] == ["decoders"]:
         decoders()
         sys.exit(0)

@@ -1,0 +1,221 @@
+"""Every BASELINE.json config on the GPU, the model API as an nn.Module, the halo path, the f16x3
+range guard and the harness's single_forward.
+
+Tolerance (SURVEY.md section 8d / BASELINE.json north_star "rtol 1e-4 fp32"): elementwise
+|a - b| <= 1e-4 |b| + 1e-6 against the reference's output (C0: one full 128x128 pair, fixture made
+by running the reference model, tests/golden/make_golden.py c0) and, at the sizes the CPU cannot
+reach in a test (C1-C4 per rank), between the two operand modes of this engine (f16x3 vs fp32 MFMA,
+which agree with the reference to ~1e-6 of max|ref| at every size the oracle covers), plus
+finiteness and bit-exact batch independence.
+"""
+import os
+import warnings
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import stif_oracle as O
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+RTOL, ATOL = 1e-4, 1e-6
+
+
+def elementwise_ok(a, b, rtol=RTOL, atol=ATOL):
+    """(all within |a - b| <= rtol |b| + atol, worst excess ratio, max |a - b|) on the device."""
+    a = torch.as_tensor(a).to("cuda", torch.float64)
+    b = torch.as_tensor(b).to("cuda", torch.float64)
+    d = (a - b).abs()
+    lim = rtol * b.abs() + atol
+    return bool((d <= lim).all()), float((d / lim).max()), float(d.max())
+
+
+def synth(first, count, H, W):
+    """bench.synth_frames: frame k = torch.rand(3, H, W) from Generator(1234 + k)."""
+    out = torch.empty(count, 3, H, W)
+    for i in range(count):
+        out[i] = torch.rand(3, H, W, generator=torch.Generator().manual_seed(1234 + first + i))
+    return out.cuda()
+
+
+@pytest.fixture(scope="module")
+def models(stif, sd):
+    ms = {}
+    for mf in ("f16x3", "f32"):
+        m = stif.LunaTokis(64, 6, 8, 5, 40, mfma=mf)
+        m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+        ms[mf] = m.eval()
+    return ms
+
+
+@pytest.mark.parametrize("mf", ["f16x3", "f32"])
+def test_c0_full_pair_matches_reference(models, mf):
+    """C0 (BASELINE configs[0]): the metric's 128x128 pair, 4x, t = 0.5, against the reference
+    model's own output, elementwise, and the PSNR criterion (< 1e-3 dB)."""
+    g = np.load(os.path.join(GOLD, "c0_pair_128.npz"))
+    with torch.no_grad():
+        out = models[mf](torch.from_numpy(g["x"]).cuda(), [torch.tensor([[0.5]])])[0][0]
+    ok, worst, dmax = elementwise_ok(out, g["out"])
+    assert ok, (worst, dmax)
+    gt = np.round(np.clip(g["out"].astype(np.float64), 0, 1) * 255) / 255
+    psnr = lambda a: 10 * np.log10(1.0 / np.mean((np.asarray(a, np.float64) - gt) ** 2))
+    assert abs(psnr(out.cpu().numpy()) - psnr(g["out"])) < 1e-3
+
+
+def test_c0_window_pairs_equal_single_pairs(models):
+    """The C0 7-frame window (bench's workload) batched = every pair run alone, bit for bit."""
+    fr = synth(0, 7, 128, 128)
+    m = models["f16x3"]
+    with torch.no_grad():
+        m.gen_feat_window(fr)
+        win = m.decoding([torch.tensor([[0.5]])])[0].clone()
+        for p in (0, 5):
+            one = m(torch.stack([fr[p], fr[p + 1]])[None], [0.5])[0]
+            assert torch.equal(win[p:p + 1], one), p
+
+
+CONFIG_CASES = {
+    # BASELINE configs[1..4] at their full per-GPU sizes: (frames, H, W, output size or None, times)
+    "C1": (7, 256, 256, None, [0.5]),
+    "C2": (7, 540, 960, None, [0.25, 0.5, 0.75]),
+    "C3_rank": (9, 720, 1280, None, [0.0, 0.5]),           # 64 frames / 8 ranks: 8 pairs per rank
+    "C4_rank": (2, 1080, 1920, (2700, 4800), [0.0, 0.25, 0.5, 0.75]),   # 1080p -> 2.5x, 4 t
+}
+
+
+@pytest.mark.parametrize("cfg", sorted(CONFIG_CASES))
+def test_config_full_size_f16x3_vs_f32(models, cfg):
+    F_, H, W, size, times = CONFIG_CASES[cfg]
+    fr = synth(0, F_, H, W)
+    tq = [torch.tensor([[t]]) for t in times]
+    outs = {}
+    with torch.no_grad():
+        for mf in ("f16x3", "f32"):
+            m = models[mf]
+            m.gen_feat_window(fr)
+            outs[mf] = m.decoding(tq, size)
+            m._feat = None
+    for a, b in zip(outs["f16x3"], outs["f32"]):
+        HH, WW = size or (4 * H, 4 * W)
+        assert tuple(a.shape) == (F_ - 1, 3, HH, WW)
+        assert bool(torch.isfinite(a).all()) and bool(torch.isfinite(b).all())
+        ok, worst, dmax = elementwise_ok(a, b)
+        assert ok, (cfg, worst, dmax)
+    del outs
+    torch.cuda.empty_cache()
+
+
+def test_chunked_window_is_bit_identical(models):
+    """Pair chunking (chunk_px: bounded working set at 720p/1080p) does not change a bit."""
+    m = models["f16x3"]
+    fr = synth(3, 5, 64, 96)
+    with torch.no_grad():
+        keep = m.chunk_px
+        m.gen_feat_window(fr)
+        a = m.decoding([0.5])[0].clone()
+        m.chunk_px = 64 * 96 + 1          # one pair per chunk
+        m.gen_feat_window(fr)
+        b = m.decoding([0.5])[0]
+        m.chunk_px = keep
+    assert torch.equal(a, b)
+
+
+def test_halo_features_are_bit_identical(models, stif):
+    """The multi-GPU halo path: the boundary frame's encoder features handed in (last_frame_feats /
+    frame_feats, what parallel.halo_exchange delivers) give bit-identical latents and outputs."""
+    m = models["f16x3"]
+    fr = synth(10, 4, 64, 64)
+    with torch.no_grad():
+        m.gen_feat_window(fr)
+        ref_feat = m.feat.clone()
+        ref = m.decoding([0.25])[0].clone()
+        last = m.frame_features(fr[-1:])
+        m.gen_feat_window(fr, last_frame_feats=last)
+        assert torch.equal(m.feat, ref_feat)
+        assert torch.equal(m.decoding([0.25])[0], ref)
+        allf = m.frame_features(fr)
+        m.gen_feat_window(fr, frame_feats=allf)
+        assert torch.equal(m.feat, ref_feat)
+        # a one-rank "world": gen_feat_shard without a neighbour is the plain window
+        stif.parallel.gen_feat_shard(m, fr, 0, 1)
+        assert torch.equal(m.feat, ref_feat)
+
+
+def test_module_api_dataparallel_and_device(models, golden):
+    """nn.Module drop-in: DataParallel(netG) as VideoSR_base_model.py:29-32 wraps it, state_dict
+    round trip, and a call made while another device context / stream is current."""
+    m = models["f16x3"]
+    g = golden["model_16x20"]
+    x = torch.from_numpy(g["x"]).cuda()
+    tq = [torch.tensor([[0.5]]).cuda()]
+    with torch.no_grad():
+        ref = m(x, tq)[0].clone()
+        dp = torch.nn.DataParallel(m)
+        out = dp(x, tq)[0]
+        assert torch.equal(out, ref)
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            out2 = m(x, tq)[0]
+        s.synchronize()
+        assert torch.equal(out2, ref)
+    sd = m.state_dict()
+    assert len(sd) == 442 and all(not v.requires_grad for v in m.parameters())
+
+
+def test_f16x3_activation_range_is_guarded(stif, sd, golden):
+    """Inputs far outside the split-fp16 range: the kernels flag the non-finite outputs, the call is
+    re-run in fp32 (bit-identical to an fp32-MFMA model), or raises with range_check='raise';
+    never silent inf/NaN."""
+    x = torch.from_numpy(golden["model_16x20"]["x"] * 5000.0).cuda()
+    tq = [torch.tensor([[0.5]])]
+    mk = lambda **kw: stif.LunaTokis(64, 6, 8, 5, 40, **kw)
+    m16, m32, mr = mk(), mk(mfma="f32"), mk(range_check="raise")
+    for m in (m16, m32, mr):
+        m.load_state_dict(sd)
+    with torch.no_grad():
+        ref = m32(x, tq)[0]
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            out = m16(x, tq)[0]
+        assert m16.range_reruns >= 1 and any("split-fp16 range" in str(i.message) for i in w)
+        assert bool(torch.isfinite(out).all())
+        assert torch.equal(out, ref)
+        with pytest.raises(stif._lib.StifError):
+            mr(x, tq)
+        # in range: no re-run
+        n = m16.range_reruns
+        m16(torch.from_numpy(golden["model_16x20"]["x"]).cuda(), tq)
+        assert m16.range_reruns == n
+
+
+def test_f16x3_weight_range_falls_back_per_layer(stif, sd, golden):
+    """A weight outside the split range (|U| >= 64) makes its layer pack in fp32 (the others stay
+    f16x3); the forward still matches the fp64 oracle on the same state dict."""
+    sd2 = dict(sd)
+    k = "recon_trunk.3.conv1.weight"
+    sd2[k] = sd[k].copy()
+    sd2[k][5, 7, 0, 0] = 80.0      # one corner tap: U[0][0] = 80 > 64, activations stay in range
+    m = stif.LunaTokis(64, 6, 8, 5, 40)
+    m.load_state_dict(sd2)
+    x = golden["model_16x20"]["x"]
+    with torch.no_grad():
+        out = m(torch.from_numpy(x).cuda(), [0.5])[0]
+    lay = m.layers["recon_trunk.3.conv1"]
+    assert not lay.mode & stif._lib.PACK_F16X3
+    assert m.layers["recon_trunk.3.conv2"].mode & stif._lib.PACK_F16X3
+    ref = O.forward(x, [0.5], sd2)[0]
+    d = np.abs(out.cpu().numpy() - ref).max()
+    assert d <= 1e-4 * np.abs(ref).max() + 1e-6, d
+
+
+def test_single_forward_matches_reference_harness(stif, models):
+    """custom_video_test.py:41-54 (single_forward): an 11x13 pair zero-padded to 12x16, eight times
+    i/8, uncropped 48x64 outputs -- against the reference run of the same five lines."""
+    g = np.load(os.path.join(GOLD, "single_11x13.npz"))
+    outs = stif.video.single_forward(models["f16x3"], torch.from_numpy(g["x"]).cuda())
+    assert len(outs) == 8
+    for i, o in enumerate(outs):
+        assert tuple(o.shape) == (1, 3, 48, 64)
+        ok, worst, dmax = elementwise_ok(o[0], g["out"][i])
+        assert ok, (i, worst, dmax)

@@ -10,16 +10,18 @@ from oracle import stif_oracle as O
 pytestmark = pytest.mark.gpu
 
 # north_star: outputs within rtol 1e-4 (fp32) and PSNR within 1e-3 dB of the reference.
-# Elementwise: |gpu - ref| <= 1e-4 * max|ref| + 1e-6.
+# Elementwise: |gpu - ref| <= 1e-4 * |ref| + 1e-6 for every element.
 RTOL = 1e-4
 ATOL = 1e-6
 
 
 def close(a, b, rtol=RTOL, atol=ATOL):
+    """(ok, max |a - b|, worst ratio of |a - b| to its elementwise bound)"""
     a = a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
     b = np.asarray(b, np.float64)
-    err = np.abs(a - b).max()
-    return err <= rtol * np.abs(b).max() + atol, float(err), float(np.abs(b).max())
+    d = np.abs(a - b)
+    lim = rtol * np.abs(b) + atol
+    return bool((d <= lim).all()), float(d.max()), float((d / lim).max())
 
 
 def psnr(a, gt):
@@ -47,6 +49,39 @@ def run16(model, golden):
     return g, outs, feat, out25
 
 
+def test_intermediates_match_reference(model, golden):
+    """PCD_Align output, fusion and BiConvLSTM latents (model_16x20.npz holds the reference's
+    forward-hook captures, make_golden.py:142-166) against the engine's own buffers."""
+    g = golden["model_16x20"]
+    x = torch.from_numpy(g["x"]).cuda()
+    cap = {}
+    orig_bilstm, orig_pcd = model._bilstm, model._pcd_align
+
+    def bilstm(X, *a, **k):
+        cap["fusion"] = X[1].detach().clone()           # fusion output = latent step 1 input
+        out = orig_bilstm(X, *a, **k)
+        cap["bilstm"] = out.detach().clone()
+        return out
+
+    def pcd(units):
+        orig_pcd(units)
+        if units[0][0] == "pcd_align." and "pcd" not in cap:
+            cap["pcd"] = [u[4].detach().clone() for u in units]
+    model._bilstm, model._pcd_align = bilstm, pcd
+    try:
+        with torch.no_grad():
+            model.gen_feat(x)
+    finally:
+        del model._bilstm, model._pcd_align
+    nchw = lambda t: t.permute(0, 3, 1, 2)[0].cpu().numpy()
+    pcd_out = np.concatenate([nchw(cap["pcd"][0]), nchw(cap["pcd"][1])], 0)     # cat(y1, y2) (:130)
+    for name, got, ref in (("pcd_align", pcd_out, g["pcd_align"]), ("fusion", nchw(cap["fusion"]), g["fusion"]),
+                           ("bilstm", np.stack([nchw(cap["bilstm"][t]) for t in range(3)]), g["bilstm"])):
+        assert got.shape == ref.shape, (name, got.shape, ref.shape)
+        ok, err, worst = close(got, ref)
+        assert ok, (name, err, worst)
+
+
 def test_gen_feat_matches_reference(run16):
     g, _, feat, _ = run16
     ok, err, mx = close(feat[0], g["feat"])
@@ -69,10 +104,11 @@ def test_arbitrary_scale_matches_reference(run16):
 
 
 def test_psnr_criterion(run16, sd):
-    """|PSNR(gpu, GT) - PSNR(ref, GT)| < 1e-3 dB with GT = the fp64 oracle perturbed by noise."""
+    """|PSNR(gpu, GT) - PSNR(ref, GT)| < 1e-3 dB, GT = the reference output quantised to 8-bit levels
+    (the precision the harness writes frames in) -- a GT close to both, so the delta is sensitive."""
     g, outs, _, _ = run16
     ref = g["out"][2]
-    gt = O.forward(g["x"], [0.5], sd)[0][0] + np.random.default_rng(0).standard_normal(ref.shape) * 0.01
+    gt = np.round(np.clip(ref.astype(np.float64), 0, 1) * 255) / 255
     d = abs(psnr(outs[2][0].cpu().numpy(), gt) - psnr(ref, gt))
     assert d < 1e-3, d
 
@@ -218,7 +254,7 @@ def test_f32_mfma_window_and_psnr(model_f32, golden, sd):
         out = model_f32.decoding([torch.tensor([[0.5]])])[0]
     ok, err, mx = close(out, g["out"])
     assert ok, (err, mx)
-    gt = np.clip(g["out"] + 0.05 * np.random.default_rng(3).standard_normal(g["out"].shape), 0, 1)
+    gt = np.round(np.clip(g["out"].astype(np.float64), 0, 1) * 255) / 255
     d = abs(psnr(out.cpu().numpy(), gt) - psnr(g["out"], gt))
     assert d < 1e-3, d
 

@@ -240,15 +240,42 @@ def test_dcn_dropin_rejects_bad_args(ops):
                            3, 3, 1, 1, 1, 1, 1, 1, 1)
 
 
-def test_dcn_sep_plugin_module_matches_reference(stif, sd, golden):
-    """The reference plugin API (dcn_v2.py:110-140) on the drop-in op vs the reference's own DCN_sep run."""
+def test_ext_shim_dcn_sep_matches_reference(sd, golden):
+    """integration/_ext.py (the `_ext` the reference's dcn_v2.py imports)
+    driven the way DCN_sep.forward drives it (dcn_v2.py:127-140: conv_offset_mask, chunk, cat,
+    sigmoid, _backend.dcn_v2_forward), against the reference's own DCN_sep output."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "_ext", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "integration", "_ext.py"))
+    ext = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ext)
     g = golden["ops"]
-    m = stif.dcn_v2.DCN_sep(64, 64, 3, stride=1, padding=1, dilation=1, deformable_groups=8).cuda()
     p = "pcd_align.L2_dcnpack_1"
-    with torch.no_grad():
-        m.weight.copy_(torch.from_numpy(sd[p + ".weight"]))
-        m.bias.copy_(torch.from_numpy(sd[p + ".bias"]))
-        m.conv_offset_mask.weight.copy_(torch.from_numpy(sd[p + ".conv_offset_mask.weight"]))
-        m.conv_offset_mask.bias.copy_(torch.from_numpy(sd[p + ".conv_offset_mask.bias"]))
-        out = m(torch.from_numpy(g["dcnsep_in"]).cuda(), torch.from_numpy(g["dcnsep_fea"]).cuda())
+    inp, fea = g["dcnsep_in"], g["dcnsep_fea"]
+    om = torch.from_numpy(O.conv2d(fea, sd[p + ".conv_offset_mask.weight"], sd[p + ".conv_offset_mask.bias"]).astype(
+        np.float32)).cuda()
+    o1, o2, m = torch.chunk(om, 3, dim=1)
+    offset = torch.cat((o1, o2), dim=1).contiguous()
+    mask = torch.sigmoid(m).contiguous()
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).cuda()
+    out = ext.dcn_v2_forward(T(inp), T(sd[p + ".weight"]), T(sd[p + ".bias"]), offset, mask, 3, 3, 1, 1, 1, 1, 1, 1, 8)
     assert relmax(out, g["dcnsep_out"]) < 1e-4
+    with pytest.raises(NotImplementedError):
+        ext.dcn_v2_backward()
+
+
+@pytest.mark.parametrize("hw", [(33, 70), (64, 64)])
+def test_dcn_v2_forward_dropin_stif_shape_fused(ops, hw):
+    """The STIF shape (64 -> 64, 3x3, s1 p1 d1, 8 groups) through the drop-in runs the fused kernel
+    (NCHW <-> NHWC transposes, device-side weight packing): gate boundaries and far offsets."""
+    H, W = hw
+    B = 2
+    x = rnd(B, 64, H, W, seed=50)
+    w = rnd(64, 64, 3, 3, seed=51, scale=0.05)
+    b = rnd(64, seed=52)
+    off, mask = _offsets(B, H, W, 53, 3.0)
+    ref = O.dcn_v2_forward(x, w, b, off, mask, 3, 3, 1, 1, 1, 1, 1, 1, 8)
+    T = lambda a: torch.from_numpy(a).cuda()
+    out = ops.dcn_v2_forward(T(x), T(w), T(b), T(off), T(mask), 3, 3, 1, 1, 1, 1, 1, 1, 8)
+    assert relmax(out, ref) < RTOL
