@@ -48,6 +48,8 @@ constexpr int IN_INST = (IN_EL + 63) / 64;     // LDS-DMA instructions per phase
 constexpr int EX_F = 2 * 2 * 2 * 1024;         // epilogue exchange: [wave 1|2][nt][b][32 tiles][32 co]
 constexpr int BUF_F = (IN_INST * 256 > EX_F) ? IN_INST * 256 : EX_F;   // floats per buffer (32 KB)
 constexpr int WG_PER_CU = 2;
+constexpr int OM_RP = 320;                     // k_wino_om: 16-B chunks per staged halo row (35 x PITCH + 5)
+static_assert(HR * OM_RP * 4 <= BUF_F && OM_RP % 8 == 0 && 35 * PITCH <= OM_RP, "k_wino_om staging image");
 #ifndef WINO_F16_XREAD_J
 #define WINO_F16_XREAD_J 3   // F16: block j after whose split the next pair's first chunk is read
 #endif
@@ -480,6 +482,250 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256) __attribute__((amdgpu_waves_per_
 }
 
 // ---------------------------------------------------------------------------------------------
+// k_wino_om: the DCN offset/mask conv (DCN_sep.conv_offset_mask, dcn_v2.py:127-133: 64 -> 216,
+// STIF_EPI_OFFMASK) in f16x3 with the transformed input held in registers.  k_wino computes one
+// 64-cout slice per tile, so for 216 outputs it stages, transforms and splits the same input four
+// times.  Here a workgroup stages a 4 x 32 tile's 64 input channels once, every wave turns its
+// transform row into the split A operands of all four 16-channel pairs (Ah/Al: 128 VGPRs), and then
+// walks the seven 32-cout N-tiles with only the B operands streaming from L2 (a 4-block register
+// ring, buffer loads at a uniform block offset): 48 MFMAs and one output-transform exchange per
+// N-tile.  The next tile's first staging phase is DMA'd into buffer 0 while the N-tiles run
+// (buffer 1 is the exchange image).  LDS-DMA source offsets relative to the tile's halo origin are
+// precomputed per lane, so an interior tile's DMA address is one add.
+template <int EPI>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_wino_om(stif_conv_args a,
+                                                                                        int ntiles) {
+  constexpr int SLICE_F = 8 * 8192;             // packed floats per 64-cout slice (8 chunks of 8 channels)
+#ifndef WINO_OM_RING
+#define WINO_OM_RING 2
+#endif
+#ifndef WINO_OM_SCHED
+#define WINO_OM_SCHED 1   // a scheduling barrier after every B block (keeps the B loads early)
+#endif
+  constexpr int RING = WINO_OM_RING;            // B blocks in flight
+  __shared__ __attribute__((aligned(16))) float smem[2 * BUF_F];
+  float* const ex = smem + BUF_F;               // exchange image (buffer 1 once the A operands are built)
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wi = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hf = lane >> 5;
+  const int tl = lane & 31;
+  const int tyl = tl >> 4, txl = tl & 15;
+  const int tiles_x = (a.Wo + 31) >> 5;
+  const int tiles_y = (a.Ho + WR - 1) / WR;
+  const int H = a.H, W = a.W;                   // C0 = 64, in1_mode 0 (host-checked)
+  const int ntn = (a.cout + 31) >> 5;           // 32-cout N-tiles
+  const int wbytes = ((a.cout + 63) >> 6) * SLICE_F * 4;
+
+  auto tile_of = [&](int T) {
+    Tile t;
+    t.slice = 0;
+    const int x = T % tiles_x;
+    int r = T / tiles_x;
+    const int y = r % tiles_y;
+    r /= tiles_y;
+    t.g = r / a.nitems;
+    t.n = r - t.g * a.nitems;
+    t.oy0 = y * WR;
+    t.ox0 = x * 32;
+    return t;
+  };
+
+  // Staging image [halo row][column slot][PITCH 16-B chunks], rows OM_RP chunks apart (35 column slots
+  // + 5 pad chunks: OM_RP = 0 mod 8 keeps both 16-lane groups of the transform's ds_read_b128
+  // conflict-free across the two patch rows).  DMA instruction (r, m) fills chunks r * OM_RP + 63 m +
+  // lane: lane -> column slot 7 m + lane / 9, chunk lane % 9 (8 = pad).  Lane 63 lands on the first
+  // chunk of the next instruction's pixel with that same pixel's data (or in the row pad), so the
+  // overlap is benign.  30 instructions per phase, wave wi issues r * 5 + m = wi, wi + 4, ...
+  const int lpx = lane / 9, lck = lane - 9 * (lane / 9);
+  auto stage = [&](const Tile& t, int p, int buf) {
+    const float* src = a.in0[t.g] + (size_t)t.n * a.in0_item;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, (int)((size_t)H * W * 256), 0x00020000);
+    float* dst = smem + buf * BUF_F;
+    const int iy0 = t.oy0 - 1, ix0 = t.ox0 - 1;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int ins = wi + 4 * k;
+      if (ins >= 30) break;
+      const int r = ins / 5, m = ins - 5 * (ins / 5);
+      const int y = iy0 + r;
+      const int slot = 7 * m + lpx;
+      const int x = ix0 + (slot < 17 ? 2 * slot : 2 * slot - 33);
+      const bool ok = ((unsigned)y < (unsigned)H) & ((unsigned)x < (unsigned)W) & (slot < HC) & (lck < 8);
+      const unsigned voff = ok ? (unsigned)(((y * W + x) * 64 + p * 32 + lck * 4) * 4) : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, dst + (r * OM_RP + 63 * m) * 4, 16, voff, 0, 0, 0);
+    }
+  };
+
+  // input transform row i (k_wino's xread / xform) -> split A operands of chunk pair q
+  const int rA = (wi == 0) ? 0 : (wi == 2 ? 2 : 1);
+  const int rB = (wi == 3) ? 3 : (wi == 2 ? 1 : 2);
+  const float sB = (wi == 1) ? 1.f : -1.f;
+  const int s0 = col_slot(0) + txl, s1 = col_slot(1) + txl, s2 = col_slot(2) + txl, s3 = col_slot(3) + txl;
+  auto xread = [&](const float* buf, int s, f32x4* rd) {
+    const float* ra = buf + ((2 * tyl + rA) * OM_RP + 2 * s + hf) * 4;
+    const float* rb = buf + ((2 * tyl + rB) * OM_RP + 2 * s + hf) * 4;
+    rd[0] = ld4(ra + s0 * PITCH * 4); rd[1] = ld4(rb + s0 * PITCH * 4);
+    rd[2] = ld4(ra + s1 * PITCH * 4); rd[3] = ld4(rb + s1 * PITCH * 4);
+    rd[4] = ld4(ra + s2 * PITCH * 4); rd[5] = ld4(rb + s2 * PITCH * 4);
+    rd[6] = ld4(ra + s3 * PITCH * 4); rd[7] = ld4(rb + s3 * PITCH * 4);
+  };
+  auto xform = [&](const f32x4* rd, f32x4* v) {
+    const f32x4 t0 = rd[0] + sB * rd[1];
+    const f32x4 t1 = rd[2] + sB * rd[3];
+    const f32x4 t2 = rd[4] + sB * rd[5];
+    const f32x4 t3 = rd[6] + sB * rd[7];
+    v[0] = t0 - t2;
+    v[1] = t1 + t2;
+    v[2] = t2 - t1;
+    v[3] = t1 - t3;
+  };
+  f16x8 Ah[4][4], Al[4][4];
+  auto make_a = [&](const float* buf, int sp, int q) {
+    f32x4 rd[8], va[4], vb[4];
+    xread(buf, 2 * sp, rd);
+    xform(rd, va);
+    xread(buf, 2 * sp + 1, rd);
+    xform(rd, vb);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) split_f16x3(va[j], vb[j], Ah[q][j], Al[q][j]);
+  };
+
+  // B fragments: [slice][pair q][i][j][u][plane][lane][8 halves] (STIF_PACK_WINO_OFFMASK | F16X3);
+  // block b = (q, j) of N-tile n at a uniform offset, this wave's row i and lane in the VGPR offset
+  const int bvo = (wi * 4096 + lane * 4) * 4;
+  auto boff = [&](int n, int b, int plane) {
+    return ((n >> 1) * SLICE_F + (b >> 2) * 16384 + (((b & 3) * 2 + (n & 1)) * 2 + plane) * 256) * 4;
+  };
+  auto wres = [&](int g) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)a.w[g], (short)0, wbytes, 0x00020000);
+  };
+  f16x8 bh[RING], bl[RING];
+  auto ldb = [&](__amdgpu_buffer_rsrc_t r, int n, int b, int slot) {
+    bh[slot] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(r, bvo, boff(n, b, 0), 0));
+    bl[slot] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(r, bvo, boff(n, b, 1), 0));
+  };
+
+  // output transform of N-tile n (k_wino's exchange, one 32-cout round); `last` also waits for the
+  // next tile's first staging phase (buffer 0) before the closing barrier
+  const int c4 = tid & 7, oxl = (tid >> 3) & 31;
+  const int bb = oxl & 1, txo = oxl >> 1;
+  auto bias_of = [&](const Tile& t, int n) {   // loaded before the N-tile's B prefetches (vmcnt order)
+    const int cob = n * 32 + c4 * 4;
+    return cob < a.cout ? ld4(a.bias[t.g] + cob) : f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  auto write_p = [&](const f32x16* acc) {
+    f32x16 yv[2];
+    yv[0] = acc[0] + acc[1] + acc[2];
+    yv[1] = acc[1] - acc[2] - acc[3];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int fl = (hf ^ b) * 32;
+      float* wb = ex + ((wi * 2 + b) * 32 + 4 * hf) * 32 + tl;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) wb[((r & 3) + 8 * (r >> 2)) * 32 + ((r & 1) ? -fl : fl)] = yv[b][r];
+    }
+  };
+  auto read_store = [&](const Tile& t, int n, f32x4 bv) {
+    const int ox = t.ox0 + oxl;
+    const int cob = n * 32 + c4 * 4;
+    const int m3 = cob % 3;
+    const bool cok = cob < a.cout;
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.out[t.g] + (size_t)t.n * a.out_item), (short)0, (int)((size_t)a.Ho * a.Wo * a.cout * 4),
+        0x00020000);
+    float chk = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float* rbase = ex + (bb * 32 + (txo ^ (((txo >> 2) ^ bb) & 1))) * 32 + c4 * 4 + (k >> 1) * 512;
+      const f32x4 p1 = ld4(rbase + 1 * 2048), p2 = ld4(rbase + 2 * 2048);
+      const f32x4 pe = ld4(rbase + ((k & 1) ? 3 : 0) * 2048);
+      f32x4 y = (k & 1) ? (p1 - p2 - pe) : (pe + p1 + p2);
+      y = y * F16X3_UNSCALE + bv;
+      chk += (y[0] + y[1]) + (y[2] + y[3]);
+      // sigmoid(m) on the mask channels (packed position % 3 == 2), branch-free: v_exp + v_rcp
+      // (a few ulp, far inside the parity bar)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (EPI == STIF_EPI_OFFMASK) y[e] = (m3 + e) % 3 == 2 ? sigmoid_fast(y[e]) : y[e];
+      const int oy = t.oy0 + k;
+      const bool ok = (oy < a.Ho) & (ox < a.Wo) & cok;
+      const unsigned vo = ok ? (unsigned)(((oy * a.Wo + ox) * a.cout + cob) * 4) : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, y), ro,
+                                             vo, 0, 0);
+    }
+    report_range(a.status, cok & not_finite(chk));   // a non-finite output makes the sum non-finite
+  };
+
+  auto mfma_nt = [&](__amdgpu_buffer_rsrc_t wr, __amdgpu_buffer_rsrc_t wrn, int n, f32x16* acc) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = f32x16{0};
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      const int q = b >> 2, j = b & 3, s = b % RING;
+      acc[j] = mfma16h(Ah[q][j], bh[s], acc[j]);
+      acc[j] = mfma16h(Ah[q][j], bl[s], acc[j]);
+      acc[j] = mfma16h(Al[q][j], bh[s], acc[j]);
+      // refill the slot with the block RING ahead: this N-tile, the next one, or the next tile's first
+      if (b + RING < 16) {
+        ldb(wr, n, b + RING, s);
+      } else {
+        const bool nn = n + 1 < ntn;
+        ldb(nn ? wr : wrn, nn ? n + 1 : 0, b + RING - 16, s);
+      }
+#if WINO_OM_SCHED
+      __builtin_amdgcn_sched_barrier(0);
+#endif
+    }
+  };
+
+  // XCD-aware persistent schedule (as k_wino): XCD x owns a contiguous range of spatial tiles
+  const int xcd = blockIdx.x & 7, nl = gridDim.x >> 3;
+  const int per = (ntiles + 7) >> 3;
+  const int tend = min((xcd + 1) * per, ntiles);
+  int T = xcd * per + (blockIdx.x >> 3);
+  if (T >= tend) return;
+  Tile cur = tile_of(T);
+  __amdgpu_buffer_rsrc_t wr = wres(cur.g);
+#pragma unroll
+  for (int s = 0; s < RING; ++s) ldb(wr, 0, s, s);
+  stage(cur, 0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (;;) {
+    const int Tn = T + nl;
+    const bool has_next = Tn < tend;
+    const Tile nxt = tile_of(has_next ? Tn : T);
+    const __amdgpu_buffer_rsrc_t wrn = wres(nxt.g);
+    stage(cur, 1, 1);
+    make_a(smem, 0, 0);
+    make_a(smem, 1, 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // phase 1 (and the B ring) landed
+    __syncthreads();
+    make_a(smem + BUF_F, 0, 2);
+    make_a(smem + BUF_F, 1, 3);
+    __syncthreads();                                     // both staging buffers consumed
+    if (has_next) stage(nxt, 0, 0);
+#pragma unroll 1
+    for (int n = 0; n < ntn; ++n) {
+      const f32x4 bv = bias_of(cur, n);   // before the N-tile's B prefetches (vmcnt order)
+      f32x16 acc[4];
+      mfma_nt(wr, wrn, n, acc);
+      write_p(acc);
+      __syncthreads();
+      read_store(cur, n, bv);
+      if (n + 1 == ntn) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // next tile's phase 0 landed
+      __syncthreads();
+    }
+    if (!has_next) break;
+    T = Tn;
+    cur = nxt;
+    wr = wrn;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // k_wino_ws: the same operator with warp specialisation.  One workgroup per CU, 8 waves: waves 0-3
 // are the MFMA waves (wave i = transform row i, exactly the k_wino loop), waves 4-7 are helpers
 // sharing their SIMDs: they issue all the LDS-DMA staging (so the MFMA waves' vmcnt queue only holds
@@ -798,6 +1044,10 @@ int num_cus() {
 #define WINO_SPLIT 0
 #endif
 
+#ifndef WINO_OM
+#define WINO_OM 1   // offset/mask conv (f16x3) by k_wino_om; 0 = the per-slice k_wino
+#endif
+
 #ifndef WINO_WS
 #define WINO_WS 0   // measured slower (k_wino_ws comment); kept as a build switch
 #endif
@@ -812,6 +1062,12 @@ int launch(const stif_conv_args& a, hipStream_t st) {
   if (WINO_WS && !(a.flags & STIF_CONV_F16X3) && (a.C0 + (a.in1_mode ? a.C1 : 0)) >= 16 * PSUB) {   // one warp-specialised workgroup per CU
     const int grid = 8 * (int)std::min<long long>((tiles + 7) / 8, (long long)num_cus() / 8);
     hipLaunchKernelGGL((k_wino_ws<IN1, EPI>), dim3(grid), dim3(512), 0, st, a, (int)tiles);
+    return stif_check_launch("stif_conv3x3_wino");
+  }
+  if constexpr (WINO_OM && EPI == STIF_EPI_OFFMASK) if ((a.flags & STIF_CONV_F16X3) && a.C0 == 64 && !a.in1_mode) {
+    const long long sp = tiles / ((a.cout + 63) / 64);   // spatial tiles: all couts per workgroup
+    const int g2 = 8 * (int)std::min<long long>((sp + 7) / 8, (long long)WG_PER_CU * num_cus() / 8);
+    hipLaunchKernelGGL((k_wino_om<EPI>), dim3(g2), dim3(256), 0, st, a, (int)sp);
     return stif_check_launch("stif_conv3x3_wino");
   }
   const int grid = 8 * (int)std::min<long long>((tiles + 7) / 8, (long long)WG_PER_CU * num_cus() / 8);

@@ -205,3 +205,29 @@ def test_wino_lstm_cell_conv(stif, sd, hw, pf):
     for g, (hn, cn) in zip(groups, refs):
         assert relmax(to_nchw(g["out"]), hn) < RTOL
         assert relmax(to_nchw(g["out2"]), cn) < RTOL
+
+
+@pytest.mark.parametrize("hw", [(10, 40), (4, 4), (33, 70), (128, 128)])
+def test_wino_offmask_groups_items(stif, hw, pf):
+    """Offset/mask conv launches as the model issues them (several weight sets x strided items;
+    f16x3: the all-couts k_wino_om kernel, border tiles, more tiles than workgroups) == the direct
+    fp32 kernel per group."""
+    L, ops = stif._lib, stif.ops
+    H, W = hw
+    G, N = 2, 3
+    xs = [rnd(N, 64, H, W, seed=40 + g) for g in range(G)]
+    ws = [rnd(216, 64, 3, 3, seed=50 + g, scale=0.05) for g in range(G)]
+    bs = [rnd(216, seed=60 + g) for g in range(G)]
+    src = torch.empty(G, N + 1, H, W, 64, device="cuda")          # item stride of N + 1 pixels maps
+    for g in range(G):
+        src[g, :N] = nhwc(xs[g])
+    out = torch.full((G, N, H, W, 216), float("nan"), device="cuda")
+    ops.conv2d([dict(layer=ops.pack_conv(ws[g], bs[g], L.PACK_WINO_OFFMASK | pf), in0=src[g, :N], out=out[g])
+                for g in range(G)], epi=L.EPI_OFFMASK)
+    for g in range(G):
+        ref = torch.empty(N, H, W, 216, device="cuda")
+        ops.conv2d([dict(layer=ops.pack_conv(ws[g], bs[g], L.PACK_OFFMASK), in0=nhwc(xs[g]), out=ref)],
+                   epi=L.EPI_OFFMASK)
+        a1, a2 = out[g].cpu().numpy(), ref.cpu().numpy()
+        assert np.isfinite(a1).all()
+        assert np.abs(a1 - a2).max() <= 1e-5 * np.abs(a2).max()
