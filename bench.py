@@ -52,6 +52,10 @@ def kernel_desc(kind, mfma="f32"):
     f16 = mfma == "f16x3"
     if kind[0] == "wino":
         _, ks, s, epi, in1, cout = kind
+        if f16 and epi == 4 and not in1:
+            return ("k_wino_om<4>", f"3x3 64->{cout} conv, EPI_OFFMASK, Winograd F(2x2,3x3) on split-fp16 MFMA, all "
+                    "couts per tile (3 fp16 products per fp32-class product); algorithmic = direct-conv FLOPs, peak = "
+                    "fp16 MFMA dense peak / 3 x 36/16", F16X3_PEAK_TFLOPS * WINO_GAIN)
         if f16:
             return (f"k_wino<{in1}, {epi}, 0, 1>", f"3x3 {64 * (2 if in1 else 1)}->{cout} conv, EPI_{EPI_NAMES[epi]}, "
                     "Winograd F(2x2,3x3) on split-fp16 MFMA (3 fp16 products per fp32-class product); algorithmic = "
@@ -134,6 +138,31 @@ class KernelTimer:
 
 
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E (MI355X_MICROARCH.md)
+
+
+def roofline(kname, kdesc, dom, peak_tflops, achieved_tflops, avg_ms, avg_flops, avg_bytes, n_launch, traffic):
+    """Roofline record of the dominant kernel.  The bound is the kernel's algorithmic intensity (direct
+    FLOPs / algorithmic HBM bytes per launch) against the ridge of the pipe it runs on (peak FLOP/s /
+    8 TB/s): below the ridge it is HBM-bound and `achieved` is algorithmic GB/s, above it MFMA-bound and
+    `achieved` is algorithmic TFLOP/s; both views are kept."""
+    gbps = avg_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms and avg_bytes else 0.0
+    intensity = avg_flops / avg_bytes if avg_bytes else float("inf")
+    ridge = peak_tflops * 1e12 / (HBM_PEAK_GBPS * 1e9)
+    hbm = intensity < ridge
+    rec = {"bound": "hbm" if hbm else "mfma", "kernel": f"{kname} ({kdesc})", "kind": list(dom)}
+    if hbm:
+        rec.update(achieved=round(gbps, 1), peak=HBM_PEAK_GBPS, unit="GB/s", frac=round(gbps / HBM_PEAK_GBPS, 4))
+    else:
+        rec.update(achieved=round(achieved_tflops, 3), peak=round(peak_tflops, 2), unit="TFLOP/s",
+                   frac=round(achieved_tflops / peak_tflops, 4))
+    rec.update(traffic=traffic, launches=n_launch, avg_launch_us=round(avg_ms * 1e3, 2),
+               flops_per_launch=avg_flops, algorithmic_bytes_per_launch=round(avg_bytes),
+               intensity_flop_per_byte=round(intensity, 1), ridge_flop_per_byte=round(ridge, 1),
+               mfma_view={"achieved": round(achieved_tflops, 3), "peak": round(peak_tflops, 2), "unit": "TFLOP/s",
+                          "frac": round(achieved_tflops / peak_tflops, 4)},
+               hbm_view={"achieved": round(gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(gbps / HBM_PEAK_GBPS, 4)})
+    return rec
 
 
 def hot_path_kernels(probe, mfma):
@@ -364,13 +393,8 @@ def main():
                        "parallelism": (f"sequence pair-sharded x{world}, boundary-frame features by "
                                        f"{'RCCL P2P halo exchange' if args.halo == 'exchange' else 'recompute'}"
                                        if world > 1 else "1 GPU")},
-            "roofline": {"bound": "mfma", "kernel": f"{kname} ({kdesc})", "kind": list(dom),
-                         "achieved": round(achieved, 3), "peak": round(peak, 2), "unit": "TFLOP/s",
-                         "frac": round(achieved / peak, 4), "traffic": traffic,
-                         "launches": n_launch, "avg_launch_us": round(avg_ms * 1e3, 2),
-                         "flops_per_launch": avg_flops,
-                         "algorithmic_bytes_per_launch": round(avg_bytes),
-                         "hbm_gbps_algorithmic": round(avg_bytes / (avg_ms * 1e-3) / 1e9, 1) if avg_ms else None},
+            "roofline": roofline(kname, kdesc, dom, peak, achieved, avg_ms, avg_flops, avg_bytes, n_launch,
+                                 traffic),
             "hot_path_kernels": hot,
         }
     if world == 1 and not args.no_extras:

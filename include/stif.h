@@ -144,6 +144,25 @@ int stif_dcn_v2_forward(const float* input, const float* weight, const float* bi
                         int dilation_h, int dilation_w, int deformable_group,
                         void* workspace, size_t workspace_bytes, void* stream);
 
+/* Drop-in for `_ext.dcn_v2_backward` (dcn_v2.h:39-52, vision.cpp:5; CUDA body dcn_v2_cuda.cu:204-335):
+ * the same NCHW tensors as stif_dcn_v2_forward plus grad_output [b, co, ho, wo]; writes grad_input
+ * [b,c,h,w], grad_offset [b, dg*2*kh*kw, ho, wo], grad_mask [b, dg*kh*kw, ho, wo], grad_weight
+ * [co,c,kh,kw] and grad_bias [co] (caller-allocated; all overwritten).  Per sample, as the reference:
+ * columns gradient = W^T grad_output (fp32 MFMA GEMM), the coordinate / mask gradients
+ * (modulated_deformable_col2im_coord semantics, one thread per group x tap x pixel), the input
+ * gradient scattered to the bilinear corners with fp32 atomics (modulated_deformable_col2im), the
+ * forward columns and grad_weight += grad_output columns^T, grad_bias += sum grad_output.
+ * workspace: at least stif_dcn_v2_backward_workspace_size bytes (c*kh*kw*ho*wo floats), 16-B aligned. */
+size_t stif_dcn_v2_backward_workspace_size(int batch, int channels, int height, int width, int channels_out,
+                                           int kernel_h, int kernel_w, int stride_h, int stride_w, int pad_h,
+                                           int pad_w, int dilation_h, int dilation_w, int deformable_group);
+int stif_dcn_v2_backward(const float* input, const float* weight, const float* bias, const float* offset,
+                         const float* mask, const float* grad_output, float* grad_input, float* grad_offset,
+                         float* grad_mask, float* grad_weight, float* grad_bias, int batch, int channels, int height,
+                         int width, int channels_out, int kernel_h, int kernel_w, int stride_h, int stride_w,
+                         int pad_h, int pad_w, int dilation_h, int dilation_w, int deformable_group, void* workspace,
+                         size_t workspace_bytes, void* stream);
+
 /* ---- implicit decoder (LunaTokis.decoding, Sakuya_arch_test.py:364-459) ---- */
 
 /* Assemble the decoder's LR source map [n,h,w,200] = [feat t0 | t1 | t2 | inp rgb0 rgb1 | 0 0]

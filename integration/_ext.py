@@ -4,8 +4,9 @@ Drop-in for the CUDA extension that ``codes/models/modules/DCNv2/setup.py`` buil
 ``codes/models/modules/DCNv2/dcn_v2.py:11`` imports (``import _ext as _backend``): put this
 directory ahead of the compiled ``_ext`` on ``sys.path`` (or ``PYTHONPATH``) and the reference's
 own ``dcn_v2.py`` -- ``_DCNv2``, ``dcn_v2_conv``, ``DCNv2``, ``DCN``, ``DCN_sep`` -- runs unchanged
-on ``stif_dcn_v2_forward`` (include/stif.h).  The engine is inference-only: the backward entry
-points raise, as ``dcn_v2_cpu.cpp`` does for the CPU build.
+on ``stif_dcn_v2_forward`` / ``stif_dcn_v2_backward`` (include/stif.h), training included (the
+autograd ``_DCNv2.backward`` calls ``dcn_v2_backward``).  PSROI pooling is not provided (STIF does
+not use ``DCNv2Pooling``).
 """
 import os
 import sys
@@ -23,9 +24,10 @@ _stif = stif_pkg.load()
 dcn_v2_forward = _stif.ops.dcn_v2_forward
 
 
-def dcn_v2_backward(*args, **kwargs):
-    """vision.cpp:5 -- not provided (inference engine)."""
-    raise NotImplementedError("dcn_v2_backward is not provided by stif_amd (inference only)")
+# vision.cpp:5 -- (input, weight, bias, offset, mask, grad_output, kernel_h, kernel_w, stride_h,
+# stride_w, pad_h, pad_w, dilation_h, dilation_w, deformable_group) -> [grad_input, grad_offset,
+# grad_mask, grad_weight, grad_bias]
+dcn_v2_backward = _stif.ops.dcn_v2_backward
 
 
 def dcn_v2_psroi_pooling_forward(*args, **kwargs):

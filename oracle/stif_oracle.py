@@ -147,6 +147,105 @@ def dcn_v2_forward(inp, weight, bias, offset, mask, kh, kw, sh, sw, ph, pw, dh, 
     return np.ascontiguousarray(out.transpose(0, 2, 1)).reshape(B, Co, Ho, Wo)
 
 
+def _dcn_sample_geometry(B, H, W, Ho, Wo, kh, kw, sh, sw, ph, pw, dh, dw, offset, dg, k):
+    """fp32 sampling coordinates of tap k (dcn_v2_im2col_cuda.cu:173-176, :216-235, :300-307):
+    h_im / w_im [B, dg, P], with the floor corners, fractions and the (-1, H) x (-1, W) gate."""
+    K = kh * kw
+    P = Ho * Wo
+    off = np.asarray(offset, F32).reshape(B, dg, K, 2, P)
+    i, j = divmod(k, kw)
+    h_in = np.repeat(np.arange(Ho) * sh - ph, Wo)[None, None]
+    w_in = np.tile(np.arange(Wo) * sw - pw, Ho)[None, None]
+    h_im = (h_in + i * dh).astype(F32) + off[:, :, k, 0]
+    w_im = (w_in + j * dw).astype(F32) + off[:, :, k, 1]
+    inside = (h_im > -1) & (w_im > -1) & (h_im < H) & (w_im < W)
+    h_low = np.floor(h_im)
+    w_low = np.floor(w_im)
+    lh = (h_im - h_low).astype(np.float64)     # fp32 subtraction, exact in float64
+    lw = (w_im - w_low).astype(np.float64)
+    return inside, h_low.astype(np.int64), w_low.astype(np.int64), lh, lw
+
+
+def dcn_v2_backward(inp, weight, bias, offset, mask, grad_out, kh, kw, sh, sw, ph, pw, dh, dw, dg,
+                    dtype=np.float64):
+    """Restatement of ``dcn_v2_cuda_backward`` (DCNv2/src/cuda/dcn_v2_cuda.cu:204-335), per sample:
+      columns = W^T . grad_out                                       (:274-277, Sgemm n/t)
+      grad_offset, grad_mask <- modulated_deformable_col2im_coord   (dcn_v2_im2col_cuda.cu:256-327):
+        per (group, tap, pixel): sum over the group's channels of
+          dmcn_get_coordinate_weight(h, w, im_c, dir) * col * mask   (:80-121; dir 0 = d/dh, 1 = d/dw)
+          and, for the mask, col * dmcn_im2col_bilinear(im_c, h, w)   (:314-317)
+        with (h, w) outside (-1, H) x (-1, W) contributing nothing (:308-313);
+      grad_input <- modulated_deformable_col2im (:197-254): col * mask scattered to the in-bounds
+        bilinear corners with dmcn_get_gradient_weight (:55-78);
+      grad_weight += grad_out . columns_fwd^T (:308-315, columns_fwd = the forward im2col);
+      grad_bias += sum over pixels of grad_out (:320-326).
+    Returns (grad_input, grad_offset, grad_mask, grad_weight, grad_bias) in the reference's shapes
+    (vision.cpp dcn_v2_backward order).  ``mask`` is the modulation after the sigmoid, as the
+    reference's backend receives it."""
+    inp = np.asarray(inp, dtype)
+    B, C, H, W = inp.shape
+    Co = weight.shape[0]
+    Ho = (H + 2 * ph - (dh * (kh - 1) + 1)) // sh + 1
+    Wo = (W + 2 * pw - (dw * (kw - 1) + 1)) // sw + 1
+    K = kh * kw
+    cpg = C // dg
+    P = Ho * Wo
+    go = np.asarray(grad_out, dtype).reshape(B, Co, P)
+    wm = np.asarray(weight, dtype).reshape(Co, C, K)
+    msk = np.asarray(mask, dtype).reshape(B, dg, K, P)
+    img = inp.reshape(B, dg, cpg, H * W)
+    cols = np.einsum("ock,bop->bckp", wm, go).reshape(B, dg, cpg, K, P)     # columns per sample
+    g_in = np.zeros((B, dg, cpg, H * W), dtype)
+    g_off = np.zeros((B, dg, K, 2, P), dtype)
+    g_msk = np.zeros((B, dg, K, P), dtype)
+    bi = np.arange(B)[:, None, None, None]
+    gi = np.arange(dg)[None, :, None, None]
+    ci = np.arange(cpg)[None, None, :, None]
+    for k in range(K):
+        inside, h_low, w_low, lh, lw = _dcn_sample_geometry(B, H, W, Ho, Wo, kh, kw, sh, sw, ph, pw, dh, dw,
+                                                            offset, dg, k)
+        hh, hw = 1 - lh, 1 - lw
+        h_high, w_high = h_low + 1, w_low + 1
+        corners = ((h_low, w_low, (h_low >= 0) & (w_low >= 0), hh * hw, -hw, -hh),
+                   (h_low, w_high, (h_low >= 0) & (w_high <= W - 1), hh * lw, -lw, hh),
+                   (h_high, w_low, (h_high <= H - 1) & (w_low >= 0), lh * hw, hw, -lh),
+                   (h_high, w_high, (h_high <= H - 1) & (w_high <= W - 1), lh * lw, lw, lh))
+        col = cols[:, :, :, k]                                  # [B, dg, cpg, P]
+        m = np.where(inside, msk[:, :, k], 0)                   # [B, dg, P]
+        gh = gw = bil = 0
+        for hc, wc, ok, wt, dwh, dww in corners:
+            ok = ok & inside
+            idx = np.clip(hc, 0, H - 1) * W + np.clip(wc, 0, W - 1)                 # [B, dg, P]
+            v = img[bi, gi, ci, idx[:, :, None, :]]                                   # [B, dg, cpg, P]
+            v = np.where(ok[:, :, None], v, 0)
+            bil = bil + v * wt[:, :, None]
+            gh = gh + v * dwh[:, :, None]
+            gw = gw + v * dww[:, :, None]
+            # col2im: col * mask * bilinear weight into the in-bounds corner
+            contrib = col * (np.where(ok, wt, 0) * m)[:, :, None]
+            np.add.at(g_in, (bi, gi, ci, idx[:, :, None, :]), contrib)
+        g_off[:, :, k, 0] = (gh * col).sum(2) * m
+        g_off[:, :, k, 1] = (gw * col).sum(2) * m
+        g_msk[:, :, k] = np.where(inside, (bil * col).sum(2), 0)
+    cols_fwd = np.empty((B, dg, cpg, K, P), dtype)
+    for k in range(K):
+        inside, h_low, w_low, lh, lw = _dcn_sample_geometry(B, H, W, Ho, Wo, kh, kw, sh, sw, ph, pw, dh, dw,
+                                                            offset, dg, k)
+        val = 0
+        for hc, wc, ok, wt in ((h_low, w_low, (h_low >= 0) & (w_low >= 0), (1 - lh) * (1 - lw)),
+                               (h_low, w_low + 1, (h_low >= 0) & (w_low + 1 <= W - 1), (1 - lh) * lw),
+                               (h_low + 1, w_low, (h_low + 1 <= H - 1) & (w_low >= 0), lh * (1 - lw)),
+                               (h_low + 1, w_low + 1, (h_low + 1 <= H - 1) & (w_low + 1 <= W - 1), lh * lw)):
+            idx = np.clip(hc, 0, H - 1) * W + np.clip(wc, 0, W - 1)
+            v = np.where(ok[:, :, None], img[bi, gi, ci, idx[:, :, None, :]], 0)
+            val = val + v * wt[:, :, None]
+        cols_fwd[:, :, :, k] = val * np.where(inside, msk[:, :, k], 0)[:, :, None]
+    g_w = np.einsum("bop,bckp->ock", go, cols_fwd.reshape(B, C, K, P)).reshape(weight.shape)
+    g_b = go.sum(axis=(0, 2))
+    return (g_in.reshape(B, C, H, W), g_off.reshape(B, dg * K * 2, Ho, Wo), g_msk.reshape(B, dg * K, Ho, Wo),
+            g_w, g_b)
+
+
 def dcn_sep(inp, fea, sd, name, groups=8, dtype=np.float64):
     """DCN_sep.forward (DCNv2/dcn_v2.py:127-140): offsets/mask from a separate feature."""
     out = conv2d(fea, sd[name + ".conv_offset_mask.weight"], sd[name + ".conv_offset_mask.bias"], dtype=dtype)

@@ -63,6 +63,8 @@ EXPORTS = {
     "stif_dcn_nhwc": (C.c_int, [C.POINTER(DcnArgs), _P]),
     "stif_dcn_v2_workspace_size": (C.c_size_t, [C.c_int] * 14),
     "stif_dcn_v2_forward": (C.c_int, [_P] * 6 + [C.c_int] * 14 + [_P, C.c_size_t, _P]),
+    "stif_dcn_v2_backward_workspace_size": (C.c_size_t, [C.c_int] * 14),
+    "stif_dcn_v2_backward": (C.c_int, [_P] * 11 + [C.c_int] * 14 + [_P, C.c_size_t, _P]),
     "stif_dec_pack_lr": (C.c_int, [_P, _P, _P, _P, _P, C.c_int, C.c_int, C.c_int, _P]),
     "stif_dec_stage1": (C.c_int, [_P, _P, C.POINTER(DecTables), C.POINTER(DecImage), _P, _P, _P] + [C.c_int] * 5
                         + [_P]),

@@ -439,6 +439,134 @@ __global__ __launch_bounds__(256) void k_pack_dcn_w(const float* __restrict__ w,
   if (i < 64) bp[i] = b[i];
 }
 
+// ------------------------------------------------------------------ backward (drop-in _ext.dcn_v2_backward)
+// C[m][n] = sum_k A(m, k) B(k, n) (+ C[m][n] when acc): A(m, k) = A[m sam + k sak], B(k, n) = B[k sbk + n sbn];
+// 64 x 64 tile per workgroup on fp32 MFMA (exact fp32 products, fp32 sums); the tile loads follow the
+// unit-stride dimension of each operand so they coalesce.
+__global__ __launch_bounds__(256) void k_sgemm(const float* __restrict__ A, long long sam, long long sak,
+                                               const float* __restrict__ Bm, long long sbk, long long sbn,
+                                               float* __restrict__ Cm, long long ldc, int M, int N, int K, int acc_c) {
+  constexpr int LS = 12;
+  __shared__ __attribute__((aligned(16))) float sA[64 * LS];
+  __shared__ __attribute__((aligned(16))) float sB[64 * LS];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l32 = lane & 31, hf = lane >> 5;
+  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+  const int mi = wv >> 1, ni = wv & 1;
+  const bool a_m = sam == 1, b_n = sbn == 1;
+  f32x16 acc = f32x16{0};
+  for (int k0 = 0; k0 < K; k0 += 8) {
+    for (int e = tid; e < 512; e += 256) {
+      const int r = a_m ? (e & 63) : (e >> 3), kk = a_m ? (e >> 6) : (e & 7);
+      const int m = m0 + r, k = k0 + kk;
+      sA[r * LS + kk] = (m < M && k < K) ? A[(long long)m * sam + (long long)k * sak] : 0.f;
+      const int c = b_n ? (e & 63) : (e >> 3), kb = b_n ? (e >> 6) : (e & 7);
+      const int n = n0 + c, kq = k0 + kb;
+      sB[c * LS + kb] = (kq < K && n < N) ? Bm[(long long)kq * sbk + (long long)n * sbn] : 0.f;
+    }
+    __syncthreads();
+    const f32x4 av = ld4(sA + (mi * 32 + l32) * LS + hf * 4);
+    const f32x4 bv = ld4(sB + (ni * 32 + l32) * LS + hf * 4);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc = mfma32(av[q], bv[q], acc);
+    __syncthreads();
+  }
+  const int n = n0 + ni * 32 + l32;
+  if (n >= N) return;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = m0 + mi * 32 + mfma_row(r, lane);
+    if (m < M) {
+      float* c = Cm + (long long)m * ldc + n;
+      *c = acc_c ? *c + acc[r] : acc[r];
+    }
+  }
+}
+
+struct DcnGeom {
+  int C, H, W, Ho, Wo, kh, kw, sh, sw, ph, pw, dh, dw, dg;
+};
+
+// sampling position of tap k at output pixel p and its (-1, H) x (-1, W) gate (dcn_v2_im2col_cuda.cu:173-176)
+STIF_DEV bool dcn_pos(const DcnGeom& G, const float* off, int g, int k, int p, float& h, float& w) {
+  const int K = G.kh * G.kw, P = G.Ho * G.Wo;
+  const int ho = p / G.Wo, wo = p - ho * G.Wo, i = k / G.kw, j = k - i * G.kw;
+  h = (float)(ho * G.sh - G.ph + i * G.dh) + off[((size_t)g * 2 * K + 2 * k) * P + p];
+  w = (float)(wo * G.sw - G.pw + j * G.dw) + off[((size_t)g * 2 * K + 2 * k + 1) * P + p];
+  return h > -1.f && w > -1.f && h < (float)G.H && w < (float)G.W;
+}
+
+// grad_offset / grad_mask of one sample (modulated_deformable_col2im_coord, dcn_v2_im2col_cuda.cu:256-327):
+// one thread per (group, tap, pixel) computes both coordinate gradients and the mask gradient in one
+// pass over the group's channels (the reference runs one thread per offset channel)
+__global__ __launch_bounds__(256) void k_dcn_bwd_coord(const float* __restrict__ colg, const float* __restrict__ im,
+                                                       const float* __restrict__ off, const float* __restrict__ msk,
+                                                       float* __restrict__ goff, float* __restrict__ gmsk, DcnGeom G) {
+  const int K = G.kh * G.kw, P = G.Ho * G.Wo, cpg = G.C / G.dg;
+  const long long n = (long long)G.dg * K * P;
+  for (long long idx = (long long)blockIdx.x * 256 + threadIdx.x; idx < n; idx += (long long)gridDim.x * 256) {
+    const int p = (int)(idx % P), k = (int)((idx / P) % K), g = (int)(idx / ((long long)P * K));
+    float h, w, vh = 0.f, vw = 0.f, vm = 0.f;
+    if (dcn_pos(G, off, g, k, p, h, w)) {
+      const int hl = (int)floorf(h), wl = (int)floorf(w);
+      const float lh = h - (float)hl, lw = w - (float)wl, hh = 1.f - lh, hw = 1.f - lw;
+      const bool b1 = hl >= 0 && wl >= 0, b2 = hl >= 0 && wl + 1 <= G.W - 1;
+      const bool b3 = hl + 1 <= G.H - 1 && wl >= 0, b4 = hl + 1 <= G.H - 1 && wl + 1 <= G.W - 1;
+      const size_t o1 = (size_t)hl * G.W + wl;
+      for (int c = 0; c < cpg; ++c) {
+        const float* img = im + (size_t)(g * cpg + c) * G.H * G.W;
+        const float v1 = b1 ? img[o1] : 0.f, v2 = b2 ? img[o1 + 1] : 0.f;
+        const float v3 = b3 ? img[o1 + G.W] : 0.f, v4 = b4 ? img[o1 + G.W + 1] : 0.f;
+        const float col = colg[((size_t)(g * cpg + c) * K + k) * P + p];
+        vh += col * (-hw * v1 - lw * v2 + hw * v3 + lw * v4);
+        vw += col * (-hh * v1 + hh * v2 - lh * v3 + lh * v4);
+        vm += col * (hh * hw * v1 + hh * lw * v2 + lh * hw * v3 + lh * lw * v4);
+      }
+    }
+    const float m = msk[((size_t)g * K + k) * P + p];
+    goff[((size_t)g * 2 * K + 2 * k) * P + p] = vh * m;
+    goff[((size_t)g * 2 * K + 2 * k + 1) * P + p] = vw * m;
+    gmsk[((size_t)g * K + k) * P + p] = vm;
+  }
+}
+
+// grad_input of one sample (modulated_deformable_col2im, dcn_v2_im2col_cuda.cu:197-254): col * mask
+// added into the in-bounds bilinear corners (hardware fp32 atomics; the reference uses atomicAdd too)
+__global__ __launch_bounds__(256) void k_dcn_bwd_col2im(const float* __restrict__ colg, const float* __restrict__ off,
+                                                        const float* __restrict__ msk, float* __restrict__ gin,
+                                                        DcnGeom G) {
+  const int K = G.kh * G.kw, P = G.Ho * G.Wo, cpg = G.C / G.dg;
+  const long long n = (long long)G.C * K * P;
+  for (long long idx = (long long)blockIdx.x * 256 + threadIdx.x; idx < n; idx += (long long)gridDim.x * 256) {
+    const int p = (int)(idx % P), k = (int)((idx / P) % K), c = (int)(idx / ((long long)P * K));
+    const int g = c / cpg;
+    float h, w;
+    if (!dcn_pos(G, off, g, k, p, h, w)) continue;
+    const float coef = colg[idx] * msk[((size_t)g * K + k) * P + p];
+    const int hl = (int)floorf(h), wl = (int)floorf(w);
+    const float lh = h - (float)hl, lw = w - (float)wl, hh = 1.f - lh, hw = 1.f - lw;
+    float* gi = gin + (size_t)c * G.H * G.W;
+    if (hl >= 0 && wl >= 0) unsafeAtomicAdd(gi + (size_t)hl * G.W + wl, hh * hw * coef);
+    if (hl >= 0 && wl + 1 <= G.W - 1) unsafeAtomicAdd(gi + (size_t)hl * G.W + wl + 1, hh * lw * coef);
+    if (hl + 1 <= G.H - 1 && wl >= 0) unsafeAtomicAdd(gi + (size_t)(hl + 1) * G.W + wl, lh * hw * coef);
+    if (hl + 1 <= G.H - 1 && wl + 1 <= G.W - 1) unsafeAtomicAdd(gi + (size_t)(hl + 1) * G.W + wl + 1, lh * lw * coef);
+  }
+}
+
+// grad_bias[co] += sum_p grad_out[co][p] of one sample (dcn_v2_cuda.cu:320-326); one workgroup per co
+__global__ __launch_bounds__(256) void k_dcn_bwd_bias(const float* __restrict__ go, float* __restrict__ gb, int P) {
+  __shared__ float red[256];
+  const int co = blockIdx.x;
+  float s = 0.f;
+  for (int p = threadIdx.x; p < P; p += 256) s += go[(size_t)co * P + p];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if (threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) gb[co] += red[0];
+}
+
 bool stif_dcn_shape(int channels, int channels_out, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw,
                     int dg, int height, int width) {
   return channels == 64 && channels_out == 64 && kh == 3 && kw == 3 && sh == 1 && sw == 1 && ph == 1 && pw == 1 &&
@@ -565,6 +693,80 @@ extern "C" int stif_dcn_v2_forward(const float* input, const float* weight, cons
     hipLaunchKernelGGL(k_gemm_bias, grid, dim3(256), 0, st, weight, cols, bias, output + (size_t)b * channels_out * N,
                        channels_out, K, N);
     rc = stif_check_launch("dcn_v2_forward/gemm");
+    if (rc) return rc;
+  }
+  return STIF_OK;
+}
+
+extern "C" size_t stif_dcn_v2_backward_workspace_size(int batch, int channels, int height, int width,
+                                                      int channels_out, int kernel_h, int kernel_w, int stride_h,
+                                                      int stride_w, int pad_h, int pad_w, int dilation_h,
+                                                      int dilation_w, int deformable_group) {
+  (void)batch;
+  (void)channels_out;
+  (void)deformable_group;
+  int Ho, Wo;
+  if (!dcn_dims(height, width, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w, dilation_h, dilation_w, &Ho,
+                &Wo))
+    return 0;
+  // the reference's per-sample columns buffer (dcn_v2_cuda.cu:242): first the columns gradient, then
+  // the forward columns for grad_weight
+  return (size_t)channels * kernel_h * kernel_w * Ho * Wo * sizeof(float);
+}
+
+extern "C" int stif_dcn_v2_backward(const float* input, const float* weight, const float* bias, const float* offset,
+                                    const float* mask, const float* grad_output, float* grad_input, float* grad_offset,
+                                    float* grad_mask, float* grad_weight, float* grad_bias, int batch, int channels,
+                                    int height, int width, int channels_out, int kernel_h, int kernel_w,
+                                    int stride_h, int stride_w, int pad_h, int pad_w, int dilation_h, int dilation_w,
+                                    int deformable_group, void* workspace, size_t workspace_bytes, void* stream) {
+  // argument checks mirror dcn_v2_cuda_backward's (dcn_v2_cuda.cu:216-240)
+  if (!input || !weight || !bias || !offset || !mask || !grad_output || !grad_input || !grad_offset || !grad_mask ||
+      !grad_weight || !grad_bias)
+    return stif_fail(STIF_E_INVALID, "dcn_v2_backward: null tensor");
+  if (batch < 1 || channels < 1 || channels_out < 1 || kernel_h < 1 || kernel_w < 1 || stride_h < 1 ||
+      stride_w < 1 || dilation_h < 1 || dilation_w < 1 || deformable_group < 1 || channels % deformable_group)
+    return stif_fail(STIF_E_INVALID, "dcn_v2_backward: invalid shape arguments");
+  int Ho, Wo;
+  if (!dcn_dims(height, width, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w, dilation_h, dilation_w, &Ho,
+                &Wo))
+    return stif_fail(STIF_E_INVALID, "dcn_v2_backward: empty output");
+  const size_t need = stif_dcn_v2_backward_workspace_size(batch, channels, height, width, channels_out, kernel_h,
+                                                          kernel_w, stride_h, stride_w, pad_h, pad_w, dilation_h,
+                                                          dilation_w, deformable_group);
+  if (!workspace || workspace_bytes < need) return stif_fail(STIF_E_WORKSPACE, "dcn_v2_backward: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  const int K = kernel_h * kernel_w, P = Ho * Wo, CK = channels * K;
+  const size_t in_n = (size_t)channels * height * width;
+  if (hipMemsetAsync(grad_input, 0, (size_t)batch * in_n * sizeof(float), st) != hipSuccess ||
+      hipMemsetAsync(grad_weight, 0, (size_t)channels_out * CK * sizeof(float), st) != hipSuccess ||
+      hipMemsetAsync(grad_bias, 0, (size_t)channels_out * sizeof(float), st) != hipSuccess)
+    return stif_fail(STIF_E_LAUNCH, "dcn_v2_backward: memset failed");
+  const DcnGeom G{channels, height, width, Ho, Wo, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w,
+                  dilation_h, dilation_w, deformable_group};
+  float* cols = (float*)workspace;
+  auto blocks = [](long long n) { return (unsigned)std::min<long long>((n + 255) / 256, 1 << 20); };
+  for (int b = 0; b < batch; ++b) {
+    const float* in_b = input + (size_t)b * in_n;
+    const float* off_b = offset + (size_t)b * deformable_group * 2 * K * P;
+    const float* msk_b = mask + (size_t)b * deformable_group * K * P;
+    const float* go_b = grad_output + (size_t)b * channels_out * P;
+    // columns gradient [c*K + k][p] = sum_co W[co][c*K + k] grad_out[co][p] (dcn_v2_cuda.cu:274-277)
+    hipLaunchKernelGGL(k_sgemm, dim3((P + 63) / 64, (CK + 63) / 64), dim3(256), 0, st, weight, 1LL, (long long)CK,
+                       go_b, (long long)P, 1LL, cols, (long long)P, CK, P, channels_out, 0);
+    hipLaunchKernelGGL(k_dcn_bwd_coord, dim3(blocks((long long)deformable_group * K * P)), dim3(256), 0, st, cols,
+                       in_b, off_b, msk_b, grad_offset + (size_t)b * deformable_group * 2 * K * P,
+                       grad_mask + (size_t)b * deformable_group * K * P, G);
+    hipLaunchKernelGGL(k_dcn_bwd_col2im, dim3(blocks((long long)CK * P)), dim3(256), 0, st, cols, off_b, msk_b,
+                       grad_input + (size_t)b * in_n, G);
+    // forward columns, then grad_weight[co][c*K + k] += sum_p grad_out[co][p] cols[c*K + k][p] (:308-315)
+    hipLaunchKernelGGL(k_im2col, dim3(blocks((long long)channels * P)), dim3(256), 0, st, in_b, off_b, msk_b, cols, 1,
+                       channels, height, width, Ho, Wo, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w,
+                       dilation_h, dilation_w, deformable_group);
+    hipLaunchKernelGGL(k_sgemm, dim3((CK + 63) / 64, (channels_out + 63) / 64), dim3(256), 0, st, go_b, (long long)P,
+                       1LL, cols, 1LL, (long long)P, grad_weight, (long long)CK, channels_out, CK, P, 1);
+    hipLaunchKernelGGL(k_dcn_bwd_bias, dim3(channels_out), dim3(256), 0, st, go_b, grad_bias, P);
+    const int rc = stif_check_launch("dcn_v2_backward");
     if (rc) return rc;
   }
   return STIF_OK;

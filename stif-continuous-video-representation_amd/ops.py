@@ -239,6 +239,33 @@ def dcn_v2_forward(input, weight, bias, offset, mask, kernel_h, kernel_w, stride
     return out
 
 
+def dcn_v2_backward(input, weight, bias, offset, mask, grad_output, kernel_h, kernel_w, stride_h, stride_w, pad_h,
+                    pad_w, dilation_h, dilation_w, deformable_group):
+    """Drop-in for ``_ext.dcn_v2_backward`` (DCNv2/src/dcn_v2.h:39-52): returns new tensors
+    (grad_input, grad_offset, grad_mask, grad_weight, grad_bias) in that order, as
+    ``_DCNv2.backward`` (DCNv2/dcn_v2.py:31-45) unpacks them."""
+    ts = (input, weight, bias, offset, mask, grad_output)
+    for t in ts:
+        if not (t.is_cuda and t.dtype == torch.float32):
+            raise RuntimeError("dcn_v2_backward: tensors must be float32 on the GPU")
+    input, weight, bias, offset, mask, grad_output = (t.contiguous() for t in ts)
+    b, c, h, w = input.shape
+    co, ci, kh, kw = weight.shape
+    if (kh, kw) != (kernel_h, kernel_w):
+        raise RuntimeError(f"Input shape and kernel shape wont match: ({kernel_h} x {kernel_w} vs {kh} x {kw}).")
+    if ci != c:
+        raise RuntimeError(f"Input shape and kernel channels wont match: ({c} vs {ci}).")
+    grads = [torch.empty_like(t) for t in (input, offset, mask, weight, bias)]
+    lib = L.lib()
+    dims = (b, c, h, w, co, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w, dilation_h, dilation_w,
+            deformable_group)
+    nbytes = lib.stif_dcn_v2_backward_workspace_size(*dims)
+    ws = torch.empty(max(nbytes // 4, 1), device=input.device, dtype=torch.float32)
+    L.check(lib.stif_dcn_v2_backward(*[_vp(t) for t in (input, weight, bias, offset, mask, grad_output)],
+                                     *[_vp(g) for g in grads], *dims, _vp(ws), nbytes, _stream()), "dcn_v2_backward")
+    return tuple(grads)
+
+
 class DecTablesDev:
     """Device copies of coords.dec_tables(h, w, HH, WW[, shift]) + the C struct pointing at them.
     With a shift (local ensemble) the HR remap tables are set too."""

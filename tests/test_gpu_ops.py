@@ -261,8 +261,76 @@ def test_ext_shim_dcn_sep_matches_reference(sd, golden):
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).cuda()
     out = ext.dcn_v2_forward(T(inp), T(sd[p + ".weight"]), T(sd[p + ".bias"]), offset, mask, 3, 3, 1, 1, 1, 1, 1, 1, 8)
     assert relmax(out, g["dcnsep_out"]) < 1e-4
+    assert callable(ext.dcn_v2_backward)
     with pytest.raises(NotImplementedError):
-        ext.dcn_v2_backward()
+        ext.dcn_v2_psroi_pooling_forward()
+
+
+DCN_BWD_CASES = [
+    # the reference's gradcheck configuration (DCNv2/test.py:15-19,69-103)
+    dict(B=2, C=2, H=4, W=4, Co=2, k=3, s=1, p=1, d=1, dg=1, seed=1),
+    # the STIF DCN_sep shape (64 -> 64, 8 groups) on a small map, far offsets and gate boundaries
+    dict(B=2, C=64, H=13, W=21, Co=64, k=3, s=1, p=1, d=1, dg=8, seed=2),
+    # stride 2 / dilation 2 / 1x1 / several groups / non-square kernels of the drop-in's shape classes
+    dict(B=1, C=6, H=11, W=9, Co=5, k=3, s=2, p=2, d=2, dg=3, seed=3),
+    dict(B=3, C=4, H=7, W=10, Co=3, k=1, s=1, p=0, d=1, dg=2, seed=4),
+]
+
+
+@pytest.mark.parametrize("case", DCN_BWD_CASES)
+def test_dcn_v2_backward_dropin_matches_oracle(ops, case):
+    """stif_dcn_v2_backward (drop-in for _ext.dcn_v2_backward) == the oracle's restatement of
+    dcn_v2_cuda_backward, every gradient, relative to its max (fp32 GEMMs and fp32 atomics vs float64)."""
+    B, C, H, W, Co, k, s, p, d, dg = (case[x] for x in ("B", "C", "H", "W", "Co", "k", "s", "p", "d", "dg"))
+    rng = np.random.default_rng(case["seed"])
+    Ho = (H + 2 * p - (d * (k - 1) + 1)) // s + 1
+    Wo = (W + 2 * p - (d * (k - 1) + 1)) // s + 1
+    x = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    off = (rng.standard_normal((B, dg * 2 * k * k, Ho, Wo)) * 3).astype(np.float32)
+    off[0, 0, 0, 0] = -1.0                                  # gate boundary: h_im exactly -1 (not sampled)
+    msk = (1 / (1 + np.exp(-rng.standard_normal((B, dg * k * k, Ho, Wo))))).astype(np.float32)
+    w = (rng.standard_normal((Co, C, k, k)) * 0.1).astype(np.float32)
+    b = rng.standard_normal(Co).astype(np.float32)
+    go = rng.standard_normal((B, Co, Ho, Wo)).astype(np.float32)
+    dims = (k, k, s, s, p, p, d, d, dg)
+    ref = O.dcn_v2_backward(x, w, b, off, msk, go, *dims)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    got = ops.dcn_v2_backward(T(x), T(w), T(b), T(off), T(msk), T(go), *dims)
+    for name, g, r in zip(("input", "offset", "mask", "weight", "bias"), got, ref):
+        assert tuple(g.shape) == r.shape, name
+        assert relmax(g, r) < 2e-5, name
+
+
+def test_dcn_v2_backward_through_reference_autograd_wiring(ops):
+    """_DCNv2 (DCNv2/dcn_v2.py:15-45) wiring -- forward = _ext.dcn_v2_forward, backward =
+    _ext.dcn_v2_backward -- in a torch.autograd.Function: the gradients reaching the inputs of
+    dcn_v2_conv(input, offset, sigmoid(m), weight, bias) match the oracle (sigmoid chain rule by torch)."""
+    class F(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, inp, off, msk, wt, bs):
+            ctx.save_for_backward(inp, off, msk, wt, bs)
+            return ops.dcn_v2_forward(inp, wt, bs, off, msk, 3, 3, 1, 1, 1, 1, 1, 1, 2)
+
+        @staticmethod
+        def backward(ctx, gout):
+            inp, off, msk, wt, bs = ctx.saved_tensors
+            gi, goff, gm, gw, gb = ops.dcn_v2_backward(inp, wt, bs, off, msk, gout, 3, 3, 1, 1, 1, 1, 1, 1, 2)
+            return gi, goff, gm, gw, gb
+
+    rng = np.random.default_rng(9)
+    x = torch.tensor(rng.standard_normal((2, 4, 6, 7)), dtype=torch.float32, device="cuda", requires_grad=True)
+    off = torch.tensor(rng.standard_normal((2, 36, 6, 7)) * 2, dtype=torch.float32, device="cuda", requires_grad=True)
+    m = torch.tensor(rng.standard_normal((2, 18, 6, 7)), dtype=torch.float32, device="cuda", requires_grad=True)
+    wt = torch.tensor(rng.standard_normal((3, 4, 3, 3)) * 0.2, dtype=torch.float32, device="cuda", requires_grad=True)
+    bs = torch.tensor(rng.standard_normal(3), dtype=torch.float32, device="cuda", requires_grad=True)
+    go = torch.tensor(rng.standard_normal((2, 3, 6, 7)), dtype=torch.float32, device="cuda")
+    F.apply(x, off, torch.sigmoid(m), wt, bs).backward(go)
+    sig = 1 / (1 + np.exp(-m.detach().cpu().numpy().astype(np.float64)))
+    gi, goff, gm, gw, gb = O.dcn_v2_backward(x.detach().cpu().numpy(), wt.detach().cpu().numpy(),
+                                             bs.detach().cpu().numpy(), off.detach().cpu().numpy(), sig,
+                                             go.cpu().numpy(), 3, 3, 1, 1, 1, 1, 1, 1, 2)
+    for t, r in ((x, gi), (off, goff), (m, gm * sig * (1 - sig)), (wt, gw), (bs, gb)):
+        assert relmax(t.grad, r) < 2e-5
 
 
 @pytest.mark.parametrize("hw", [(33, 70), (64, 64)])

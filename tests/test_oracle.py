@@ -133,3 +133,50 @@ def test_oracle_imresize_matches_reference():
     assert (s0, s1) == tuple(h["sym_37_19"])
     for k in ("37x50", "64x90", "21x33"):
         assert np.abs(O.imresize_np(h["img_" + k], 0.5) - h["half_" + k]).max() < 1e-3
+
+
+def _dcn_fd_case(seed, B=2, C=2, H=4, W=4, Co=2, dg=1, k=3, s=1, p=1, d=1):
+    """DCNv2/test.py:69-103 check_gradient_dconv inputs: input U[0,1)*0.01, offset N(0,1)*2,
+    mask sigmoid(U[0,1)), weight N(0,1), bias U[0,1)."""
+    rng = np.random.default_rng(seed)
+    Ho = (H + 2 * p - (d * (k - 1) + 1)) // s + 1
+    Wo = (W + 2 * p - (d * (k - 1) + 1)) // s + 1
+    x = rng.random((B, C, H, W)) * 0.01
+    off = (rng.standard_normal((B, dg * 2 * k * k, Ho, Wo)) * 2).astype(np.float32)
+    msk = 1 / (1 + np.exp(-rng.random((B, dg * k * k, Ho, Wo))))
+    w = rng.standard_normal((Co, C, k, k))
+    b = rng.random(Co)
+    go = rng.standard_normal((B, Co, Ho, Wo))
+    return x, w, b, off, msk, go, (k, k, s, s, p, p, d, d, dg)
+
+
+@pytest.mark.parametrize("case", [dict(seed=3), dict(seed=4, dg=2, C=4, Co=3),
+                                  dict(seed=5, H=6, W=5, s=2, d=2, p=2, C=2, Co=2)])
+def test_dcn_backward_oracle_matches_finite_differences(case):
+    """The backward restatement (dcn_v2_cuda_backward) against central differences of the forward
+    restatement at the reference's own gradcheck configuration and tolerances (DCNv2/test.py:69-103:
+    eps 1e-3, atol 1e-4, rtol 1e-2), over every input of dcn_v2_conv."""
+    x, w, b, off, msk, go, dims = _dcn_fd_case(**case)
+    gi, goff, gm, gw, gb = O.dcn_v2_backward(x, w, b, off, msk, go, *dims)
+    f = lambda x_, w_, b_, o_, m_: float((O.dcn_v2_forward(x_, w_, b_, o_, m_, *dims) * go).sum())
+    args = [x, w, b, off, msk]
+
+    def fd(ai, eps):
+        num = np.zeros(args[ai].shape)
+        for idx in np.ndindex(args[ai].shape):
+            ap, am = [a.copy() for a in args], [a.copy() for a in args]
+            ap[ai][idx] += eps
+            am[ai][idx] -= eps
+            num[idx] = (f(*ap) - f(*am)) / (2 * eps)
+        return num
+    for ai, g in zip(range(5), (gi, gw, gb, goff, gm)):
+        num = fd(ai, 1e-3)
+        tol = dict(atol=1e-4 * max(1.0, np.abs(num).max()), rtol=1e-2)
+        if ai == 3:
+            # the output is piecewise bilinear in the offsets: a sample within eps of a cell edge or of
+            # the (-1, H) gate has no derivative there; such elements are the ones whose difference
+            # quotient changes with eps (at most a few of them)
+            smooth = np.isclose(num, fd(ai, 2.5e-4), **tol)
+            assert smooth.mean() > 0.98
+            g, num = g[smooth], num[smooth]
+        np.testing.assert_allclose(g, num, **tol)
