@@ -39,7 +39,8 @@ def _item_stride(ts: Sequence[Optional[torch.Tensor]], what: str) -> int:
         if t.dtype != torch.float32 or not t.is_cuda:
             raise ValueError(f"{what}: expected float32 CUDA tensors")
         _, h, w, c = t.shape
-        if t.stride(3) != 1 or t.stride(2) != c or t.stride(1) != w * c:
+        # strides of size-1 dims never address anything
+        if (c > 1 and t.stride(3) != 1) or (w > 1 and t.stride(2) != c) or (h > 1 and t.stride(1) != w * c):
             raise ValueError(f"{what}: pixels of an item must be contiguous NHWC")
     return strides.pop() if strides else 0
 
