@@ -16,11 +16,6 @@
 #include "stif.h"
 #include "abi_util.h"
 
-// vectorised offset/mask loads in the f16x3 kernel (C1 L1 shape: 446 -> 432 us); DCN_OM_SCALAR
-// builds the per-value loads for comparison
-#ifndef DCN_OM_SCALAR
-#define DCN_OM_VEC 1
-#endif
 
 namespace {
 
@@ -67,13 +62,7 @@ __global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l32 = lane & 31, hf = lane >> 5;
   const int H = a.H, W = a.W;
   const int tiles_x = (W + 31) >> 5;
-#ifdef DCN_XCD
-  // kernel experiment: XCD x (workgroups b = x mod 8) takes a contiguous range of spatial tiles
-  const int nbx = gridDim.x;
-  const int bx = (nbx & 7) ? (int)blockIdx.x : (int)(blockIdx.x & 7) * (nbx >> 3) + (int)(blockIdx.x >> 3);
-#else
   const int bx = blockIdx.x;
-#endif
   const int tx = bx % tiles_x, ty = bx / tiles_x;
   const int g = blockIdx.z / a.nitems, n = blockIdx.z - g * a.nitems;
   const float* in = a.in[g] + (size_t)n * a.in_item;
@@ -88,9 +77,6 @@ __global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
       __builtin_amdgcn_make_buffer_rsrc((void*)in, (short)0, (int)((size_t)H * W * 64 * 4), 0x00020000);
 
   auto stage = [&](int dg, int buf) {
-#ifdef DCN_EXP_NOSTAGE
-    if (dg < 100) return;
-#endif
     float* st = smem + buf * BUF_F;
     float* sw = st + T_F;
     for (int i = wv; i < T_INST; i += NW) {
@@ -111,15 +97,10 @@ __global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
   auto om_load = [&](int dgi, float* o) {
 #pragma unroll
     for (int k = 0; k < NOM; ++k) {
-#ifdef DCN_EXP_NOOM
-      o[k] = 0.5f * k;
-#else
       if constexpr (F16) o[k] = omp[dgi * 27 + min(2 * (k / 3) + hf, 8) * 3 + k % 3];
       else o[k] = omp[dgi * 27 + k];
-#endif
     }
   };
-#ifdef DCN_OM_VEC
   // F16 variant: a group's 27 offset/mask floats (108 B, dword-aligned) as 6 x 16-B + 1 x 12-B loads
   // per lane instead of 15 scalar loads; lane half h picks its taps 2p + h at the group switch
   typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
@@ -142,15 +123,13 @@ __global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
     }
   };
   float omr[27];
-#endif
   float omc[NOM], omn[NOM];
-#ifdef DCN_OM_VEC
   if constexpr (F16) {
     om_raw(0, omr);
     om_pick(omr, omc);
-  } else
-#endif
-  om_load(0, omc);
+  } else {
+    om_load(0, omc);
+  }
 
   f32x16 acc0 = f32x16{0}, acc1 = f32x16{0};
   stage(0, 0);
@@ -158,11 +137,8 @@ __global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
   for (int dg = 0; dg < 8; ++dg) {
     if (dg + 1 < 8) {
       stage(dg + 1, (dg + 1) & 1);
-#ifdef DCN_OM_VEC
       if constexpr (F16) om_raw(dg + 1, omr);
-      else
-#endif
-      om_load(dg + 1, omn);
+      else om_load(dg + 1, omn);
     }
     const float* st = smem + (dg & 1) * BUF_F;
     const float* sw = st + T_F;
@@ -238,9 +214,6 @@ __global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
       const float* p0 = st + (((in_tile ? r0 : 0) * 2 + hf) * TC + (in_tile ? c0 : 0)) * 4;
       const float* p1 = p0 + 2 * TC * 4;
       f32x4 av = w1 * ld4(p0) + w2 * ld4(p0 + 4) + w3 * ld4(p1) + w4 * ld4(p1 + 4);
-#ifdef DCN_EXP_NOSAMPLE
-      av = f32x4{h_im, w_im, 1.f, m};
-#endif
       const bool fb = valid & !in_tile;
       if (__builtin_amdgcn_ballot_w64(fb)) {
         if (fb) {
@@ -263,12 +236,12 @@ __global__ __launch_bounds__(256) void k_dcn(stif_dcn_args a) {
     }
     }
     if (dg + 1 < 8) {
-#ifdef DCN_OM_VEC
-      if constexpr (F16) om_pick(omr, omc);
-      else
-#endif
+      if constexpr (F16) {
+        om_pick(omr, omc);
+      } else {
 #pragma unroll
-      for (int k = 0; k < NOM; ++k) omc[k] = omn[k];
+        for (int k = 0; k < NOM; ++k) omc[k] = omn[k];
+      }
     }
     lds_dma_barrier();
   }

@@ -104,11 +104,7 @@ extern "C" int stif_upsample2x_nhwc(const float* in, float* out, int n, int h1, 
   // on large maps (48 x 128^2 -> 256^2: 282 -> 250 us), slower on small ones whose input stays in
   // cache (48 x 64^2: 43 -> 47 us), so it takes launches of >= 8M quad threads
   const long long quads = (long long)n * h1 * w1 * (c / 4);
-#ifdef UP2_PERPIXEL
-  const bool quad = false;
-#else
   const bool quad = quads >= (8LL << 20);
-#endif
   if (quad) {
     const dim3 grid((unsigned)((w1 * (c / 4) + 255) / 256), (unsigned)h1, (unsigned)n);
     hipLaunchKernelGGL(k_up2q, grid, dim3(256), 0, (hipStream_t)stream, in, out, n, h1, w1, c, scale, in_item,

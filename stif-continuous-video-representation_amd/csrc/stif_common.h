@@ -89,9 +89,6 @@ enum { STIF_ACT_NONE = 0, STIF_ACT_LRELU = 1, STIF_ACT_RELU = 2, STIF_ACT_RES = 
 // sinf: 3.3e-8); 15 VALU ops.  Used instead of ocml sinf, whose Payne-Hanek path costs ~200 VGPRs
 // in the MLP kernels.
 STIF_DEV float stif_sin(float x) {
-#ifdef DEC_EXP_NOSIN
-  return x * 0.001f;   // kernel experiment: the cost of the sines
-#endif
   const float q = rintf(x * 0.318309886183790671538f);
   float r = fmaf(q, -3.140625f, x);
   r = fmaf(q, -9.67502593994140625e-4f, r);

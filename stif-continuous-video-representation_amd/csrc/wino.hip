@@ -33,42 +33,40 @@ namespace {
 constexpr int WR = 4;      // output rows per tile
 constexpr int HR = 6;      // halo rows
 constexpr int HC = 34;     // halo columns
-#ifndef WINO_PSUB
 constexpr int PSUB = 4;    // 8-channel chunks per staging phase
-#else
-constexpr int PSUB = WINO_PSUB;
-#endif
-// phase image: [halo row][column slot][16-B channel chunk: 2 * PSUB of them + 1 pad] -- a pixel's
-// chunks are consecutive, so 8 lanes of an LDS-DMA instruction read one pixel's 128 B (8 cache
-// lines per instruction instead of 64), and the odd pitch (2 * PSUB + 1 = 9 slots) keeps 16
-// consecutive pixels in 16 distinct bank groups for the transform's ds_read_b128
+constexpr int XREAD_J = 3; // F16: block j after whose split the next pair's first chunk is read
+// phase image: [halo row][column slot][16-B channel chunk: 2 * PSUB of them + 1 pad], halo rows
+// OM_RP chunks apart.  A pixel's chunks are consecutive (8 lanes of an LDS-DMA instruction read one
+// pixel's 128 B); the odd pixel pitch (9 slots) keeps 16 consecutive pixels in 16 distinct bank
+// groups for the transform's ds_read_b128, and OM_RP = 0 mod 8 keeps the two patch rows a lane
+// group spans (lanes of tile rows 0 and 1 share a 16-lane group) conflict-free as well.
 constexpr int PITCH = 2 * PSUB + 1;
-constexpr int IN_EL = HR * HC * PITCH;      // 16-B elements per phase buffer
-constexpr int IN_INST = (IN_EL + 63) / 64;     // LDS-DMA instructions per phase
+constexpr int OM_RP = 320;                     // 16-B chunks per staged halo row (35 x PITCH + 5)
 constexpr int EX_F = 2 * 2 * 2 * 1024;         // epilogue exchange: [wave 1|2][nt][b][32 tiles][32 co]
-constexpr int BUF_F = (IN_INST * 256 > EX_F) ? IN_INST * 256 : EX_F;   // floats per buffer (32 KB)
+constexpr int BUF_F = EX_F;                    // floats per buffer (32 KB)
 constexpr int WG_PER_CU = 2;
-constexpr int OM_RP = 320;                     // k_wino_om: 16-B chunks per staged halo row (35 x PITCH + 5)
-static_assert(HR * OM_RP * 4 <= BUF_F && OM_RP % 8 == 0 && 35 * PITCH <= OM_RP, "k_wino_om staging image");
-#ifndef WINO_F16_XREAD_J
-#define WINO_F16_XREAD_J 3   // F16: block j after whose split the next pair's first chunk is read
-#endif
+static_assert(HR * OM_RP * 4 <= BUF_F && OM_RP % 8 == 0 && 35 * PITCH <= OM_RP, "staging image");
 
 // slot of halo column c in its (row, chunk, half) run: even columns first, then odd
 STIF_DEV int col_slot(int c) { return (c & 1) ? 17 + (c >> 1) : (c >> 1); }
 
-#ifdef WINO_EXP_TRACE
-// per-wave s_memtime event trace (kernel experiment builds only): [block][wave][128 events]
-__device__ unsigned long long g_wtrace[512 * 4 * 128];
-#define WTR(tag)                                                                                   \
-  do {                                                                                             \
-    if (ntr < 127 && blockIdx.x < 512 && lane == 0 && wv < 4)                                                \
-      g_wtrace[(blockIdx.x * 4 + wi) * 128 + ntr] = (__builtin_amdgcn_s_memtime() << 8) | (tag);   \
-    ++ntr;                                                                                         \
-  } while (0)
-#else
-#define WTR(tag) do {} while (0)
-#endif
+// LDS-DMA of one staging phase (2 * PSUB 16-B chunks = 32 channels from channel cbase of a
+// Cs-channel NHWC map) of the 6 x 34 halo at (iy0, ix0) into `dst`: 30 instructions, (r, m) =
+// (halo row, run of 7 column slots); lane -> column slot 7 m + lane / 9, chunk lane % 9 (8 = pad).
+// Lane 63 lands on the next run's first chunk with that same pixel's data (or in the row pad), so
+// the overlap is benign.  Wave w of nw issues instructions w, w + nw, ...  No divisions per lane.
+STIF_DEV void stage_image(__amdgpu_buffer_rsrc_t rs, float* dst, int iy0, int ix0, int H, int W, int Cs, int cbase,
+                          int w, int nw, int lpx, int lck) {
+  for (int ins = w; ins < 30; ins += nw) {
+    const int r = ins / 5, m = ins - 5 * (ins / 5);
+    const int y = iy0 + r;
+    const int slot = 7 * m + lpx;
+    const int x = ix0 + (slot < 17 ? 2 * slot : 2 * slot - 33);
+    const bool ok = ((unsigned)y < (unsigned)H) & ((unsigned)x < (unsigned)W) & (slot < HC) & (lck < 2 * PSUB);
+    const unsigned voff = ok ? (unsigned)(((y * W + x) * Cs + cbase + lck * 4) * 4) : 0x80000000u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, dst + (r * OM_RP + 63 * m) * 4, 16, voff, 0, 0, 0);
+  }
+}
 
 struct Tile {
   int oy0, ox0, slice, g, n;
@@ -78,22 +76,13 @@ struct Tile {
 // 64-cout slice of one item), and the last staging phase of a tile already LDS-DMAs the first
 // phase of the next tile and the last chunk prefetches the next tile's first B operands, so a
 // workgroup's MFMA stream only pauses at the per-phase barriers and the short epilogue exchange.
-// SPLIT = 0: 4 waves, wave i = transform row i for both 32-cout halves (2 waves/SIMD, ~250 VGPRs);
-// SPLIT = 1: 8 waves, wave (i, nh) = transform row i for cout half nh (4 waves/SIMD, <= 128 VGPRs:
-// twice the waves to hide latencies, the input transform computed by both halves).
-template <int IN1, int EPI, int SPLIT, int F16>
-__global__ __launch_bounds__(SPLIT ? 512 : 256) __attribute__((amdgpu_waves_per_eu(SPLIT ? 4 : 2))) void k_wino(
-    stif_conv_args a, int ntiles) {
-  constexpr int NWV = SPLIT ? 8 : 4;      // waves per workgroup
-  constexpr int NTW = SPLIT ? 1 : 2;      // 32-cout halves per wave
-  constexpr int NTHR = NWV * 64;
-  constexpr int KPT = 4 / (NWV / 4);      // output rows per thread in the epilogue
+// Wave i = transform row i for both 32-cout halves (2 waves per SIMD, ~250 VGPRs).
+template <int IN1, int EPI, int F16>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_wino(stif_conv_args a, int ntiles) {
   __shared__ __attribute__((aligned(16))) float smem[2 * BUF_F];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wi = wv & 3;                                     // transform row i of this wave
-  const int nh = SPLIT ? (wv >> 2) : 0;                      // its cout half (SPLIT)
+  const int wi = __builtin_amdgcn_readfirstlane(tid >> 6);   // transform row i of this wave
   const int hf = lane >> 5;
   const int tl = lane & 31;                                  // Winograd tile of this lane
   const int tyl = tl >> 4, txl = tl & 15;
@@ -127,9 +116,11 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256) __attribute__((amdgpu_waves_per_
   // of pair q at wsl + q * 16384 + ((j * 2 + u) * 2 + plane) * 256 (float offsets)
   auto wbase = [&](const Tile& t) {
     return F16 ? a.w[t.g] + (size_t)t.slice * NC * 8192 + wi * 4096 + lane * 4
-               : a.w[t.g] + (size_t)t.slice * NC * 8192 + wi * 2048 + nh * 256 + lane * 4;
+               : a.w[t.g] + (size_t)t.slice * NC * 8192 + wi * 2048 + lane * 4;
   };
 
+  // staging image (stage_image): DMA instruction (r, m) = wave wi's ins = wi, wi + 4, ... of 30
+  const int lpx = lane / 9, lck = lane - 9 * (lane / 9);
   auto stage = [&](const Tile& t, int p, int buf) {
     // a phase lies entirely in one input (NC0 % PSUB == 0, host-checked)
     const bool second = IN1 && p * PSUB >= NC0;
@@ -138,23 +129,7 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256) __attribute__((amdgpu_waves_per_
     const int cbase = (second ? p * PSUB - NC0 : p * PSUB) * 8;
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, (int)((size_t)H * W * Cs * 4), 0x00020000);
-    float* dst = smem + buf * BUF_F;
-    const int iy0 = t.oy0 - 1, ix0 = t.ox0 - 1;
-#ifdef WINO_EXP_NOSTAGE
-    if (p < 1000000) return;
-#endif
-    for (int q = wv; q < IN_INST; q += NWV) {
-      // 16-B element e of the phase image = (halo row, 8-channel sub-chunk, half h, column slot)
-      const int e = q * 64 + lane;
-      const int px = e / PITCH;                 // pixel = row * HC + column slot
-      const int ck = e - px * PITCH;            // 16-B chunk (channels cbase + 4 ck ..), PITCH - 1 = pad
-      const int row = px / HC, slot = px - row * HC;
-      const int col = slot < 17 ? 2 * slot : 2 * (slot - 17) + 1;
-      const int y = iy0 + row, x = ix0 + col;
-      const bool ok = (e < IN_EL) & (ck < 2 * PSUB) & ((unsigned)y < (unsigned)H) & ((unsigned)x < (unsigned)W);
-      const unsigned voff = ok ? (unsigned)(((y * W + x) * Cs + cbase + ck * 4) * 4) : 0x80000000u;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, dst + q * 256, 16, voff, 0, 0, 0);
-    }
+    stage_image(rs, smem + buf * BUF_F, t.oy0 - 1, t.ox0 - 1, H, W, Cs, cbase, wi, 4, lpx, lck);
   };
 
   // rows of the 4x4 patch feeding transform row i: (B^T d)_i = d[rA] + sB * d[rB]
@@ -168,8 +143,8 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256) __attribute__((amdgpu_waves_per_
   // one chunk ahead where registers allow, so their latency hides under the current chunk's MFMAs)
   // and the add/subtract part.
   auto xread = [&](const float* buf, int s, f32x4* rd) {
-    const float* ra = buf + ((2 * tyl + rA) * HC * PITCH + 2 * s + hf) * 4;
-    const float* rb = buf + ((2 * tyl + rB) * HC * PITCH + 2 * s + hf) * 4;
+    const float* ra = buf + ((2 * tyl + rA) * OM_RP + 2 * s + hf) * 4;
+    const float* rb = buf + ((2 * tyl + rB) * OM_RP + 2 * s + hf) * 4;
     rd[0] = ld4(ra + s0 * PITCH * 4); rd[1] = ld4(rb + s0 * PITCH * 4);
     rd[2] = ld4(ra + s1 * PITCH * 4); rd[3] = ld4(rb + s1 * PITCH * 4);
     rd[4] = ld4(ra + s2 * PITCH * 4); rd[5] = ld4(rb + s2 * PITCH * 4);
@@ -194,17 +169,9 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256) __attribute__((amdgpu_waves_per_
   const int tend = min((xcd + 1) * per, ntiles);
   int T = xcd * per + (blockIdx.x >> 3);
   if (T >= tend) return;
-#ifdef WINO_EXP_TRACE
-  int ntr = 0;
-  if (blockIdx.x < 512 && lane == 0 && wv < 4) {   // slot 127: hardware placement (HW_ID, XCC_ID)
-    const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));
-    const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));
-    g_wtrace[(blockIdx.x * 4 + wi) * 128 + 127] = ((unsigned long long)xcc << 32) | hw;
-  }
-#endif
   Tile cur = tile_of(T);
   const float* wsl = wbase(cur);
-  f32x4 bw[4][NTW];
+  f32x4 bw[4][2];
   // F16: B operand ring over the (pair, j) blocks, two blocks deep: slot j & 1 holds block j's
   // (u, plane) fragments and is refilled with block j + 2 right after block j's MFMAs
   f16x8 bh[2][2], bl[2][2];
@@ -220,7 +187,7 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256) __attribute__((amdgpu_waves_per_
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int u = 0; u < NTW; ++u) bw[j][u] = ld4(wsl + (j * 2 + u) * 256);
+      for (int u = 0; u < 2; ++u) bw[j][u] = ld4(wsl + (j * 2 + u) * 256);
   }
   int gp = 0;                     // phases staged so far: buffer of phase gp = gp & 1
   stage(cur, 0, 0);
@@ -232,14 +199,11 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256) __attribute__((amdgpu_waves_per_
     const Tile nxt = tile_of(has_next ? Tn : T);
     const float* wnx = wbase(nxt);
 
-    f32x16 acc[4][NTW];
+    f32x16 acc[4][2];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int u = 0; u < NTW; ++u) acc[j][u] = f32x16{0};
-    // offset/mask conv: couts 224..255 of the last slice are padding (216 = 6.75 x 32), skip them
-    const bool last_half_pad = EPI == STIF_EPI_OFFMASK && cur.slice * 64 + 32 >= a.cout;
-    WTR(1);
+      for (int u = 0; u < 2; ++u) acc[j][u] = f32x16{0};
 
     if constexpr (F16) {
       for (int p = 0; p < NP; ++p, ++gp) {
@@ -254,14 +218,9 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256) __attribute__((amdgpu_waves_per_
           // K values of a 32x32x16 f16 MFMA; transform both, split all four j, then fetch the next
           // pair's first chunk so its LDS reads hide under this pair's MFMAs
           f32x4 va[4], vb[4];
-#ifdef WINO_EXP_NOXF
-          va[0] = va[1] = va[2] = va[3] = f32x4{1.f * sp, 1.f, 1.f, (float)lane};
-          vb[0] = vb[1] = vb[2] = vb[3] = f32x4{1.f * sp, 1.f, 3.f, (float)lane};
-#else
           xform(rd, va);
           xread(buf, 2 * sp + 1, rd);
           xform(rd, vb);
-#endif
           const int q = p * (PSUB / 2) + sp;
           const float* wq = wsl + (size_t)q * 16384;
           const float* wq1 = q + 1 < NQ ? wq + 16384 : wnx;
@@ -269,37 +228,27 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256) __attribute__((amdgpu_waves_per_
           for (int j = 0; j < 4; ++j) {
             f16x8 ah, al;
             split_f16x3(va[j], vb[j], ah, al);
-#if WINO_F16_XREAD_J >= 0
-            if (j == WINO_F16_XREAD_J && 2 * sp + 2 < PSUB) xread(buf, 2 * sp + 2, rd);
-#endif
+            if (j == XREAD_J && 2 * sp + 2 < PSUB) xread(buf, 2 * sp + 2, rd);
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
-              if (last_half_pad && u == 1) continue;
               acc[j][u] = mfma16h(ah, bh[j & 1][u], acc[j][u]);
               acc[j][u] = mfma16h(ah, bl[j & 1][u], acc[j][u]);
               acc[j][u] = mfma16h(al, bh[j & 1][u], acc[j][u]);
             }
             // refill the slot with block j + 2: (pair q, j + 2) or (pair q + 1, j - 2)
             const float* wn = j < 2 ? wq + (j + 2) * 1024 : wq1 + (j - 2) * 1024;
-#ifndef WINO_EXP_NOB
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
               bh[j & 1][u] = ldh8(wn + (u * 2) * 256);
               bl[j & 1][u] = ldh8(wn + (u * 2 + 1) * 256);
             }
-#else
-            (void)wn;
-            for (int u = 0; u < 2; ++u) bh[j & 1][u] += (_Float16)1.f;
-#endif
             __builtin_amdgcn_sched_barrier(0);
           }
         }
         // every load older than the last two blocks' B refills (8) -- the phase's LDS-DMA among
         // them -- has landed
-        WTR(6);
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         __syncthreads();
-        WTR(2);
       }
     } else
     for (int p = 0; p < NP; ++p, ++gp) {
@@ -307,17 +256,12 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256) __attribute__((amdgpu_waves_per_
       else if (has_next) stage(nxt, 0, (gp + 1) & 1);
       const float* buf = smem + (gp & 1) * BUF_F;
       f32x4 rd[8];
-      if (!SPLIT) xread(buf, 0, rd);
+      xread(buf, 0, rd);
 #pragma unroll
       for (int s = 0; s < PSUB; ++s) {
         f32x4 v[4];
-#ifdef WINO_EXP_NOXF
-        v[0] = v[1] = v[2] = v[3] = f32x4{1.f * s, 1.f, 1.f, (float)lane};
-#else
-        if (SPLIT) xread(buf, s, rd);
         xform(rd, v);
-        if (!SPLIT && s + 1 < PSUB) xread(buf, s + 1, rd);
-#endif
+        if (s + 1 < PSUB) xread(buf, s + 1, rd);
         // B operands of the next chunk (the next tile's first chunk after the last one).  bw[j] is
         // reloaded right after its MFMAs, 3/4 of a chunk before its next use; the scheduling
         // barriers keep the compiler from sinking those loads next to their use, which would
@@ -327,63 +271,39 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256) __attribute__((amdgpu_waves_per_
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
 #pragma unroll
-          for (int u = 0; u < NTW; ++u) {
-            if (last_half_pad && (SPLIT ? nh : u) == 1) continue;
+          for (int u = 0; u < 2; ++u)
 #pragma unroll
             for (int e = 0; e < 4; ++e) acc[j][u] = mfma32(v[j][e], bw[j][u][e], acc[j][u]);
-          }
-#ifndef WINO_EXP_NOB
 #pragma unroll
-          for (int u = 0; u < NTW; ++u) bw[j][u] = ld4(wn + (j * 2 + u) * 256);
-#else
-          for (int u = 0; u < NTW; ++u) bw[j][u] += 1.f;
-          (void)wn;
-#endif
+          for (int u = 0; u < 2; ++u) bw[j][u] = ld4(wn + (j * 2 + u) * 256);
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-#ifndef WINO_EXP_NOBAR
       // every load older than the last chunk's B-operand prefetches -- the phase's LDS-DMA among
-      // them -- has landed; those 4*NTW stay in flight across the barrier
-      WTR(6);
-      if (SPLIT) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      // them -- has landed; those 8 stay in flight across the barrier
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       __syncthreads();
-      WTR(2);
-#endif
     }
 
-#ifdef WINO_EXP_NOEPI2
-    // kernel experiment: no output transform at all (keep the accumulators alive)
-    {
-      float sum = 0.f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int u = 0; u < NTW; ++u) sum += acc[j][u][j + u];
-      if (sum == 1234.5f) a.out[0][tid] = sum;
-    }
-#else
     // ---- output transform, balanced over all waves.  Wave i holds P_i[b] = sum_j M[i][j] A[j][b]
     // (registers); Y[0] = P_0 + P_1 + P_2, Y[1] = P_1 - P_2 - P_3.  Two rounds (32-cout halves nt):
-    // the waves holding half nt write their P_i[nt] into the buffer of the phase just finished
-    // (free after the barrier; the other one is receiving the next tile) transposed to
-    // [i][b][tile][co], then every thread combines and stores (pixel, 4-cout) vectors as coalesced
-    // 16-B accesses (8 lanes = one pixel's 128 B).  Row swizzle R ^ (bit2(tile) ^ b) keeps both the
-    // b32 writes (lane halves 4 tiles apart) and the b128 reads (16-lane groups = b 0/1 of one
-    // tile) conflict-free.
+    // the waves write their P_i[nt] into the buffer of the phase just finished (free after the
+    // barrier; the other one is receiving the next tile) transposed to [i][b][tile][co], then every
+    // thread combines and stores (pixel, 4-cout) vectors as coalesced 16-B accesses (8 lanes = one
+    // pixel's 128 B).  Row swizzle R ^ (bit2(tile) ^ b) keeps both the b32 writes (lane halves 4
+    // tiles apart) and the b128 reads (16-lane groups = b 0/1 of one tile) conflict-free.
     float* ex = smem + ((gp - 1) & 1) * BUF_F;
-    f32x16 yv[NTW][2];   // [local half][b]
+    f32x16 yv[2][2];   // [local half][b]
 #pragma unroll
-    for (int u = 0; u < NTW; ++u) {
+    for (int u = 0; u < 2; ++u) {
       yv[u][0] = acc[0][u] + acc[1][u] + acc[2][u];
       yv[u][1] = acc[1][u] - acc[2][u] - acc[3][u];
     }
     // Exchange addresses as a per-lane base plus compile-time offsets (no hoisted address VGPRs):
     //   writer (m = mfma_row(r, lane), bit2(m) = hf): row bit 0 is flipped iff hf ^ b, i.e.
     //   +32 floats for even r, -32 for odd r;  reader (m = 16(k >> 1) + txo): bit2(m) = bit2(txo).
-    // this thread's outputs: cout quad c4, column ox of the tile, rows k = k0 + (NWV/4) r
-    const int c4 = tid & 7, oxl = (tid >> 3) & 31, k0 = tid >> 8;
+    // this thread's outputs: cout quad c4, column ox of the tile, rows k = 0..3
+    const int c4 = tid & 7, oxl = (tid >> 3) & 31;
     const int ox = cur.ox0 + oxl;
     const int bb = oxl & 1, txo = oxl >> 1;
     // LSTM: the quad is (i, f, o, g) of hidden channel cout/4; out / out2 / res are 64-ch maps
@@ -404,76 +324,65 @@ __global__ __launch_bounds__(SPLIT ? 512 : 256) __attribute__((amdgpu_waves_per_
       const bool ok = (oy < a.Ho) & (ox < a.Wo) & (co < a.cout);
       return ok ? (unsigned)(((oy * a.Wo + ox) * ostride + (LSTM ? co >> 2 : co)) * 4) : 0x80000000u;
     };
-    f32x4 rv[2][KPT];
-    float cc[2][KPT];
+    f32x4 rv[2][4];
+    float cc[2][4];
     if (EPI == STIF_EPI_RES) {
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-        for (int r = 0; r < KPT; ++r)
-          rv[nt][r] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, voff(nt, k0 + (NWV / 4) * r), 0, 0));
+        for (int k = 0; k < 4; ++k)
+          rv[nt][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, voff(nt, k), 0, 0));
     }
     if (LSTM) {
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-        for (int r = 0; r < KPT; ++r)
-          cc[nt][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, voff(nt, k0 + (NWV / 4) * r), 0, 0));
+        for (int k = 0; k < 4; ++k)
+          cc[nt][k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, voff(nt, k), 0, 0));
     }
+    float chk = 0.f;
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
       if (nt) __syncthreads();   // round-0 readers are done with the exchange image
-      if (!SPLIT || nh == nt) {
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          const int fl = (hf ^ b) * 32;
-          float* wb = ex + ((wi * 2 + b) * 32 + 4 * hf) * 32 + tl;
+      for (int b = 0; b < 2; ++b) {
+        const int fl = (hf ^ b) * 32;
+        float* wb = ex + ((wi * 2 + b) * 32 + 4 * hf) * 32 + tl;
 #pragma unroll
-          for (int r = 0; r < 16; ++r)
-            wb[((r & 3) + 8 * (r >> 2)) * 32 + ((r & 1) ? -fl : fl)] = yv[SPLIT ? 0 : nt][b][r];
-        }
+        for (int r = 0; r < 16; ++r)
+          wb[((r & 3) + 8 * (r >> 2)) * 32 + ((r & 1) ? -fl : fl)] = yv[nt][b][r];
       }
       __syncthreads();
-      WTR(3);
       const int cob = cur.slice * 64 + nt * 32 + c4 * 4;
       const f32x4 bv = cob < a.cout ? ld4(a.bias[cur.g] + cob) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int r = 0; r < KPT; ++r) {
-        const int k = k0 + (NWV / 4) * r;
+      for (int k = 0; k < 4; ++k) {
         const float* rbase = ex + (bb * 32 + (txo ^ (((txo >> 2) ^ bb) & 1))) * 32 + c4 * 4 + (k >> 1) * 512;
         const f32x4 p1 = ld4(rbase + 1 * 2048), p2 = ld4(rbase + 2 * 2048);
         const f32x4 pe = ld4(rbase + ((k & 1) ? 3 : 0) * 2048);
         f32x4 y = (k & 1) ? (p1 - p2 - pe) : (pe + p1 + p2);
-        if (F16) y *= F16X3_UNSCALE;   // exact power of two
-        y += bv;
-        if (F16)
-          report_range(a.status, (cob < a.cout) & (not_finite(y[0]) | not_finite(y[1]) | not_finite(y[2]) |
-                                                   not_finite(y[3])));
+        y = y * (F16 ? F16X3_UNSCALE : 1.f) + bv;   // exact power of two
+        if (F16) chk += (cob < a.cout) ? (y[0] + y[1]) + (y[2] + y[3]) : 0.f;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           if (EPI == STIF_EPI_LRELU) y[e] = lrelu01(y[e]);
           if (EPI == STIF_EPI_RELU) y[e] = fmaxf(y[e], 0.f);
           if (EPI == STIF_EPI_OFFMASK && (cob + e) % 3 == 2) y[e] = sigmoidf_(y[e]);
         }
-        if (EPI == STIF_EPI_RES) y += rv[nt][r];
+        if (EPI == STIF_EPI_RES) y += rv[nt][k];
         if (LSTM) {
           // ConvLSTMCell (convlstm.py:51-56): c_next = f * c_cur + i * g, h_next = o * tanh(c_next)
-          const float cn = sigmoidf_(y[1]) * cc[nt][r] + sigmoidf_(y[0]) * tanhf(y[3]);
+          const float cn = sigmoidf_(y[1]) * cc[nt][k] + sigmoidf_(y[0]) * tanhf(y[3]);
           const float hn = sigmoidf_(y[2]) * tanhf(cn);
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, hn), ro, voff(nt, k), 0, 0);
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, cn), ro2, voff(nt, k), 0, 0);
           continue;
         }
-#ifdef WINO_EXP_NOEPI
-        if (y[0] == 12345.f)
-#endif
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, y), ro, voff(nt, k), 0, 0);
       }
     }
+    if (F16) report_range(a.status, not_finite(chk));   // a non-finite output makes the sum non-finite
     __syncthreads();   // exchange buffer free for the next tile's staging
-    WTR(4);
-#endif
-    WTR(5);
     if (!has_next) break;
     T = Tn;
     cur = nxt;
@@ -531,32 +440,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     return t;
   };
 
-  // Staging image [halo row][column slot][PITCH 16-B chunks], rows OM_RP chunks apart (35 column slots
-  // + 5 pad chunks: OM_RP = 0 mod 8 keeps both 16-lane groups of the transform's ds_read_b128
-  // conflict-free across the two patch rows).  DMA instruction (r, m) fills chunks r * OM_RP + 63 m +
-  // lane: lane -> column slot 7 m + lane / 9, chunk lane % 9 (8 = pad).  Lane 63 lands on the first
-  // chunk of the next instruction's pixel with that same pixel's data (or in the row pad), so the
-  // overlap is benign.  30 instructions per phase, wave wi issues r * 5 + m = wi, wi + 4, ...
+  // staging: k_wino's image (stage_image), 32 channels per phase, all four waves issuing
   const int lpx = lane / 9, lck = lane - 9 * (lane / 9);
   auto stage = [&](const Tile& t, int p, int buf) {
     const float* src = a.in0[t.g] + (size_t)t.n * a.in0_item;
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, (int)((size_t)H * W * 256), 0x00020000);
-    float* dst = smem + buf * BUF_F;
-    const int iy0 = t.oy0 - 1, ix0 = t.ox0 - 1;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int ins = wi + 4 * k;
-      if (ins >= 30) break;
-      const int r = ins / 5, m = ins - 5 * (ins / 5);
-      const int y = iy0 + r;
-      const int slot = 7 * m + lpx;
-      const int x = ix0 + (slot < 17 ? 2 * slot : 2 * slot - 33);
-      const bool ok = ((unsigned)y < (unsigned)H) & ((unsigned)x < (unsigned)W) & (slot < HC) & (lck < 8);
-      const unsigned voff = ok ? (unsigned)(((y * W + x) * 64 + p * 32 + lck * 4) * 4) : 0x80000000u;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, dst + (r * OM_RP + 63 * m) * 4, 16, voff, 0, 0, 0);
-    }
+    stage_image(rs, smem + buf * BUF_F, t.oy0 - 1, t.ox0 - 1, H, W, 64, p * 32, wi, 4, lpx, lck);
   };
+
 
   // input transform row i (k_wino's xread / xform) -> split A operands of chunk pair q
   const int rA = (wi == 0) ? 0 : (wi == 2 ? 2 : 1);
@@ -725,311 +617,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// k_wino_ws: the same operator with warp specialisation.  One workgroup per CU, 8 waves: waves 0-3
-// are the MFMA waves (wave i = transform row i, exactly the k_wino loop), waves 4-7 are helpers
-// sharing their SIMDs: they issue all the LDS-DMA staging (so the MFMA waves' vmcnt queue only holds
-// their own B-operand prefetches and never waits on a DMA), and they run the output transform of
-// tile T-1 from a dedicated 64-KB exchange image while the MFMA waves already compute tile T.
-// The MFMA waves' per-tile epilogue shrinks to summing over j and writing P_i (64 ds_write_b32)
-// before one extra barrier.  Barrier sequence, identical for both roles: one per staging phase,
-// one after the P write.  Staging runs two phases ahead (3 buffers).
-// Measured (s_memtime trace, tools/trace_wino_ws.py): slower than k_wino (465 vs 425 us on the
-// trunk RELU conv at C1).  The MFMA waves alone keep the pipe ~80 % busy inside a phase, but the
-// helpers' LDS-DMA issue is the bottleneck: 8 buffer_load...lds instructions take 8-10K cycles
-// to issue even with the MFMA waves idle (WINO_EXP_NOMFMA), ~3 B/clk per CU -- k_wino hides that
-// cost because two workgroups per CU overlap each other's staging.  Kept behind WINO_WS=1.
-template <int IN1, int EPI>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_wino_ws(stif_conv_args a,
-                                                                                        int ntiles) {
-  constexpr int IN_F = IN_INST * 256;                // floats per staging buffer
-  constexpr int XF = 2 * 4 * 2 * 32 * 32;            // exchange image [nt][i][b][tile 32][co 32]
-  __shared__ __attribute__((aligned(16))) float smem[3 * IN_F + XF];   // 3 staging buffers + exchange
-  float* const X = smem + 3 * IN_F;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool mf = wv < 4;                                    // MFMA wave
-  const int wi = wv & 3;                                     // transform row (MFMA) / helper index
-  const int hf = lane >> 5;
-  const int tl = lane & 31;
-  const int tyl = tl >> 4, txl = tl & 15;
-
-  const int tiles_x = (a.Wo + 31) >> 5;
-  const int tiles_y = (a.Ho + WR - 1) / WR;
-  const int slices = (a.cout + 63) >> 6;
-  const int H = a.H, W = a.W, C0 = a.C0, C1 = a.C1;
-  const int NC0 = C0 >> 3;
-  const int NC = NC0 + (IN1 ? (C1 >> 3) : 0);
-  const int NP = NC / PSUB;
-
-  auto tile_of = [&](int T) {
-    Tile t;
-    t.slice = T % slices;
-    int r = T / slices;
-    const int x = r % tiles_x;
-    r /= tiles_x;
-    const int y = r % tiles_y;
-    r /= tiles_y;
-    t.g = r / a.nitems;
-    t.n = r - t.g * a.nitems;
-    t.oy0 = y * WR;
-    t.ox0 = x * 32;
-    return t;
-  };
-  auto wbase = [&](const Tile& t) { return a.w[t.g] + (size_t)t.slice * NC * 8192 + wi * 2048 + lane * 4; };
-
-  // helpers: LDS-DMA of staging phase p of tile t (the k_wino phase image)
-  auto stage = [&](const Tile& t, int p, int buf) {
-    const bool second = IN1 && p * PSUB >= NC0;
-    const float* src = second ? a.in1[t.g] + (size_t)t.n * a.in1_item : a.in0[t.g] + (size_t)t.n * a.in0_item;
-    const int Cs = second ? C1 : C0;
-    const int cbase = (second ? p * PSUB - NC0 : p * PSUB) * 8;
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, (int)((size_t)H * W * Cs * 4), 0x00020000);
-    float* dst = smem + buf * IN_F;
-    const int iy0 = t.oy0 - 1, ix0 = t.ox0 - 1;
-    for (int q = wi; q < IN_INST; q += 4) {
-      const int e = q * 64 + lane;
-      const int px = e / PITCH;                 // pixel = row * HC + column slot
-      const int ck = e - px * PITCH;            // 16-B chunk (channels cbase + 4 ck ..), PITCH - 1 = pad
-      const int row = px / HC, slot = px - row * HC;
-      const int col = slot < 17 ? 2 * slot : 2 * (slot - 17) + 1;
-      const int y = iy0 + row, x = ix0 + col;
-      const bool ok = (e < IN_EL) & (ck < 2 * PSUB) & ((unsigned)y < (unsigned)H) & ((unsigned)x < (unsigned)W);
-      const unsigned voff = ok ? (unsigned)(((y * W + x) * Cs + cbase + ck * 4) * 4) : 0x80000000u;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, dst + q * 256, 16, voff, 0, 0, 0);
-    }
-  };
-
-  // helpers: output transform + epilogue of tile t from the exchange image (k_wino's reader side,
-  // both cout halves): thread = (cout quad c4, column oxl), rows k = 0..3
-  auto epilogue = [&](const Tile& t) {
-    const int ht = tid - 256;
-    const int c4 = ht & 7, oxl = ht >> 3;
-    const int ox = t.ox0 + oxl;
-    const int bb = oxl & 1, txo = oxl >> 1;
-    constexpr bool LSTM = EPI == STIF_EPI_LSTM;
-    const int ostride = LSTM ? 64 : a.cout;
-    const size_t slab = (size_t)a.Ho * a.Wo * ostride;
-    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(a.out[t.g] + (size_t)t.n * a.out_item), (short)0, (int)(slab * 4), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(EPI == STIF_EPI_RES || LSTM ? a.res[t.g] + (size_t)t.n * a.res_item : a.in0[t.g]), (short)0,
-        (int)(slab * 4), 0x00020000);
-    const __amdgpu_buffer_rsrc_t ro2 = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(LSTM ? a.out2[t.g] + (size_t)t.n * a.out2_item : a.out[t.g]), (short)0, (int)(slab * 4),
-        0x00020000);
-    auto voff = [&](int nt, int k) -> unsigned {
-      const int oy = t.oy0 + k;
-      const int co = t.slice * 64 + nt * 32 + c4 * 4;
-      const bool ok = (oy < a.Ho) & (ox < a.Wo) & (co < a.cout);
-      return ok ? (unsigned)(((oy * a.Wo + ox) * ostride + (LSTM ? co >> 2 : co)) * 4) : 0x80000000u;
-    };
-    f32x4 rv[2][4];
-    float cc[2][4];
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (EPI == STIF_EPI_RES)
-          rv[nt][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, voff(nt, k), 0, 0));
-        if (LSTM) cc[nt][k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, voff(nt, k), 0, 0));
-      }
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      const int cob = t.slice * 64 + nt * 32 + c4 * 4;
-      const f32x4 bv = cob < a.cout ? ld4(a.bias[t.g] + cob) : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float* rbase =
-            X + nt * 8192 + (bb * 32 + (txo ^ (((txo >> 2) ^ bb) & 1))) * 32 + c4 * 4 + (k >> 1) * 512;
-        const f32x4 p1 = ld4(rbase + 1 * 2048), p2 = ld4(rbase + 2 * 2048);
-        const f32x4 pe = ld4(rbase + ((k & 1) ? 3 : 0) * 2048);
-        f32x4 y = (k & 1) ? (p1 - p2 - pe) : (pe + p1 + p2);
-        y += bv;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          if (EPI == STIF_EPI_LRELU) y[e] = lrelu01(y[e]);
-          if (EPI == STIF_EPI_RELU) y[e] = fmaxf(y[e], 0.f);
-          if (EPI == STIF_EPI_OFFMASK && (cob + e) % 3 == 2) y[e] = sigmoidf_(y[e]);
-        }
-        if (EPI == STIF_EPI_RES) y += rv[nt][k];
-        if (LSTM) {
-          // ConvLSTMCell (convlstm.py:51-56): c_next = f * c_cur + i * g, h_next = o * tanh(c_next)
-          const float cn = sigmoidf_(y[1]) * cc[nt][k] + sigmoidf_(y[0]) * tanhf(y[3]);
-          const float hn = sigmoidf_(y[2]) * tanhf(cn);
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, hn), ro, voff(nt, k), 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, cn), ro2, voff(nt, k), 0, 0);
-          continue;
-        }
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, y),
-                                               ro, voff(nt, k), 0, 0);
-      }
-    }
-  };
-
-  // MFMA waves: transform row i (see k_wino)
-  const int rA = (wi == 0) ? 0 : (wi == 2 ? 2 : 1);
-  const int rB = (wi == 3) ? 3 : (wi == 2 ? 1 : 2);
-  const float sB = (wi == 1) ? 1.f : -1.f;
-  const int s0 = col_slot(0) + txl, s1 = col_slot(1) + txl, s2 = col_slot(2) + txl, s3 = col_slot(3) + txl;
-  auto xread = [&](const float* buf, int s, f32x4* rd) {
-    const float* ra = buf + ((2 * tyl + rA) * HC * PITCH + 2 * s + hf) * 4;
-    const float* rb = buf + ((2 * tyl + rB) * HC * PITCH + 2 * s + hf) * 4;
-    rd[0] = ld4(ra + s0 * PITCH * 4); rd[1] = ld4(rb + s0 * PITCH * 4);
-    rd[2] = ld4(ra + s1 * PITCH * 4); rd[3] = ld4(rb + s1 * PITCH * 4);
-    rd[4] = ld4(ra + s2 * PITCH * 4); rd[5] = ld4(rb + s2 * PITCH * 4);
-    rd[6] = ld4(ra + s3 * PITCH * 4); rd[7] = ld4(rb + s3 * PITCH * 4);
-  };
-  auto xform = [&](const f32x4* rd, f32x4* v) {
-    const f32x4 t0 = rd[0] + sB * rd[1];
-    const f32x4 t1 = rd[2] + sB * rd[3];
-    const f32x4 t2 = rd[4] + sB * rd[5];
-    const f32x4 t3 = rd[6] + sB * rd[7];
-    v[0] = t0 - t2;
-    v[1] = t1 + t2;
-    v[2] = t2 - t1;
-    v[3] = t1 - t3;
-  };
-
-  // XCD-aware persistent schedule (see k_wino)
-  const int xcd = blockIdx.x & 7, nl = gridDim.x >> 3;
-  const int per = (ntiles + 7) >> 3;
-  const int tend = min((xcd + 1) * per, ntiles);
-  int T = xcd * per + (blockIdx.x >> 3);
-  if (T >= tend) return;   // uniform over the workgroup
-
-#ifdef WINO_EXP_TRACE
-  // MFMA waves in trace blocks [0, 256), helpers in [256, 512)
-  int ntr = 0;
-  const int trb = blockIdx.x + (mf ? 0 : 256);
-#define WTRW(tag)                                                                                  \
-  do {                                                                                             \
-    if (ntr < 127 && trb < 512 && lane == 0)                                                       \
-      g_wtrace[(trb * 4 + wi) * 128 + ntr] = (__builtin_amdgcn_s_memtime() << 8) | (tag);          \
-    ++ntr;                                                                                         \
-  } while (0)
-#else
-#define WTRW(tag) do {} while (0)
-#endif
-  Tile cur = tile_of(T), prev = cur;
-  const float* wsl = wbase(cur);
-  f32x4 bw[4][2];
-  // staging runs two phases ahead of the MFMA waves (3 buffers): the DMA of a phase has a whole
-  // phase to land before the helpers' counted wait.  Host: NP >= 2.
-  const int my_dma = (IN_INST - wi + 3) / 4;   // DMA instructions this helper issues per phase
-  if (mf) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) bw[j][nt] = ld4(wsl + (j * 2 + nt) * 256);
-  } else {
-#ifdef WINO_HELPER_PRIO
-    __builtin_amdgcn_s_setprio(WINO_HELPER_PRIO);   // kernel experiment: helper issue priority
-#endif
-    stage(cur, 0, 0);
-    stage(cur, 1, 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  int gp = 0;           // phases computed so far
-  int cb = 0;           // buffer of phase gp (gp % 3)
-  bool has_prev = false;
-
-  for (;;) {
-    const int Tn = T + nl;
-    const bool has_next = Tn < tend;
-    const Tile nxt = tile_of(has_next ? Tn : T);
-    const float* wnx = wbase(nxt);
-    const bool last_half_pad = EPI == STIF_EPI_OFFMASK && cur.slice * 64 + 32 >= a.cout;
-
-    f32x16 acc[4][2];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j][0] = acc[j][1] = f32x16{0};
-    WTRW(1);
-
-    for (int p = 0; p < NP; ++p, ++gp) {
-      if (!mf) {
-        const int sb = cb == 0 ? 2 : cb - 1;   // (gp + 2) % 3: the buffer phase gp - 1 just released
-        const bool staged = p + 2 < NP || has_next;
-        const Tile st = p + 2 < NP ? cur : nxt;
-        const int sp = p + 2 < NP ? p + 2 : p + 2 - NP;
-        if (p == 0 && has_prev) epilogue(prev);
-        WTRW(7);
-        if (staged) stage(st, sp, sb);
-        WTRW(8);
-        // everything but this phase's own DMA has landed -- in particular the next phase's image
-        if (!staged) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else if (my_dma >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-      } else {
-#ifdef WINO_EXP_NOMFMA
-        if (p < 100000) { __syncthreads(); WTRW(2); cb = cb == 2 ? 0 : cb + 1; continue; }
-#endif
-        const float* buf = smem + cb * IN_F;
-        f32x4 rd[8];
-        xread(buf, 0, rd);
-#pragma unroll
-        for (int s = 0; s < PSUB; ++s) {
-          f32x4 v[4];
-          xform(rd, v);
-          if (s + 1 < PSUB) xread(buf, s + 1, rd);
-          const int kn = p * PSUB + s + 1;
-          const float* wn = kn < NC ? wsl + (size_t)kn * 8192 : wnx;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-#pragma unroll
-            for (int nt = 0; nt < 2; ++nt) {
-              if (nt == 1 && last_half_pad) continue;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) acc[j][nt] = mfma32(v[j][e], bw[j][nt][e], acc[j][nt]);
-            }
-#ifndef WINO_EXP_NOB
-#pragma unroll
-            for (int nt = 0; nt < 2; ++nt) bw[j][nt] = ld4(wn + (j * 2 + nt) * 256);
-#else
-            for (int nt = 0; nt < 2; ++nt) bw[j][nt] += 1.f;
-            (void)wn;
-#endif
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        }
-      }
-      WTRW(6);
-      __syncthreads();
-      WTRW(2);
-      cb = cb == 2 ? 0 : cb + 1;
-    }
-    if (mf) {
-      // P_i[nt][b] = sum_j M[i][j] A[j][b] -> exchange image (k_wino's writer side, both halves)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const f32x16 y0 = acc[0][nt] + acc[1][nt] + acc[2][nt];
-        const f32x16 y1 = acc[1][nt] - acc[2][nt] - acc[3][nt];
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          const int fl = (hf ^ b) * 32;
-          float* wb = X + nt * 8192 + ((wi * 2 + b) * 32 + 4 * hf) * 32 + tl;
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            wb[((r & 3) + 8 * (r >> 2)) * 32 + ((r & 1) ? -fl : fl)] = b ? y1[r] : y0[r];
-        }
-      }
-    }
-    WTRW(3);
-    __syncthreads();   // P of tile T published; the helpers read it during tile T+1's first phase
-    WTRW(4);
-    prev = cur;
-    has_prev = true;
-    if (!has_next) break;
-    T = Tn;
-    cur = nxt;
-    wsl = wnx;
-  }
-  if (!mf) epilogue(prev);
-}
-
 int num_cus() {
   static int n = 0;
   if (!n) {
@@ -1040,16 +627,8 @@ int num_cus() {
   return n;
 }
 
-#ifndef WINO_SPLIT
-#define WINO_SPLIT 0
-#endif
-
 #ifndef WINO_OM
 #define WINO_OM 1   // offset/mask conv (f16x3) by k_wino_om; 0 = the per-slice k_wino
-#endif
-
-#ifndef WINO_WS
-#define WINO_WS 0   // measured slower (k_wino_ws comment); kept as a build switch
 #endif
 
 template <int IN1, int EPI>
@@ -1059,11 +638,6 @@ int launch(const stif_conv_args& a, hipStream_t st) {
   if (tiles > 0x7fffffff) return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: too many tiles");
   if ((long long)a.H * a.W * std::max(a.C0, std::max(a.C1, a.cout)) * 4 >= 0x7fffffffLL)
     return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: item larger than 2 GB (buffer addressing)");
-  if (WINO_WS && !(a.flags & STIF_CONV_F16X3) && (a.C0 + (a.in1_mode ? a.C1 : 0)) >= 16 * PSUB) {   // one warp-specialised workgroup per CU
-    const int grid = 8 * (int)std::min<long long>((tiles + 7) / 8, (long long)num_cus() / 8);
-    hipLaunchKernelGGL((k_wino_ws<IN1, EPI>), dim3(grid), dim3(512), 0, st, a, (int)tiles);
-    return stif_check_launch("stif_conv3x3_wino");
-  }
   if constexpr (WINO_OM && EPI == STIF_EPI_OFFMASK) if ((a.flags & STIF_CONV_F16X3) && a.C0 == 64 && !a.in1_mode) {
     const long long sp = tiles / ((a.cout + 63) / 64);   // spatial tiles: all couts per workgroup
     const int g2 = 8 * (int)std::min<long long>((sp + 7) / 8, (long long)WG_PER_CU * num_cus() / 8);
@@ -1072,19 +646,13 @@ int launch(const stif_conv_args& a, hipStream_t st) {
   }
   const int grid = 8 * (int)std::min<long long>((tiles + 7) / 8, (long long)WG_PER_CU * num_cus() / 8);
   if (a.flags & STIF_CONV_F16X3)
-    hipLaunchKernelGGL((k_wino<IN1, EPI, 0, 1>), dim3(grid), dim3(256), 0, st, a, (int)tiles);
+    hipLaunchKernelGGL((k_wino<IN1, EPI, 1>), dim3(grid), dim3(256), 0, st, a, (int)tiles);
   else
-    hipLaunchKernelGGL((k_wino<IN1, EPI, WINO_SPLIT, 0>), dim3(grid), dim3(WINO_SPLIT ? 512 : 256), 0, st, a, (int)tiles);
+    hipLaunchKernelGGL((k_wino<IN1, EPI, 0>), dim3(grid), dim3(256), 0, st, a, (int)tiles);
   return stif_check_launch("stif_conv3x3_wino");
 }
 
 }  // namespace
-
-#ifdef WINO_EXP_TRACE
-extern "C" int stif_exp_wino_trace(unsigned long long* host) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wtrace), sizeof(g_wtrace)) == hipSuccess ? 0 : -1;
-}
-#endif
 
 extern "C" int stif_conv3x3_wino(const stif_conv_args* pa, void* stream) {
   if (!pa) return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: null args");
