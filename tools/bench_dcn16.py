@@ -10,7 +10,7 @@ import stif_pkg  # noqa: E402
 
 stif = stif_pkg.load()
 L, ops = stif._lib, stif.ops
-N, H, W = int(os.environ.get("N", 8)), 256, 256
+N, H, W = int(os.environ.get("N", 8)), int(os.environ.get("HW", 256)), int(os.environ.get("HW", 256))
 rng = np.random.default_rng(0)
 w = (rng.standard_normal((64, 64, 3, 3)) * 0.05).astype(np.float32)
 b = rng.standard_normal(64).astype(np.float32)
