@@ -83,24 +83,20 @@ STIF_DEV float sigmoid_fast(float x) {
 enum { STIF_ACT_NONE = 0, STIF_ACT_LRELU = 1, STIF_ACT_RELU = 2, STIF_ACT_RES = 3,
        STIF_ACT_OFFMASK = 4, STIF_ACT_LSTM = 5 };
 
-// sin(x): Cody-Waite reduction by pi (3-part constant, q * P1 exact for |q| < 2^16), then an odd
-// degree-11 polynomial on [-pi/2, pi/2] (coefficients fitted by iteratively reweighted least
-// squares, near-minimax) and the sign of (-1)^q.  Max abs error 1.2e-7 over |x| <= 3000 (glibc
-// sinf: 3.3e-8); 15 VALU ops.  Used instead of ocml sinf, whose Payne-Hanek path costs ~200 VGPRs
-// in the MLP kernels.
+// sin(x): one Cody-Waite step by 2 pi in radians (q = rint(x / 2 pi) by magic-number rounding; 2-part
+// constant, q * P1 exact for |q| < 2^16, |P1 + P2 - 2 pi| < 1.2e-10), then the hardware v_sin_f32 on
+// r / 2 pi in [-1/2, 1/2] revolutions.  5 VALU ops + one transcendental (8 issue cycles) instead of
+// a 15-op polynomial: the SIREN decoder is VALU-issue-bound and evaluates one sine per hidden unit.
+// v_sin_f32 alone, on x / 2 pi, loses accuracy with |x| (the rounding of x / 2 pi: 1.4e-6 at |x| = 16,
+// 2.8e-5 at 400); reduced first it stays within ~4e-7 of sin over |x| <= 3000
+// (tools/experiments/sin_acc.hip).  Used instead of ocml sinf, whose Payne-Hanek path costs ~200
+// VGPRs in the MLP kernels.
 STIF_DEV float stif_sin(float x) {
-  const float q = rintf(x * 0.318309886183790671538f);
-  float r = fmaf(q, -3.140625f, x);
-  r = fmaf(q, -9.67502593994140625e-4f, r);
-  r = fmaf(q, -1.509957990e-7f, r);
-  const float r2 = r * r;
-  float p = fmaf(r2, -2.3845164e-08f, 2.7522526e-06f);
-  p = fmaf(r2, p, -1.9840802e-04f);
-  p = fmaf(r2, p, 8.3333300e-03f);
-  p = fmaf(r2, p, -1.6666667e-01f);
-  const float s = fmaf(r * r2, p, r);
-  // (-1)^q: flip the sign bit when q is odd
-  return __int_as_float(__float_as_int(s) ^ (((int)q & 1) << 31));
+  const float qm = fmaf(x, 0.159154943091895335769f, 12582912.0f);   // + 1.5 * 2^23 rounds to integer
+  const float q = qm - 12582912.0f;
+  float r = fmaf(q, -6.28125f, x);                                    // exact (P1 has 8 significant bits)
+  r = fmaf(q, -1.93530717958e-3f, r);
+  return __builtin_amdgcn_sinf(r * 0.159154943091895335769f);
 }
 
 // Epilogue helper: write one 32 px x 32 cout accumulator tile (lane = cout, regs = px) into the
