@@ -47,6 +47,7 @@ constexpr int I_END = I_E2 + 2 * T;
 // 128 MFMAs per 32 pixels of which 28/32 (29/32) would multiply zero-padded rows
 constexpr int L_W3V = I_END;             // [4][256]
 constexpr int E_W4V = L_W3V + 4 * 256;   // [3][256], padded to a whole 4-KB tile (LDS-DMA granule)
+constexpr int E_W4V_B3 = E_W4V + 768;    // the pad holds a copy of E_B3 (k_dec2 reads it from LDS)
 constexpr int V_END = E_W4V + 1024;
 
 constexpr int MLP_FLOATS = V_END;

@@ -59,17 +59,29 @@ constexpr float ACC_S = F16 ? F16X3_UNSCALE : 1.f;   // accumulator -> value
 template <int F16>
 constexpr float ACC_IN = F16 ? 16384.f : 1.f;        // value -> accumulator
 
+// the 16 biases of one 32-feature register tile (features F(r, hf)) as 4 vector loads
+struct Bias32 {
+  f32x4 v[4];
+};
+STIF_DEV Bias32 bias_ld(const float* __restrict__ b, int hf) {
+  Bias32 o;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) o.v[v] = ld4(b + 8 * v + 4 * hf);
+  return o;
+}
 // SineLayer: sin(30 * (z + b)) (SIREN.py:44-45, omega_0 = 30); the packed weights and biases of every
 // sine layer carry the factor 30 (pack.cpp), so the kernel evaluates sin(z + b)
 template <int F16>
-STIF_DEV f32x16 bias_sin(f32x16 z, const float* __restrict__ b, int hf) {
+STIF_DEV f32x16 bias_sin(f32x16 z, const Bias32& bb) {
 #pragma unroll
-  for (int v = 0; v < 4; ++v) {
-    const f32x4 bb = ld4(b + 8 * v + 4 * hf);
+  for (int v = 0; v < 4; ++v)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) z[4 * v + e] = stif_sin(fmaf(z[4 * v + e], ACC_S<F16>, bb[e]));
-  }
+    for (int e = 0; e < 4; ++e) z[4 * v + e] = stif_sin(fmaf(z[4 * v + e], ACC_S<F16>, bb.v[v][e]));
   return z;
+}
+template <int F16>
+STIF_DEV f32x16 bias_sin(f32x16 z, const float* __restrict__ b, int hf) {
+  return bias_sin<F16>(z, bias_ld(b, hf));
 }
 
 template <int F16>
@@ -113,19 +125,30 @@ STIF_DEV Bilin bilin(float gx, float gy, int Wd, int Hd) {
 // bilinear sample of channel block [c0, c0+64) of an NHWC map with `stride` channels,
 // into two register tiles (features F(r, hf) of each 32-block)
 STIF_DEV void gather64(f32x16* dst, const float* __restrict__ base, int stride, int c0, const Bilin& b, int hf) {
+  // all 32 corner loads (8 channel groups x 4 corners, 128 VGPRs) are issued before the first blend,
+  // so a gather waits for one memory latency, not one per channel group
+  const int c = c0 + 4 * hf;
+  const float* p00 = base + (size_t)b.o00 * stride + c;
+  const float* p01 = base + (size_t)b.o01 * stride + c;
+  const float* p10 = base + (size_t)b.o10 * stride + c;
+  const float* p11 = base + (size_t)b.o11 * stride + c;
+  f32x4 cr[8][4];
 #pragma unroll
-  for (int ot = 0; ot < 2; ++ot)
+  for (int g = 0; g < 8; ++g) {   // group g = (ot, v) = (g >> 2, g & 3): channels 8 g + 4 hf ..
+    cr[g][0] = ld4(p00 + 8 * g);
+    cr[g][1] = ld4(p01 + 8 * g);
+    cr[g][2] = ld4(p10 + 8 * g);
+    cr[g][3] = ld4(p11 + 8 * g);
+  }
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int c = c0 + ot * 32 + 8 * v + 4 * hf;
-      f32x4 s = b.w00 * ld4(base + (size_t)b.o00 * stride + c) + b.w01 * ld4(base + (size_t)b.o01 * stride + c) +
-                      b.w10 * ld4(base + (size_t)b.o10 * stride + c) + b.w11 * ld4(base + (size_t)b.o11 * stride + c);
-      // combine the corners here: otherwise the blend is sunk to the first use (past a barrier)
-      // and all four corners of every channel stay live
-      asm volatile("" : "+v"(s));
+  for (int g = 0; g < 8; ++g) {
+    f32x4 s = b.w00 * cr[g][0] + b.w01 * cr[g][1] + b.w10 * cr[g][2] + b.w11 * cr[g][3];
+    // combine the corners here, in load order: otherwise the blend is sunk to the first use (past a
+    // barrier) and all four corners of every channel stay live
+    asm volatile("" : "+v"(s));
 #pragma unroll
-      for (int e = 0; e < 4; ++e) dst[ot][4 * v + e] = s[e];
-    }
+    for (int e = 0; e < 4; ++e) dst[g >> 2][4 * (g & 3) + e] = s[e];
+  }
 }
 
 // z[ot] += W_img . img: the 6 image channels (padded to 8) are one K chunk, so lane half h supplies
@@ -168,8 +191,17 @@ constexpr int SEG1 = 8;      // max tiles per segment (k_dec1)
 // tile (flat global_load_lds would keep a 64-bit VGPR address per hoisted tile live).
 template <int NW>
 STIF_DEV void dma_tiles(float* dst, __amdgpu_buffer_rsrc_t rm, int src, int ntiles, int wv, int lane) {
-  for (int k = wv; k < ntiles * 4; k += NW)
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rm, dst + k * 256, 16, lane * 16, (src + k * 256) * 4, 0, 0);
+  if ((ntiles * 4) % NW == 0) {
+    // the same number of pieces per wave, known at compile time: the compiler counts them in vmcnt, so
+    // waiting for a load issued before the DMA does not wait for the DMA
+#pragma unroll
+    for (int i = 0; i < ntiles * 4 / NW; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rm, dst + (wv + i * NW) * 256, 16, lane * 16,
+                                               (src + (wv + i * NW) * 256) * 4, 0, 0);
+  } else {
+    for (int k = wv; k < ntiles * 4; k += NW)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rm, dst + k * 256, 16, lane * 16, (src + k * 256) * 4, 0, 0);
+  }
 }
 
 STIF_DEV __amdgpu_buffer_rsrc_t mlp_rsrc(const float* mlp) {
@@ -277,6 +309,8 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
     dma_tiles<DEC_NW>(dst + 3 * T, rm, F_W3 + (8 + kt) * T, 1, wv, lane);
   };
   lds_dma_barrier();
+  const Bias32 fb1[2] = {bias_ld(mlp + F_B1, hf), bias_ld(mlp + F_B1 + 32, hf)};   // before the DMA
+  __builtin_amdgcn_sched_barrier(0);
   seg_feat23(B1, 0);
   // ---- layer 1: 64 -> 64
   {
@@ -286,17 +320,22 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
       f32x16 acc = f32x16{0};
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) tile_mma<F16>(acc, B0 + (ot * 2 + kt) * T, xs[kt], lane);
-      x1[ot] = bias_sin<F16>(acc, mlp + F_B1 + ot * 32, hf);
+      x1[ot] = bias_sin<F16>(acc, fb1[ot]);
     }
   }
   // ---- layer 2 (64 -> 256, sine) streamed into layer 3 (256 -> 64, linear)
   const XT<F16> x1s[2] = {xop<F16>(x1[0]), xop<F16>(x1[1])};
-#pragma unroll 1
-  for (int kt = 0; kt < 8; ++kt) {
+  // the streamed steps (kt = 7 peeled: its DMA differs, and the loop's steps must all issue the same
+  // number of DMA pieces for the compiler's vmcnt bookkeeping to stay exact across the back edge)
+  auto feat_step = [&](int kt, bool last) {
     lds_dma_barrier();
+    // this step's bias is loaded before the next segment's DMA is issued, so waiting for it does not
+    // wait for the DMA (vmcnt counts in issue order)
+    const Bias32 b2 = bias_ld(mlp + F_B2 + kt * 32, hf);
+    __builtin_amdgcn_sched_barrier(0);
     float* cur = (kt & 1) ? B0 : B1;
     float* nxt = (kt & 1) ? B1 : B0;
-    if (kt < 7) seg_feat23(nxt, kt + 1);
+    if (!last) seg_feat23(nxt, kt + 1);
     else {   // prefetch flow layer 0 (4 tiles) + layer 1 (4 tiles)
       dma_tiles<DEC_NW>(nxt, rm, L_W0, 4, wv, lane);
       dma_tiles<DEC_NW>(nxt + 4 * T, rm, L_W1, 4, wv, lane);
@@ -304,10 +343,13 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
     f32x16 acc = f32x16{0};
     tile_mma<F16>(acc, cur, x1s[0], lane);
     tile_mma<F16>(acc, cur + T, x1s[1], lane);
-    const XT<F16> h2 = xop<F16>(bias_sin<F16>(acc, mlp + F_B2 + kt * 32, hf));
+    const XT<F16> h2 = xop<F16>(bias_sin<F16>(acc, b2));
     tile_mma<F16>(hr[0], cur + 2 * T, h2, lane);
     tile_mma<F16>(hr[1], cur + 3 * T, h2, lane);
-  }
+  };
+#pragma unroll 1
+  for (int kt = 0; kt < 7; ++kt) feat_step(kt, false);
+  feat_step(7, true);
 #pragma unroll
   for (int ot = 0; ot < 2; ++ot) hr[ot] = bias_add<F16>(hr[ot], mlp + F_B3 + ot * 32, hf);
   if (valid) {
@@ -363,6 +405,8 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
   }
   // flow layers 0/1 live in B1 (prefetched during the last feat segment, or at the start)
   lds_dma_barrier();
+  const Bias32 lb1[2] = {bias_ld(mlp + L_B1, hf), bias_ld(mlp + L_B1 + 32, hf)};   // before the DMA
+  __builtin_amdgcn_sched_barrier(0);
   auto seg_flow23 = [&](float* dst, int kt) {   // W2 rows kt (2 tiles); W3 is resident (W3V)
     dma_tiles<DEC_NW>(dst, rm, L_W2 + kt * 2 * T, 2, wv, lane);
   };
@@ -384,23 +428,27 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
       f32x16 acc = f32x16{0};
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) tile_mma<F16>(acc, B1 + (4 + ot * 2 + kt) * T, zs[kt], lane);
-      x1[ot] = bias_sin<F16>(acc, mlp + L_B1 + ot * 32, hf);
+      x1[ot] = bias_sin<F16>(acc, lb1[ot]);
     }
   }
   const XT<F16> x1f[2] = {xop<F16>(x1[0]), xop<F16>(x1[1])};
   float fl[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-  for (int kt = 0; kt < 8; ++kt) {
+  auto flow_step = [&](int kt, bool last) {   // kt = 7 peeled (see feat_step)
     lds_dma_barrier();
+    const Bias32 b2 = bias_ld(mlp + L_B2 + kt * 32, hf);   // before the DMA (see feat_step)
+    __builtin_amdgcn_sched_barrier(0);
     float* cur = (kt & 1) ? B1 : B0;
     float* nxt = (kt & 1) ? B0 : B1;
-    if (kt < 7) seg_flow23(nxt, kt + 1);
+    if (!last) seg_flow23(nxt, kt + 1);
     f32x16 acc = f32x16{0};
     tile_mma<F16>(acc, cur, x1f[0], lane);
     tile_mma<F16>(acc, cur + T, x1f[1], lane);
-    const f32x16 h2 = bias_sin<F16>(acc, mlp + L_B2 + kt * 32, hf);
+    const f32x16 h2 = bias_sin<F16>(acc, b2);
     narrow_dot<4>(fl, W3V, kt, h2, hf);   // flow_imnet.net.3 (256 -> 4, linear)
-  }
+  };
+#pragma unroll 1
+  for (int kt = 0; kt < 7; ++kt) flow_step(kt, false);
+  flow_step(7, true);
 #pragma unroll
   for (int c = 0; c < 4; ++c) fl[c] += __shfl_xor(fl[c], 32);   // the other lane half's 128 features
   if (valid && hf == 0) {
@@ -494,6 +542,8 @@ __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DE
     }
   }
   lds_dma_barrier();
+  const Bias32 eb1[2] = {bias_ld(mlp + E_B1, hf), bias_ld(mlp + E_B1 + 32, hf)};   // before the DMA
+  __builtin_amdgcn_sched_barrier(0);
   auto seg_l23_first = [&](float* dst) {
     dma_tiles<DEC2_NW>(dst, rm, E_W2, 2, wv, lane);
 #pragma unroll
@@ -508,7 +558,7 @@ __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DE
       f32x16 acc = f32x16{0};
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) tile_mma<F16>(acc, B1 + (ot * 2 + kt) * T, xs[kt], lane);
-      x1[ot] = bias_sin<F16>(acc, mlp + E_B1 + ot * 32, hf);
+      x1[ot] = bias_sin<F16>(acc, eb1[ot]);
     }
   }
   const XT<F16> x1s[2] = {xop<F16>(x1[0]), xop<F16>(x1[1])};
@@ -522,27 +572,31 @@ __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DE
   f32x16 a3[8];
 #pragma unroll
   for (int ot = 0; ot < 8; ++ot) a3[ot] = f32x16{0};
-#pragma unroll 1
-  for (int kt = 0; kt < 8; ++kt) {
+  auto l23_step = [&](int kt, bool last) {   // kt = 7 peeled (see k_dec1's feat_step)
     lds_dma_barrier();
+    const Bias32 b2 = bias_ld(mlp + E_B2 + kt * 32, hf);   // before the DMA (see k_dec1)
+    __builtin_amdgcn_sched_barrier(0);
     float* cur = (kt & 1) ? B1 : B0;
     float* nxt = (kt & 1) ? B0 : B1;
-    if (kt < 7) seg_l23(nxt, kt + 1);
+    if (!last) seg_l23(nxt, kt + 1);
     else dma_tiles<DEC2_NW>(nxt, rm, E_W4V, 1, wv, lane);
     f32x16 acc = f32x16{0};
     tile_mma<F16>(acc, cur, x1s[0], lane);
     tile_mma<F16>(acc, cur + T, x1s[1], lane);
-    const XT<F16> h2 = xop<F16>(bias_sin<F16>(acc, mlp + E_B2 + kt * 32, hf));
+    const XT<F16> h2 = xop<F16>(bias_sin<F16>(acc, b2));
 #pragma unroll
     for (int ot = 0; ot < 8; ++ot) tile_mma<F16>(a3[ot], cur + (2 + ot) * T, h2, lane);
-  }
+  };
+#pragma unroll 1
+  for (int kt = 0; kt < 7; ++kt) l23_step(kt, false);
+  l23_step(7, true);
   // layer 3 sine streamed into layer 4 (256 -> 3, linear, VALU dot products); W4 sits in B0 as
-  // plain rows (kt = 7 prefetch)
+  // plain rows, followed by the layer-3 biases (E_W4V_B3; kt = 7 prefetch)
   lds_dma_barrier();
   float o4[3] = {0.f, 0.f, 0.f};
 #pragma unroll
   for (int kt = 0; kt < 8; ++kt) {
-    const f32x16 h3 = bias_sin<F16>(a3[kt], mlp + E_B3 + kt * 32, hf);
+    const f32x16 h3 = bias_sin<F16>(a3[kt], B0 + (E_W4V_B3 - E_W4V) + kt * 32, hf);
     narrow_dot<3>(o4, B0, kt, h3, hf);
   }
 #pragma unroll

@@ -418,6 +418,7 @@ extern "C" int stif_pack_dec_mlp_ex(const float* const* f, const float* const* l
   // plain last layers for the VALU dot products
   memcpy(d + L_W3V, l[6], sizeof(float) * 4 * 256);
   memcpy(d + E_W4V, e[8], sizeof(float) * 3 * 256);
+  memcpy(d + E_W4V_B3, d + E_B3, sizeof(float) * 256);   // layer-3 biases beside W4 (one LDS-DMA tile)
   if (flags & STIF_CONV_F16X3) {
     // every MFMA weight tile split; the fp32 image tiles (img_mma) scaled to the accumulators' 2^14
     const int regions[][2] = {{F_W1, 4}, {F_W2, 16}, {F_W3, 16}, {L_W0, 4}, {L_W1, 4}, {L_W2, 16}, {L_W3, 8},
