@@ -57,13 +57,22 @@ STIF_DEV int col_slot(int c) { return (c & 1) ? 17 + (c >> 1) : (c >> 1); }
 // the overlap is benign.  Wave w of nw issues instructions w, w + nw, ...  No divisions per lane.
 STIF_DEV void stage_image(__amdgpu_buffer_rsrc_t rs, float* dst, int iy0, int ix0, int H, int W, int Cs, int cbase,
                           int w, int nw, int lpx, int lck) {
+  // lane constants: the chunk's byte offset within a pixel, and an x bias that fails the range test
+  // for the pad chunk (lck = 8); 24-bit multiplies (pixel index < 2^24, host-checked 2-GB items)
+  const unsigned cb = (unsigned)(cbase + lck * 4) * 4u;
+  const int xpad = lck < 2 * PSUB ? 0 : (1 << 28);
+  const unsigned cs4 = (unsigned)Cs * 4u;
   for (int ins = w; ins < 30; ins += nw) {
-    const int r = ins / 5, m = ins - 5 * (ins / 5);
+    const int r = ins / 5, m = ins - 5 * (ins / 5);   // wave-uniform
     const int y = iy0 + r;
     const int slot = 7 * m + lpx;
-    const int x = ix0 + (slot < 17 ? 2 * slot : 2 * slot - 33);
-    const bool ok = ((unsigned)y < (unsigned)H) & ((unsigned)x < (unsigned)W) & (slot < HC) & (lck < 2 * PSUB);
-    const unsigned voff = ok ? (unsigned)(((y * W + x) * Cs + cbase + lck * 4) * 4) : 0x80000000u;
+    // column of the slot (even columns 0..32 in slots 0..16, odd 1..33 in 17..33; slots >= HC out of
+    // range), as shift-and-mask arithmetic so the compiler emits no divergent branch
+    const int xo = 2 * slot - (((16 - slot) >> 31) & 33) + (((HC - 1 - slot) >> 31) & (1 << 28)) + xpad;
+    const int x = ix0 + xo;
+    const unsigned off = __umul24((unsigned)(y * W + x), cs4) + cb;
+    // select, not branch: every lane's offset is computed, out-of-range ones replaced
+    const unsigned voff = (((unsigned)y < (unsigned)H) & ((unsigned)x < (unsigned)W)) ? off : 0x80000000u;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, dst + (r * OM_RP + 63 * m) * 4, 16, voff, 0, 0, 0);
   }
 }

@@ -1,8 +1,8 @@
-"""Per-wave s_memtime trace of the Winograd conv (kernel-experiment build with -DWINO_EXP_TRACE):
-average cycles of each segment between trace points per wave, and for the two waves that share a
-SIMD, how much of the time at least one of them is inside a phase (MFMA stream).  STIF_HIP_LIB must
-point at the trace build.  Tags: 1 tile start, 6 before a phase barrier, 2 after it, 3 after the
-exchange barrier(s), 4 after the final epilogue barrier, 5 end of the tile."""
+"""Per-wave s_memtime trace of the f16x3 Winograd conv (tools/exp_trace.so, built by
+tools/experiments/make_wino_trace.py): average cycles of each segment between trace points per wave,
+and for the two waves that share a SIMD, how much of the time at least one of them is inside a phase
+(MFMA stream).  Tags: 1 tile start, 6 before a phase's wait+barrier, 2 after it, 3 after an exchange
+barrier, 5 before the closing barrier, 4 after it.  Env: N, HW (trunk shape N x HW x HW x 64), EPI."""
 import ctypes as C
 import os
 import sys
@@ -11,19 +11,22 @@ from collections import defaultdict
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+os.environ.setdefault("STIF_HIP_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(
+    os.path.abspath(__file__)))), "tools", "exp_trace.so"))
 import stif_pkg  # noqa: E402
 
 stif = stif_pkg.load()
 L, ops = stif._lib, stif.ops
-N, H, W = int(os.environ.get("N", 18)), 256, 256
+N, H = int(os.environ.get("N", 18)), int(os.environ.get("HW", 128))
+W = H
 EPI = int(os.environ.get("EPI", L.EPI_RELU))
 rng = np.random.default_rng(0)
 w = (rng.standard_normal((64, 64, 3, 3)) * 0.05).astype(np.float32)
 b = rng.standard_normal(64).astype(np.float32)
 x = torch.randn(N, H, W, 64, device="cuda")
 r = torch.randn(N, H, W, 64, device="cuda")
-lay = ops.pack_conv(w, b, L.PACK_WINO | (L.PACK_F16X3 if os.environ.get("F16") else 0))
+lay = ops.pack_conv(w, b, L.PACK_WINO | L.PACK_F16X3)
 out = torch.empty(N, H, W, 64, device="cuda")
 for _ in range(3):
     ops.conv2d([dict(layer=lay, in0=x, out=out, res=r)], epi=EPI)
@@ -43,11 +46,11 @@ for blk in range(512):
         hw = int(tr[blk, wv, 127])
         xcc, hid = hw >> 32, hw & 0xFFFFFFFF
         simd[(xcc & 0xF, (hid >> 8) & 0xF, (hid >> 12) & 1, (hid >> 13) & 7, (hid >> 4) & 3)].append((blk, wv))
-names = {1: "start", 6: "pre-bar", 2: "post-bar", 3: "xchg", 4: "comb", 5: "stored"}
+names = {1: "start", 6: "pre-bar", 2: "post-bar", 3: "xchg", 4: "end-bar", 5: "stored"}
 for k in sorted(seg):
     v = np.array(seg[k])
     print(f"wave {k[0]} {names[k[1]]:>8s} -> {names[k[2]]:<8s} n={len(v):5d} avg {v.mean():8.0f} med {np.median(v):8.0f} cyc")
-print("MFMA cycles per tile per wave at peak:", 4 * 24 * 32 if os.environ.get("F16") else 256 * 64)
+print("MFMA cycles per tile per wave at peak (C0 = 64 -> 64):", 96 * 32)
 
 
 def phase_intervals(blk, wv):
