@@ -17,10 +17,10 @@ NOPK_SRC := wino decoder conv resample
 
 all: $(LIB)
 
-$(OBJDIR)/%.o: $(PKG)/csrc/%.hip $(HDR) | $(OBJDIR)
+$(OBJDIR)/%.o: $(PKG)/csrc/%.hip $(HDR) Makefile | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) $(if $(filter $*,$(NOPK_SRC)),$(NOPK)) -c -o $@ $<
 
-$(OBJDIR)/pack.o: $(PKG)/csrc/pack.cpp $(HDR) | $(OBJDIR)
+$(OBJDIR)/pack.o: $(PKG)/csrc/pack.cpp $(HDR) Makefile | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
 $(OBJDIR):
