@@ -57,10 +57,10 @@ def kernel_desc(kind, mfma="f32"):
                     "couts per tile (3 fp16 products per fp32-class product); algorithmic = direct-conv FLOPs, peak = "
                     "fp16 MFMA dense peak / 3 x 36/16", F16X3_PEAK_TFLOPS * WINO_GAIN)
         if f16:
-            return (f"k_wino<{in1}, {epi}, 0, 1>", f"3x3 {64 * (2 if in1 else 1)}->{cout} conv, EPI_{EPI_NAMES[epi]}, "
+            return (f"k_wino<{in1}, {epi}, 1>", f"3x3 {64 * (2 if in1 else 1)}->{cout} conv, EPI_{EPI_NAMES[epi]}, "
                     "Winograd F(2x2,3x3) on split-fp16 MFMA (3 fp16 products per fp32-class product); algorithmic = "
                     "direct-conv FLOPs, peak = fp16 MFMA dense peak / 3 x 36/16", F16X3_PEAK_TFLOPS * WINO_GAIN)
-        return (f"k_wino<{in1}, {epi}, 0, 0>", f"3x3 {64 * (2 if in1 else 1)}->{cout} conv, EPI_{EPI_NAMES[epi]}, "
+        return (f"k_wino<{in1}, {epi}, 0>", f"3x3 {64 * (2 if in1 else 1)}->{cout} conv, EPI_{EPI_NAMES[epi]}, "
                 f"Winograd F(2x2,3x3) on fp32 MFMA; algorithmic = direct-conv FLOPs, peak = fp32 MFMA peak x 36/16",
                 FP32_PEAK_TFLOPS * WINO_GAIN)
     if kind[0] == "conv":
