@@ -1,7 +1,7 @@
 """Build tools/exp_trace.so: the engine library with k_wino (F16 path) instrumented by a per-wave
 s_memtime event trace, patched into a temporary copy of the sources (the product kernel carries no
 trace hooks).  Tags: 1 tile start, 6 before a phase's wait+barrier, 2 after it, 3 after an exchange
-barrier, 5 before the closing barrier, 4 after it.  Read with tools/experiments/trace_wino.py."""
+barrier, 5 before the closing barrier, 4 after it, 7 tile setup done (accumulators zeroed), 8 / 9 after sub-phase 0 / 1 of a phase.  Read with tools/experiments/trace_wino.py."""
 import os
 import shutil
 import subprocess
@@ -71,8 +71,23 @@ sub('''          wb[((r & 3) + 8 * (r >> 2)) * 32 + ((r & 1) ? -fl : fl)] = yv[n
 sub('''    if (F16) report_range(a.status, not_finite(chk));   // a non-finite output makes the sum non-finite
     __syncthreads();   // exchange buffer free for the next tile's staging''', '''    if (F16) report_range(a.status, not_finite(chk));   // a non-finite output makes the sum non-finite
     WTR(5);
+    STORE_WAIT
     __syncthreads();   // exchange buffer free for the next tile's staging
     WTR(4);''')
+sub('''            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+        WTR(6);''', '''            __builtin_amdgcn_sched_barrier(0);
+          }
+          WTR(8 + sp);
+        }
+        WTR(6);''')
+sub('''    if constexpr (F16) {
+      for (int p = 0; p < NP; ++p, ++gp) {''', '''    if constexpr (F16) {
+      WTR(7);
+      for (int p = 0; p < NP; ++p, ++gp) {''')
+# STORE_WAIT=1: drain the tile's output stores before the closing barrier (probe of store latency)
+s = s.replace("STORE_WAIT", 'asm volatile("s_waitcnt vmcnt(0)" ::: "memory");' if os.environ.get("STORE_WAIT") else "")
 s += '''
 extern "C" int stif_exp_wino_trace(unsigned long long* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wtrace), sizeof(g_wtrace)) == hipSuccess ? 0 : -1;
@@ -81,7 +96,7 @@ extern "C" int stif_exp_wino_trace(unsigned long long* host) {
 open(p, "w").write(s)
 src = [os.path.join(T, "csrc", f) for f in sorted(os.listdir(os.path.join(T, "csrc"))) if f.endswith(".hip")]
 src.append(os.path.join(T, "csrc", "pack.cpp"))
-out = os.path.join(R, "tools", "exp_trace.so")
+out = os.path.join(R, "tools", os.environ.get("OUT", "exp_trace.so"))
 subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
                        "-I" + os.path.join(R, "include"), "-I" + os.path.join(T, "csrc"), "-shared", "-o", out] + src)
 shutil.rmtree(T)

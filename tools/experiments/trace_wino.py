@@ -2,7 +2,7 @@
 tools/experiments/make_wino_trace.py): average cycles of each segment between trace points per wave,
 and for the two waves that share a SIMD, how much of the time at least one of them is inside a phase
 (MFMA stream).  Tags: 1 tile start, 6 before a phase's wait+barrier, 2 after it, 3 after an exchange
-barrier, 5 before the closing barrier, 4 after it.  Env: N, HW (trunk shape N x HW x HW x 64), EPI."""
+barrier, 5 before the closing barrier, 4 after it, 7 tile setup done.  Env: N, HW (trunk shape N x HW x HW x 64), EPI."""
 import ctypes as C
 import os
 import sys
@@ -46,7 +46,7 @@ for blk in range(512):
         hw = int(tr[blk, wv, 127])
         xcc, hid = hw >> 32, hw & 0xFFFFFFFF
         simd[(xcc & 0xF, (hid >> 8) & 0xF, (hid >> 12) & 1, (hid >> 13) & 7, (hid >> 4) & 3)].append((blk, wv))
-names = {1: "start", 6: "pre-bar", 2: "post-bar", 3: "xchg", 4: "end-bar", 5: "stored"}
+names = {1: "start", 6: "pre-bar", 2: "post-bar", 3: "xchg", 4: "end-bar", 5: "stored", 7: "setup", 8: "sp0", 9: "sp1"}
 for k in sorted(seg):
     v = np.array(seg[k])
     print(f"wave {k[0]} {names[k[1]]:>8s} -> {names[k[2]]:<8s} n={len(v):5d} avg {v.mean():8.0f} med {np.median(v):8.0f} cyc")
@@ -58,7 +58,7 @@ def phase_intervals(blk, wv):
     ev = [(int(v) >> 8, int(v) & 0xFF) for v in tr[blk, wv, :127] if v]
     iv = []
     for (t0, a), (t1, bb) in zip(ev, ev[1:]):
-        if a in (1, 2) and bb == 6:
+        if a in (7, 2) and bb == 8:
             iv.append((t0, t1))
     return iv, (ev[0][0], ev[-1][0]) if ev else (0, 0)
 
