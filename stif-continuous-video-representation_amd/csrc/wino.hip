@@ -79,6 +79,8 @@ STIF_DEV void stage_image(__amdgpu_buffer_rsrc_t rs, float* dst, int iy0, int ix
 
 struct Tile {
   int oy0, ox0, slice, g, n;
+  const float* src0;   // the item's input maps (k_wino: in0 and in1 of group g, item n), loaded from the
+  const float* src1;   // kernel arguments once per tile, not per staging phase
 };
 
 // Persistent: WG_PER_CU workgroups per CU walk the tiles (tile = 4 output rows x 32 columns x one
@@ -118,6 +120,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     t.n = r - t.g * a.nitems;
     t.oy0 = y * WR;
     t.ox0 = x * 32;
+    t.src0 = a.in0[t.g] + (size_t)t.n * a.in0_item;
+    t.src1 = IN1 ? a.in1[t.g] + (size_t)t.n * a.in1_item : t.src0;
     return t;
   };
   // packed U: [slice][chunk][i][j][nt][lane][4]; B fragment (j, local half u) at wsl + (j*2 + u)*256
@@ -133,7 +137,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   auto stage = [&](const Tile& t, int p, int buf) {
     // a phase lies entirely in one input (NC0 % PSUB == 0, host-checked)
     const bool second = IN1 && p * PSUB >= NC0;
-    const float* src = second ? a.in1[t.g] + (size_t)t.n * a.in1_item : a.in0[t.g] + (size_t)t.n * a.in0_item;
+    const float* src = second ? t.src1 : t.src0;
     const int Cs = second ? C1 : C0;
     const int cbase = (second ? p * PSUB - NC0 : p * PSUB) * 8;
     const __amdgpu_buffer_rsrc_t rs =
@@ -216,11 +220,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 
     if constexpr (F16) {
       for (int p = 0; p < NP; ++p, ++gp) {
-        if (p + 1 < NP) stage(cur, p + 1, (gp + 1) & 1);
-        else if (has_next) stage(nxt, 0, (gp + 1) & 1);
         const float* buf = smem + (gp & 1) * BUF_F;
         f32x4 rd[8];
+        // the phase's first LDS reads go out before the next phase's LDS-DMA is issued, so the DMA
+        // issue (~1K cycles per wave) overlaps their latency instead of preceding it
         xread(buf, 0, rd);
+        if (p + 1 < NP) stage(cur, p + 1, (gp + 1) & 1);
+        else if (has_next) stage(nxt, 0, (gp + 1) & 1);
 #pragma unroll
         for (int sp = 0; sp < PSUB / 2; ++sp) {
           // chunk pair (2 sp, 2 sp + 1): lane half h holds channels 4h..4h+3 of both, i.e. the 8
