@@ -19,6 +19,8 @@
 #include "stif.h"
 #include "abi_util.h"
 
+#include <algorithm>
+
 namespace {
 
 // F16 (the 3x3 64 -> 64 convs with weights packed STIF_PACK_PLAIN | STIF_PACK_F16X3, as the DCN
@@ -297,6 +299,88 @@ __global__ __launch_bounds__(NW * 64) void k_conv(stif_conv_args a) {
   }
 }
 
+// ---------------------------------------------------------------- 1x1 convs on split-fp16 MFMA
+// k_conv1x1: the 1x1 128 -> 64 convs of the STIF graph (Easy_PCD / PCD fusion on cat(a, b), the
+// ConvBLSTM conv_1x1; Sakuya_arch_test.py:141,254), f16x3, EPI_NONE.  HBM-bound (768 B and 16 KFLOP
+// per pixel), so the kernel is built for memory-level parallelism: the slice's weights (8 16-channel
+// chunks x 2 N-tiles x 2 planes = 32 KB) are LDS-DMA'd once per workgroup, and each wave walks
+// 32-pixel M-tiles, issuing all 16 of a tile's 16-B activation loads per lane (the pixel's 8
+// consecutive channels 16 c + 8 h.. of chunk c for lane half h) before its first MFMA, then 48
+// MFMAs; outputs leave as b32 stores, a half-wave writing one pixel's 32 couts (128 B).  Tiles never
+// straddle items (an item's last tile is partial: its lanes past H * W load the last pixel and store
+// nothing).  Pixel p of item n: in0 + n * in0_item + p * 64 (in1 alike).  114 VGPRs, 32 KB LDS: four
+// workgroups per CU.
+constexpr int C1X1_NC = 8;   // 16-channel chunks: 64 from in0 + 64 from in1
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_conv1x1(stif_conv_args a,
+                                                                                      int tiles_per_item) {
+  __shared__ __attribute__((aligned(16))) float sw[C1X1_NC * 1024];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hf = lane >> 5, l32 = lane & 31;
+  const int slice = blockIdx.y, g = blockIdx.z;
+  const float* wsl = a.w[g] + (size_t)slice * C1X1_NC * 1024;
+  for (int i = wv; i < C1X1_NC * 4; i += 4)
+    __builtin_amdgcn_global_load_lds(wsl + (i * 64 + lane) * 4, sw + i * 256, 16, 0, 0);
+  lds_dma_barrier();
+  const int ntiles = tiles_per_item * a.nitems;
+  const int HW = a.H * a.W;
+  const float b0 = a.bias[g][slice * 64 + l32], b1 = a.bias[g][slice * 64 + 32 + l32];
+  bool bad = false;
+  for (int mt = blockIdx.x * 4 + wv; mt < ntiles; mt += gridDim.x * 4) {
+    const int n = mt / tiles_per_item, p0 = (mt - n * tiles_per_item) * 32;
+    const size_t px = (size_t)min(p0 + l32, HW - 1);
+    const float* x0 = a.in0[g] + (size_t)n * a.in0_item + px * 64 + 8 * hf;
+    const float* x1 = a.in1[g] + (size_t)n * a.in1_item + px * 64 + 8 * hf;
+    f32x4 xv[C1X1_NC][2];
+#pragma unroll
+    for (int c = 0; c < C1X1_NC; ++c) {
+      const float* xp = (c < C1X1_NC / 2 ? x0 : x1) + 16 * (c % (C1X1_NC / 2));
+      xv[c][0] = ld4(xp);
+      xv[c][1] = ld4(xp + 4);
+    }
+    f32x16 acc0 = f32x16{0}, acc1 = f32x16{0};
+#pragma unroll
+    for (int c = 0; c < C1X1_NC; ++c) {
+      f16x8 ah, al;
+      split_f16x3(xv[c][0], xv[c][1], ah, al);
+      const float* wp = sw + c * 1024 + lane * 4;   // [chunk][nt][plane][lane][8 halves]
+      const f16x8 bh0 = ldh8(wp), bl0 = ldh8(wp + 256), bh1 = ldh8(wp + 512), bl1 = ldh8(wp + 768);
+      acc0 = mfma16h(ah, bh0, acc0);
+      acc1 = mfma16h(ah, bh1, acc1);
+      acc0 = mfma16h(ah, bl0, acc0);
+      acc1 = mfma16h(ah, bl1, acc1);
+      acc0 = mfma16h(al, bh0, acc0);
+      acc1 = mfma16h(al, bh1, acc1);
+    }
+    float* o = a.out[g] + (size_t)n * a.out_item + (size_t)p0 * a.cout + slice * 64 + l32;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float v0 = acc0[r] * F16X3_UNSCALE + b0, v1 = acc1[r] * F16X3_UNSCALE + b1;
+      bad |= not_finite(v0 + v1);
+      const int pr = mfma_row(r, lane);
+      if (p0 + pr < HW) {
+        o[(size_t)pr * a.cout] = v0;
+        o[(size_t)pr * a.cout + 32] = v1;
+      }
+    }
+  }
+  report_range(a.status, bad);
+}
+
+int launch_conv1x1(const stif_conv_args& a, hipStream_t st) {
+  const int tpi = (a.H * a.W + 31) / 32;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  const long long wgs = ((long long)tpi * a.nitems + 3) / 4;
+  // four workgroups per CU over all (slice, group) grid planes, each walking several M-tiles
+  const int per = a.ngroups * (a.cout / 64);
+  const int gx = (int)std::max<long long>(1, std::min<long long>(wgs, (4LL * cus + per - 1) / per));
+  hipLaunchKernelGGL(k_conv1x1, dim3(gx, a.cout / 64, a.ngroups), dim3(256), 0, st, a, tpi);
+  return stif_check_launch("stif_conv2d_nhwc");
+}
+
 template <int KS, int S, int MT, int NT, int NW, int IN1, int EPI, int F16 = 0>
 int launch(const stif_conv_args& a, hipStream_t st) {
   constexpr int TH = NW * MT;
@@ -364,8 +448,11 @@ extern "C" int stif_conv2d_nhwc(const stif_conv_args* pa, void* stream) {
   if (a.ngroups < 1 || a.ngroups > STIF_MAX_GROUPS || a.nitems < 1)
     return stif_fail(STIF_E_INVALID, "stif_conv2d_nhwc: bad ngroups/nitems");
   const bool f16 = a.flags & STIF_CONV_F16X3;
-  if (f16 && !(a.ks == 3 && a.stride == 2 && a.cout == 64 && a.C0 == 64 && a.in1_mode == 0))
-    return stif_fail(STIF_E_INVALID, "stif_conv2d_nhwc: STIF_CONV_F16X3 takes the 3x3 stride-2 64 -> 64 convs only");
+  const bool f16_1x1 = a.ks == 1 && a.stride == 1 && a.in1_mode == 1 && a.C0 == 64 && a.C1 == 64 &&
+                       a.cout % 64 == 0 && a.epi == STIF_EPI_NONE;
+  if (f16 && !(a.ks == 3 && a.stride == 2 && a.cout == 64 && a.C0 == 64 && a.in1_mode == 0) && !f16_1x1)
+    return stif_fail(STIF_E_INVALID, "stif_conv2d_nhwc: STIF_CONV_F16X3 takes the 3x3 stride-2 64 -> 64 convs and "
+                                     "the 1x1 (64 | 64) -> 64k convs only");
   if (a.C0 % 8 || a.C0 <= 0 || (a.in1_mode && (a.C1 % 8 || a.C1 <= 0)))
     return stif_fail(STIF_E_INVALID, "stif_conv2d_nhwc: channel counts must be multiples of 8");
   const int pad = a.ks / 2;
@@ -398,6 +485,7 @@ extern "C" int stif_conv2d_nhwc(const stif_conv_args* pa, void* stream) {
     return stif_fail(STIF_E_INVALID, "strided conv: unsupported epilogue");
   }
   if (a.ks == 1) {
+    if (f16) return launch_conv1x1(a, st);
     if (a.epi != STIF_EPI_NONE) return stif_fail(STIF_E_INVALID, "1x1 conv: unsupported epilogue");
     if (a.in1_mode == 0) return launch<1, 1, 2, 2, 4, 0, STIF_EPI_NONE>(a, st);
     if (a.in1_mode == 1) return launch<1, 1, 2, 2, 4, 1, STIF_EPI_NONE>(a, st);

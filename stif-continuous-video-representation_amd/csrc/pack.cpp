@@ -97,7 +97,9 @@ std::vector<float> omega(const float* src, size_t n) {
 
 extern "C" size_t stif_conv_weight_floats(int cout, int cin, int ks, int mode) {
   // PLAIN | F16X3 (the DCN core, 64 -> 64 3x3): 5 tap pairs x 2 nt x 2 planes x 1 KB per 8-channel group
-  if (mode == (STIF_PACK_PLAIN | STIF_PACK_F16X3)) return (size_t)(cin / 8) * 5 * 2 * 2 * 256;
+  if (mode == (STIF_PACK_PLAIN | STIF_PACK_F16X3) && ks == 3) return (size_t)(cin / 8) * 5 * 2 * 2 * 256;
+  // PLAIN | F16X3 1x1 (k_conv1x1): 2 nt x 2 planes x 1 KB per (64-cout slice, 16-channel chunk) = the
+  // plain size below
   mode &= ~STIF_PACK_F16X3;   // Winograd: same bytes, two fp16 planes per fp32 value
   if (mode == STIF_PACK_WINO || mode == STIF_PACK_WINO_OFFMASK || mode == STIF_PACK_WINO_LSTM)
     return (size_t)round64(cout) * cin * 16;
@@ -220,6 +222,28 @@ int pack_wino_f16x3(const float* w, const float* b, int cout, int cin, int perm,
     }
   return STIF_OK;
 }
+// PLAIN | F16X3, 1x1 (k_conv1x1): [slice][chunk c16][nt][plane][lane][8 halves]; element e of lane l
+// holds input channel 16 c16 + 8 (l >> 5) + e of cout slice * 64 + nt * 32 + (l & 31) -- lane half h
+// supplies its pixel's 8 consecutive channels 16 c16 + 8 h .. as the A operand -- as W * 2^10 split
+int pack_1x1_f16x3(const float* w, const float* b, int cout, int cin, float* w_dst, float* b_dst) {
+  if (cin % 16 || cout % 64) return stif_fail(STIF_E_INVALID, "PLAIN | F16X3 1x1 packing needs cin % 16 == 0, cout % 64 == 0");
+  for (size_t i = 0; i < (size_t)cout * cin; ++i)
+    if (!f16x3_ok(w[i])) return range_fail("stif_pack_conv_weight: a weight is outside the f16x3 range (|w| < 64); pack it without STIF_PACK_F16X3");
+  const int NS = cout / 64, NC = cin / 16;
+  _Float16* dst = reinterpret_cast<_Float16*>(w_dst);
+  for (int s = 0; s < NS; ++s)
+    for (int c = 0; c < NC; ++c)
+      for (int nt = 0; nt < 2; ++nt)
+        for (int l = 0; l < 64; ++l)
+          for (int e = 0; e < 8; ++e) {
+            const int co = s * 64 + nt * 32 + (l & 31), ci = 16 * c + 8 * (l >> 5) + e;
+            const size_t o = (((((size_t)s * NC + c) * 2 + nt) * 2) * 64 + l) * 8 + e;
+            split_f16x3_host((double)w[(size_t)co * cin + ci], dst + o, dst + o + 512);
+          }
+  if (b_dst)
+    for (int j = 0; j < cout; ++j) b_dst[j] = b ? b[j] : 0.f;
+  return STIF_OK;
+}
 }  // namespace
 
 extern "C" int stif_pack_conv_weight(const float* w, const float* b, int cout, int cin, int ks, int mode,
@@ -237,6 +261,7 @@ extern "C" int stif_pack_conv_weight(const float* w, const float* b, int cout, i
     const int perm = mode == STIF_PACK_WINO ? STIF_PACK_PLAIN : (mode == STIF_PACK_WINO_OFFMASK ? STIF_PACK_OFFMASK : mode);
     return f16x3 ? pack_wino_f16x3(w, b, cout, cin, perm, w_dst, b_dst) : pack_wino(w, b, cout, cin, perm, w_dst, b_dst);
   }
+  if (f16x3 && mode == STIF_PACK_PLAIN && ks == 1) return pack_1x1_f16x3(w, b, cout, cin, w_dst, b_dst);
   if (f16x3 && mode == STIF_PACK_PLAIN) {
     if (ks != 3 || cout != 64 || cin != 64)
       return stif_fail(STIF_E_INVALID, "PLAIN | F16X3 (DCN core) packing needs a 64 -> 64 3x3 weight");

@@ -169,8 +169,9 @@ class LunaTokis(nn.Module):
 
         # 3x3 / stride-1 / 64-cout convs run by Winograd F(2x2,3x3) (stif_conv3x3_wino; the
         # cat(., up(.)) ones on a materialised x2-upsampled second input), as do the offset/mask
-        # (64 -> 216) and ConvLSTMCell (128 -> 256, gate epilogue) convs; the strided and 1x1
-        # convs keep the direct kernel.
+        # (64 -> 216) and ConvLSTMCell (128 -> 256, gate epilogue) convs; the strided convs keep the
+        # direct kernel, the 1x1 cat convs (fusion, conv_1x1) run k_conv1x1 (f16x3) or the direct
+        # kernel (f32).
         f16 = L.PACK_F16X3 if self.mfma == "f16x3" else 0
         wino = (L.PACK_WINO | f16) if self.winograd else L.PACK_PLAIN
 
@@ -195,16 +196,16 @@ class LunaTokis(nn.Module):
                         conv(n, wino)
 
         pcd("pcd_align.")
-        conv("fusion")
+        conv("fusion", L.PACK_PLAIN | f16)
         conv("ConvBLSTM.forward_net.cell_list.0.conv", (L.PACK_WINO_LSTM | f16) if self.winograd else L.PACK_LSTM)
         for p in ("ConvBLSTM.forward_net.pcd_h.", "ConvBLSTM.forward_net.pcd_c."):
             for n in ("fea_L2_conv1", "fea_L3_conv1"):
                 conv(p + n, L.PACK_PLAIN | f16)
-            conv(p + "fusion")
+            conv(p + "fusion", L.PACK_PLAIN | f16)
             for n in ("fea_L2_conv2", "fea_L3_conv2"):
                 conv(p + n, wino)
             pcd(p + "pcd_align.")
-        conv("ConvBLSTM.conv_1x1")
+        conv("ConvBLSTM.conv_1x1", L.PACK_PLAIN | f16)
         for i in range(self.back_RBs):
             conv(f"recon_trunk.{i}.conv1", wino)
             conv(f"recon_trunk.{i}.conv2", wino)

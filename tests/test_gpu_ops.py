@@ -121,6 +121,38 @@ def test_conv1x1_wide(ops, L):
     assert relmax(to_nchw(out), O.conv2d(x, w, b)) < RTOL
 
 
+@pytest.mark.parametrize("hw", [(12, 20), (7, 13), (32, 48)])   # 240 and 91 px: partial last M-tile
+def test_conv1x1_cat_f16x3(ops, L, hw):
+    """k_conv1x1 (the fusion / conv_1x1 convs on cat(a, b), split-fp16): two weight groups over
+    strided item views, items whose pixel count is not a multiple of the 32-pixel M-tile."""
+    H, W = hw
+    fr = rnd(6, 64, H, W, seed=40)
+    wa, wb = rnd(64, 128, 1, 1, seed=41, scale=0.1), rnd(64, 128, 1, 1, seed=42, scale=0.1)
+    ba, bb = rnd(64, seed=43), rnd(64, seed=44)
+    t = nhwc(fr)
+    f1, f2 = t[0::2], t[1::2]
+    out = torch.full((2, 3, H, W, 64), float("nan"), device="cuda")
+    la, lb = ops.pack_conv(wa, ba, L.PACK_PLAIN | L.PACK_F16X3), ops.pack_conv(wb, bb, L.PACK_PLAIN | L.PACK_F16X3)
+    assert la.mode & L.PACK_F16X3 and lb.mode & L.PACK_F16X3
+    ops.conv2d([dict(layer=la, in0=f1, in1=f2, out=out[0]), dict(layer=lb, in0=f2, in1=f1, out=out[1])], in1_mode=1)
+    refa = O.conv2d(np.concatenate([fr[0::2], fr[1::2]], 1), wa, ba)
+    refb = O.conv2d(np.concatenate([fr[1::2], fr[0::2]], 1), wb, bb)
+    assert bool(torch.isfinite(out).all())   # every pixel written, none past the item
+    assert relmax(to_nchw(out[0]), refa) < RTOL
+    assert relmax(to_nchw(out[1]), refb) < RTOL
+
+
+def test_conv1x1_f16x3_range_status(ops, L):
+    """An activation past the split-fp16 range turns the 1x1 outputs non-finite and sets the status."""
+    x0, x1 = rnd(1, 64, 8, 8, seed=45), rnd(1, 64, 8, 8, seed=46)
+    x1[0, 3, 2, 2] = 1e6
+    lay = ops.pack_conv(rnd(64, 128, 1, 1, seed=47, scale=0.1), rnd(64, seed=48), L.PACK_PLAIN | L.PACK_F16X3)
+    st = torch.zeros(1, dtype=torch.int32, device="cuda")
+    out = torch.empty(1, 8, 8, 64, device="cuda")
+    ops.conv2d([dict(layer=lay, in0=nhwc(x0), in1=nhwc(x1), out=out)], in1_mode=1, status=st)
+    assert int(st.item()) == 1
+
+
 def test_offmask_conv(ops, L):
     x = rnd(2, 64, 10, 40, seed=20)
     w = rnd(216, 64, 3, 3, seed=21, scale=0.05)

@@ -1,11 +1,11 @@
 #!/bin/bash
-# Build the engine library of a git revision (default HEAD) with that revision's Makefile as
-# tools/exp_base.so, for same-box A/B runs against the working tree's in-tree build (tools/r2_ab*.sh).
+# Export a git revision (default HEAD) -- sources, scripts, bench -- to tools/base_tree/ and build its
+# library with that revision's Makefile; also copy the library to tools/exp_base.so.  Same-box A/B
+# runs (tools/r2_ab*.sh) time the working tree against it.
 set -e
 cd "$(dirname "$0")/.."
 REV=${1:-HEAD}
-T=$(mktemp -d)
-git archive "$REV" Makefile stif-continuous-video-representation_amd/csrc include | tar -x -C "$T"
-make -C "$T" -j8 > "$T/build.log" 2>&1 || { tail -20 "$T/build.log"; exit 1; }
-cp "$T/stif-continuous-video-representation_amd/libstif_hip.so" tools/exp_base.so
-rm -rf "$T"
+rm -rf tools/base_tree && mkdir -p tools/base_tree
+git archive "$REV" -- . ':!tests/golden' ':!profiles' ':!tools' | tar -x -C tools/base_tree
+make -C tools/base_tree -j8 > tools/base_tree/build.log 2>&1 || { tail -20 tools/base_tree/build.log; exit 1; }
+cp tools/base_tree/stif-continuous-video-representation_amd/libstif_hip.so tools/exp_base.so
