@@ -272,10 +272,13 @@ size_t stif_conv_bias_floats(int cout, int mode);
 int stif_pack_conv_weight(const float* w_oihw, const float* b, int cout, int cin, int ks, int mode,
                           float* w_dst, float* b_dst);
 
-size_t stif_dec_proj_floats(void);   /* packed 1x1 weight of the LR projection: [25][256][1][8] */
+size_t stif_dec_proj_floats(void);   /* packed fp32 1x1 weight of the LR projection: [25][256][1][8]; the
+                                        f16x3 packing: stif_conv_weight_floats(256, 200, 1, STIF_PACK_PLAIN | STIF_PACK_F16X3) */
 int stif_pack_dec_proj(const float* feat_w0, const float* feat_b0, const float* flow_w0,
                        const float* enc_w0, float* w_dst, float* b_dst);
-/* lr_image = 0: P2..P4 without the image columns (decoding_test samples a high-resolution image) */
+/* lr_image bit 0 clear: P2..P4 without the image columns (decoding_test samples a high-resolution
+ * image); lr_image | STIF_PACK_F16X3: the PLAIN | F16X3 1x1 packing for stif_conv2d_nhwc with
+ * flags = STIF_CONV_F16X3 (split-fp16 k_conv1x1) */
 int stif_pack_dec_proj_ex(const float* feat_w0, const float* feat_b0, const float* flow_w0,
                           const float* enc_w0, int lr_image, float* w_dst, float* b_dst);
 size_t stif_dec_mlp_floats(void);

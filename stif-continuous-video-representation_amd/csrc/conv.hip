@@ -300,45 +300,52 @@ __global__ __launch_bounds__(NW * 64) void k_conv(stif_conv_args a) {
 }
 
 // ---------------------------------------------------------------- 1x1 convs on split-fp16 MFMA
-// k_conv1x1: the 1x1 128 -> 64 convs of the STIF graph (Easy_PCD / PCD fusion on cat(a, b), the
-// ConvBLSTM conv_1x1; Sakuya_arch_test.py:141,254), f16x3, EPI_NONE.  HBM-bound (768 B and 16 KFLOP
-// per pixel), so the kernel is built for memory-level parallelism: the slice's weights (8 16-channel
-// chunks x 2 N-tiles x 2 planes = 32 KB) are LDS-DMA'd once per workgroup, and each wave walks
-// 32-pixel M-tiles, issuing all 16 of a tile's 16-B activation loads per lane (the pixel's 8
-// consecutive channels 16 c + 8 h.. of chunk c for lane half h) before its first MFMA, then 48
-// MFMAs; outputs leave as b32 stores, a half-wave writing one pixel's 32 couts (128 B).  Tiles never
-// straddle items (an item's last tile is partial: its lanes past H * W load the last pixel and store
-// nothing).  Pixel p of item n: in0 + n * in0_item + p * 64 (in1 alike).  114 VGPRs, 32 KB LDS: four
-// workgroups per CU.
-constexpr int C1X1_NC = 8;   // 16-channel chunks: 64 from in0 + 64 from in1
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_conv1x1(stif_conv_args a,
-                                                                                      int tiles_per_item) {
-  __shared__ __attribute__((aligned(16))) float sw[C1X1_NC * 1024];
+// k_conv1x1<NC, IN1>: the 1x1 convs of the STIF graph on split-fp16 MFMA, EPI_NONE -- the (64 | 64) ->
+// 64 cat convs (Easy_PCD / PCD fusion, ConvBLSTM conv_1x1; Sakuya_arch_test.py:141,254; NC = 8,
+// IN1) and the decoder's LR projection 200 -> 256 (NC = 13, the last 16-channel chunk half used).
+// HBM-bound (e.g. 768 B and 16 KFLOP per pixel for the cat convs), so the kernel is built for
+// memory-level parallelism: the 64-cout slice's weights (NC 16-channel chunks x 2 N-tiles x 2 planes)
+// are LDS-DMA'd once per workgroup, and each wave walks 32-pixel M-tiles, issuing all of a tile's
+// 16-B activation loads per lane (its pixel's 8 consecutive channels 16 c + 8 h.. of chunk c for lane
+// half h) before its first MFMA; outputs leave as b32 stores, a half-wave writing one pixel's 32
+// couts (128 B).  Tiles never straddle items (an item's last tile is partial: its lanes past H * W
+// load the last pixel and store nothing).  Pixel p of item n: in0 + n * in0_item + p * C0 (in1 alike).
+template <int NC, int IN1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(IN1 ? 4 : 2))) void k_conv1x1(stif_conv_args a,
+                                                                                                int tiles_per_item) {
+  __shared__ __attribute__((aligned(16))) float sw[NC * 1024];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hf = lane >> 5, l32 = lane & 31;
   const int slice = blockIdx.y, g = blockIdx.z;
-  const float* wsl = a.w[g] + (size_t)slice * C1X1_NC * 1024;
-  for (int i = wv; i < C1X1_NC * 4; i += 4)
-    __builtin_amdgcn_global_load_lds(wsl + (i * 64 + lane) * 4, sw + i * 256, 16, 0, 0);
+  const float* wsl = a.w[g] + (size_t)slice * NC * 1024;
+  // (through a plain pointer: the builtin on the dependent-size __shared__ array itself makes this
+  // clang drop the kernel's host launch stub)
+  float* const swp = sw;
+  for (int i = wv; i < NC * 4; i += 4)
+    __builtin_amdgcn_global_load_lds(wsl + (i * 64 + lane) * 4, swp + i * 256, 16, 0, 0);
   lds_dma_barrier();
   const int ntiles = tiles_per_item * a.nitems;
-  const int HW = a.H * a.W;
+  const int HW = a.H * a.W, C0 = IN1 ? 64 : a.C0, C1 = 64;   // host: (64 | 64) or one C0-channel input
+  constexpr int NC0 = IN1 ? NC / 2 : NC;   // chunks read from in0
   const float b0 = a.bias[g][slice * 64 + l32], b1 = a.bias[g][slice * 64 + 32 + l32];
   bool bad = false;
   for (int mt = blockIdx.x * 4 + wv; mt < ntiles; mt += gridDim.x * 4) {
     const int n = mt / tiles_per_item, p0 = (mt - n * tiles_per_item) * 32;
     const size_t px = (size_t)min(p0 + l32, HW - 1);
-    const float* x0 = a.in0[g] + (size_t)n * a.in0_item + px * 64 + 8 * hf;
-    const float* x1 = a.in1[g] + (size_t)n * a.in1_item + px * 64 + 8 * hf;
-    f32x4 xv[C1X1_NC][2];
+    const float* x0 = a.in0[g] + (size_t)n * a.in0_item + px * C0;
+    const float* x1 = IN1 ? a.in1[g] + (size_t)n * a.in1_item + px * C1 : x0;
+    f32x4 xv[NC][2];
 #pragma unroll
-    for (int c = 0; c < C1X1_NC; ++c) {
-      const float* xp = (c < C1X1_NC / 2 ? x0 : x1) + 16 * (c % (C1X1_NC / 2));
+    for (int c = 0; c < NC; ++c) {
+      const int ch = 16 * (c < NC0 ? c : c - NC0);
+      const int cs = c < NC0 ? C0 : C1;
+      // a half-used last chunk (C % 16 == 8): lane half 1 re-reads half 0's channels (zero weights)
+      const float* xp = (c < NC0 ? x0 : x1) + ch + (ch + 8 < cs ? 8 * hf : 0);
       xv[c][0] = ld4(xp);
       xv[c][1] = ld4(xp + 4);
     }
     f32x16 acc0 = f32x16{0}, acc1 = f32x16{0};
 #pragma unroll
-    for (int c = 0; c < C1X1_NC; ++c) {
+    for (int c = 0; c < NC; ++c) {
       f16x8 ah, al;
       split_f16x3(xv[c][0], xv[c][1], ah, al);
       const float* wp = sw + c * 1024 + lane * 4;   // [chunk][nt][plane][lane][8 halves]
@@ -365,7 +372,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   report_range(a.status, bad);
 }
 
-int launch_conv1x1(const stif_conv_args& a, hipStream_t st) {
+template <int NC, int IN1>
+int launch_conv1x1(const stif_conv_args& a, hipStream_t st, int wg_per_cu) {
   const int tpi = (a.H * a.W + 31) / 32;
   static int cus = 0;
   if (!cus) {
@@ -374,10 +382,10 @@ int launch_conv1x1(const stif_conv_args& a, hipStream_t st) {
       cus = 256;
   }
   const long long wgs = ((long long)tpi * a.nitems + 3) / 4;
-  // four workgroups per CU over all (slice, group) grid planes, each walking several M-tiles
+  // wg_per_cu workgroups per CU over all (slice, group) grid planes, each walking several M-tiles
   const int per = a.ngroups * (a.cout / 64);
-  const int gx = (int)std::max<long long>(1, std::min<long long>(wgs, (4LL * cus + per - 1) / per));
-  hipLaunchKernelGGL(k_conv1x1, dim3(gx, a.cout / 64, a.ngroups), dim3(256), 0, st, a, tpi);
+  const int gx = (int)std::max<long long>(1, std::min<long long>(wgs, ((long long)wg_per_cu * cus + per - 1) / per));
+  hipLaunchKernelGGL((k_conv1x1<NC, IN1>), dim3(gx, a.cout / 64, a.ngroups), dim3(256), 0, st, a, tpi);
   return stif_check_launch("stif_conv2d_nhwc");
 }
 
@@ -448,11 +456,12 @@ extern "C" int stif_conv2d_nhwc(const stif_conv_args* pa, void* stream) {
   if (a.ngroups < 1 || a.ngroups > STIF_MAX_GROUPS || a.nitems < 1)
     return stif_fail(STIF_E_INVALID, "stif_conv2d_nhwc: bad ngroups/nitems");
   const bool f16 = a.flags & STIF_CONV_F16X3;
-  const bool f16_1x1 = a.ks == 1 && a.stride == 1 && a.in1_mode == 1 && a.C0 == 64 && a.C1 == 64 &&
-                       a.cout % 64 == 0 && a.epi == STIF_EPI_NONE;
+  const bool f16_cat = a.in1_mode == 1 && a.C0 == 64 && a.C1 == 64;   // (64 | 64) -> 64k
+  const bool f16_proj = a.in1_mode == 0 && a.C0 == 200;                 // the decoder's LR projection
+  const bool f16_1x1 = a.ks == 1 && a.stride == 1 && (f16_cat || f16_proj) && a.cout % 64 == 0 && a.epi == STIF_EPI_NONE;
   if (f16 && !(a.ks == 3 && a.stride == 2 && a.cout == 64 && a.C0 == 64 && a.in1_mode == 0) && !f16_1x1)
     return stif_fail(STIF_E_INVALID, "stif_conv2d_nhwc: STIF_CONV_F16X3 takes the 3x3 stride-2 64 -> 64 convs and "
-                                     "the 1x1 (64 | 64) -> 64k convs only");
+                                     "the 1x1 (64 | 64) -> 64k and 200 -> 64k convs only");
   if (a.C0 % 8 || a.C0 <= 0 || (a.in1_mode && (a.C1 % 8 || a.C1 <= 0)))
     return stif_fail(STIF_E_INVALID, "stif_conv2d_nhwc: channel counts must be multiples of 8");
   const int pad = a.ks / 2;
@@ -485,7 +494,7 @@ extern "C" int stif_conv2d_nhwc(const stif_conv_args* pa, void* stream) {
     return stif_fail(STIF_E_INVALID, "strided conv: unsupported epilogue");
   }
   if (a.ks == 1) {
-    if (f16) return launch_conv1x1(a, st);
+    if (f16) return f16_cat ? launch_conv1x1<8, 1>(a, st, 4) : launch_conv1x1<13, 0>(a, st, 3);
     if (a.epi != STIF_EPI_NONE) return stif_fail(STIF_E_INVALID, "1x1 conv: unsupported epilogue");
     if (a.in1_mode == 0) return launch<1, 1, 2, 2, 4, 0, STIF_EPI_NONE>(a, st);
     if (a.in1_mode == 1) return launch<1, 1, 2, 2, 4, 1, STIF_EPI_NONE>(a, st);

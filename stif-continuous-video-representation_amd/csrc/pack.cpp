@@ -98,8 +98,8 @@ std::vector<float> omega(const float* src, size_t n) {
 extern "C" size_t stif_conv_weight_floats(int cout, int cin, int ks, int mode) {
   // PLAIN | F16X3 (the DCN core, 64 -> 64 3x3): 5 tap pairs x 2 nt x 2 planes x 1 KB per 8-channel group
   if (mode == (STIF_PACK_PLAIN | STIF_PACK_F16X3) && ks == 3) return (size_t)(cin / 8) * 5 * 2 * 2 * 256;
-  // PLAIN | F16X3 1x1 (k_conv1x1): 2 nt x 2 planes x 1 KB per (64-cout slice, 16-channel chunk) = the
-  // plain size below
+  // PLAIN | F16X3 1x1 (k_conv1x1): 2 nt x 2 planes x 1 KB per (64-cout slice, 16-channel chunk)
+  if (mode == (STIF_PACK_PLAIN | STIF_PACK_F16X3) && ks == 1) return (size_t)(cout + 63) / 64 * ((cin + 15) / 16) * 1024;
   mode &= ~STIF_PACK_F16X3;   // Winograd: same bytes, two fp16 planes per fp32 value
   if (mode == STIF_PACK_WINO || mode == STIF_PACK_WINO_OFFMASK || mode == STIF_PACK_WINO_LSTM)
     return (size_t)round64(cout) * cin * 16;
@@ -224,12 +224,13 @@ int pack_wino_f16x3(const float* w, const float* b, int cout, int cin, int perm,
 }
 // PLAIN | F16X3, 1x1 (k_conv1x1): [slice][chunk c16][nt][plane][lane][8 halves]; element e of lane l
 // holds input channel 16 c16 + 8 (l >> 5) + e of cout slice * 64 + nt * 32 + (l & 31) -- lane half h
-// supplies its pixel's 8 consecutive channels 16 c16 + 8 h .. as the A operand -- as W * 2^10 split
+// supplies its pixel's 8 consecutive channels 16 c16 + 8 h .. as the A operand -- as W * 2^10 split;
+// a half-used last chunk (cin % 16 == 8) has zero weights in its upper half
 int pack_1x1_f16x3(const float* w, const float* b, int cout, int cin, float* w_dst, float* b_dst) {
-  if (cin % 16 || cout % 64) return stif_fail(STIF_E_INVALID, "PLAIN | F16X3 1x1 packing needs cin % 16 == 0, cout % 64 == 0");
+  if (cout % 64) return stif_fail(STIF_E_INVALID, "PLAIN | F16X3 1x1 packing needs cout % 64 == 0");
   for (size_t i = 0; i < (size_t)cout * cin; ++i)
     if (!f16x3_ok(w[i])) return range_fail("stif_pack_conv_weight: a weight is outside the f16x3 range (|w| < 64); pack it without STIF_PACK_F16X3");
-  const int NS = cout / 64, NC = cin / 16;
+  const int NS = cout / 64, NC = (cin + 15) / 16;
   _Float16* dst = reinterpret_cast<_Float16*>(w_dst);
   for (int s = 0; s < NS; ++s)
     for (int c = 0; c < NC; ++c)
@@ -238,7 +239,7 @@ int pack_1x1_f16x3(const float* w, const float* b, int cout, int cin, float* w_d
           for (int e = 0; e < 8; ++e) {
             const int co = s * 64 + nt * 32 + (l & 31), ci = 16 * c + 8 * (l >> 5) + e;
             const size_t o = (((((size_t)s * NC + c) * 2 + nt) * 2) * 64 + l) * 8 + e;
-            split_f16x3_host((double)w[(size_t)co * cin + ci], dst + o, dst + o + 512);
+            split_f16x3_host(ci < cin ? (double)w[(size_t)co * cin + ci] : 0.0, dst + o, dst + o + 512);
           }
   if (b_dst)
     for (int j = 0; j < cout; ++j) b_dst[j] = b ? b[j] : 0.f;
@@ -326,19 +327,20 @@ extern "C" int stif_pack_dec_proj_ex(const float* feat_w0, const float* feat_b0,
   for (int o = 0; o < 64; ++o) {
     for (int c = 0; c < 198; ++c) {
       W[(size_t)o * C + c] = feat_w0[(size_t)o * 201 + c];
-      if (c < 192 || lr_image) W[(size_t)(64 + o) * C + c] = flow_w0[(size_t)o * 263 + 64 + c];
+      if (c < 192 || (lr_image & 1)) W[(size_t)(64 + o) * C + c] = flow_w0[(size_t)o * 263 + 64 + c];
     }
     for (int c = 0; c < 192; ++c) {
       W[(size_t)(128 + o) * C + c] = enc_w0[(size_t)o * 525 + 128 + c];
       W[(size_t)(192 + o) * C + c] = enc_w0[(size_t)o * 525 + 320 + c];
     }
-    for (int c = 0; c < 6 && lr_image; ++c) {
+    for (int c = 0; c < 6 && (lr_image & 1); ++c) {
       W[(size_t)(128 + o) * C + 192 + c] = enc_w0[(size_t)o * 525 + 512 + c];
       W[(size_t)(192 + o) * C + 192 + c] = enc_w0[(size_t)o * 525 + 518 + c];
     }
     B[o] = feat_b0[o];
   }
-  return stif_pack_conv_weight(W.data(), B.data(), 256, C, 1, STIF_PACK_PLAIN, w_dst, b_dst);
+  return stif_pack_conv_weight(W.data(), B.data(), 256, C, 1, STIF_PACK_PLAIN | (lr_image & STIF_PACK_F16X3), w_dst,
+                               b_dst);
 }
 
 extern "C" size_t stif_dec_mlp_floats(void) { return stif_dec::MLP_FLOATS; }

@@ -253,14 +253,25 @@ class LunaTokis(nn.Module):
         """LR projection of the decoder's first layers (stif_pack_dec_proj_ex); lr_image=False leaves
         the LR frames out of P2..P4 for decoding_test, which samples the x4-upsampled frames."""
         h, dev, lib = self._host, self.device, L.lib()
-        wd = np.empty(lib.stif_dec_proj_floats(), np.float32)
-        bd = np.empty(lib.stif_conv_bias_floats(256, L.PACK_PLAIN), np.float32)
-        L.check(lib.stif_pack_dec_proj_ex(h["feat_imnet.net.0.linear.weight"].ctypes.data,
-                                          h["feat_imnet.net.0.linear.bias"].ctypes.data,
-                                          h["flow_imnet.net.0.linear.weight"].ctypes.data,
-                                          h["encode_imnet.net.0.linear.weight"].ctypes.data, int(lr_image),
-                                          wd.ctypes.data, bd.ctypes.data), "stif_pack_dec_proj_ex")
-        return ops.PackedConv(torch.from_numpy(wd).to(dev), torch.from_numpy(bd).to(dev), 256, 200, 1, L.PACK_PLAIN)
+
+        def pack(mode):
+            wd = np.empty(lib.stif_conv_weight_floats(256, 200, 1, mode), np.float32)
+            bd = np.empty(lib.stif_conv_bias_floats(256, L.PACK_PLAIN), np.float32)
+            L.check(lib.stif_pack_dec_proj_ex(h["feat_imnet.net.0.linear.weight"].ctypes.data,
+                                              h["feat_imnet.net.0.linear.bias"].ctypes.data,
+                                              h["flow_imnet.net.0.linear.weight"].ctypes.data,
+                                              h["encode_imnet.net.0.linear.weight"].ctypes.data,
+                                              int(lr_image) | (mode & L.PACK_F16X3), wd.ctypes.data, bd.ctypes.data),
+                    "stif_pack_dec_proj_ex")
+            return ops.PackedConv(torch.from_numpy(wd).to(dev), torch.from_numpy(bd).to(dev), 256, 200, 1, mode)
+
+        if self.mfma == "f16x3":   # k_conv1x1; a weight outside the split range -> fp32 packing
+            try:
+                return pack(L.PACK_PLAIN | L.PACK_F16X3)
+            except L.StifError as e:
+                if e.code != L.E_RANGE:
+                    raise
+        return pack(L.PACK_PLAIN)
 
     def _build_layers(self, pk, meta):
         bufs = pk._buffers

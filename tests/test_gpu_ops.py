@@ -112,12 +112,17 @@ def test_conv_f16x3_rejects_other_shapes(ops, L):
         ops.conv2d([dict(layer=lay, in0=x, out=torch.empty(1, 8, 8, 64, device="cuda"))])
 
 
-def test_conv1x1_wide(ops, L):
+@pytest.mark.parametrize("f16", [0, 1], ids=["f32", "f16x3"])
+def test_conv1x1_wide(ops, L, f16):
+    """The decoder's LR projection shape (200 -> 256): direct fp32 kernel, or k_conv1x1<13> whose last
+    16-channel chunk is half used."""
     x = rnd(2, 200, 9, 11, seed=17)
     w = rnd(256, 200, 1, 1, seed=18, scale=0.05)
     b = rnd(256, seed=19)
-    out = torch.empty(2, 9, 11, 256, device="cuda")
-    ops.conv2d([dict(layer=ops.pack_conv(w, b), in0=nhwc(x), out=out)])
+    out = torch.full((2, 9, 11, 256), float("nan"), device="cuda")
+    lay = ops.pack_conv(w, b, L.PACK_PLAIN | (L.PACK_F16X3 if f16 else 0))
+    assert bool(lay.mode & L.PACK_F16X3) == bool(f16)
+    ops.conv2d([dict(layer=lay, in0=nhwc(x), out=out)])
     assert relmax(to_nchw(out), O.conv2d(x, w, b)) < RTOL
 
 
