@@ -37,8 +37,8 @@ STIF_DEV f32x4 dcn_sample4(const float* __restrict__ img, int H, int W, float h,
   return w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4;
 }
 
-// Workgroup: DCN_ROWS waves, DCN_ROWS output rows x 32 px, all 64 output channels.  Per deformable group
-// (= 8 input channels = one K chunk): the group's input tile with an M-pixel margin around the
+// Workgroup: DCN_ROWS waves, MR output rows x 32 px per wave, all 64 output channels.  Per deformable
+// group (= 8 input channels = one K chunk): the group's input tile with an M-pixel margin around the
 // 3x3 footprint ([row][channel half][col][4], zero-filled outside the frame) and the group's
 // weight fragments are LDS-DMA'd one chunk ahead (double-buffered).  Each lane then bilinearly
 // samples its own MFMA A-fragment (pixel = lane & 31, channels 4h..4h+3) tap by tap from the
@@ -47,15 +47,21 @@ STIF_DEV f32x4 dcn_sample4(const float* __restrict__ img, int H, int W, float h,
 // F16: the contraction on split-fp16 MFMA (stif_common.h split_f16x3): two taps per 32x32x16 MFMA,
 // lane half h sampling tap 2p + h (tap 9 = 0) for all 8 channels of the group (elements 0..7), so
 // each (pixel, tap) computes its bilinear weights once; weights packed STIF_PACK_PLAIN |
-// STIF_PACK_F16X3 ([group][pair][nt][plane][lane][8 halves]).
+// STIF_PACK_F16X3 ([group][pair][nt][plane][lane][8 halves]).  On large maps each wave owns MR = 2
+// output rows (two M-tiles): every B fragment read from LDS feeds both rows' MFMAs, which halves the
+// weight traffic through LDS -- the kernel is bound by LDS bandwidth (bilinear corner reads at
+// data-dependent addresses conflict) -- and the 16-row tile stages 2.1x its pixels instead of 2.95x
+// (C0 L1 shape 342 -> 322 us); small maps keep MR = 1, where the halved grid would leave CUs idle.
 #ifndef DCN_TH
-#define DCN_TH 8   // 8 rows x 32 px per workgroup: halo staging 2.95x instead of 4.6x the pixels (C1 L1 438.7 -> 414.9 us, same-box A/B)
+#define DCN_TH 8   // 8 waves per workgroup (C1 L1 438.7 -> 414.9 us against 4, same-box A/B)
 #endif
-constexpr int DCN_ROWS = DCN_TH;   // output rows per workgroup = waves per workgroup
+constexpr int DCN_ROWS = DCN_TH;   // waves per workgroup
 
-template <int EPI, int F16>
+// MR: output rows per wave (2 only with F16; the launcher picks it by grid size, see stif_dcn_nhwc)
+template <int EPI, int F16, int MR = 1>
 __global__ __launch_bounds__(64 * DCN_ROWS) void k_dcn(stif_dcn_args a) {
-  constexpr int NW = DCN_ROWS, TH = DCN_ROWS, M = 4;
+  static_assert(MR == 1 || F16, "two rows per wave: split-fp16 path only");
+  constexpr int NW = DCN_ROWS, TH = NW * MR, M = 4;
   constexpr int TR = TH + 2 + 2 * M, TC = 32 + 2 + 2 * M;   // tile rows / cols
   constexpr int T_EL = TR * 2 * TC;                          // 16-B elements
   constexpr int T_INST = (T_EL + 63) / 64;
@@ -75,9 +81,16 @@ __global__ __launch_bounds__(64 * DCN_ROWS) void k_dcn(stif_dcn_args a) {
   const float* wt = a.w[g];
   const int oy0 = ty * TH, ox0 = tx * 32;
   const int ty0 = oy0 - 1 - M, tx0 = ox0 - 1 - M;           // tile origin (frame coords)
-  const int oy = oy0 + wv, ox = ox0 + l32;                   // this lane's output pixel
-  const bool pix_ok = oy < H && ox < W;
-  const float* omp = om + ((size_t)min(oy, H - 1) * W + min(ox, W - 1)) * OMC;
+  const int ox = ox0 + l32;                                  // this lane's output column
+  int oy[MR];
+  bool pix_ok[MR];
+  const float* omp[MR];
+#pragma unroll
+  for (int mr = 0; mr < MR; ++mr) {                          // this wave's output rows
+    oy[mr] = oy0 + wv * MR + mr;
+    pix_ok[mr] = oy[mr] < H && ox < W;
+    omp[mr] = om + ((size_t)min(oy[mr], H - 1) * W + min(ox, W - 1)) * OMC;
+  }
   const __amdgpu_buffer_rsrc_t rin =
       __builtin_amdgcn_make_buffer_rsrc((void*)in, (short)0, (int)((size_t)H * W * 64 * 4), 0x00020000);
 
@@ -99,19 +112,16 @@ __global__ __launch_bounds__(64 * DCN_ROWS) void k_dcn(stif_dcn_args a) {
   // offset/mask values of a group: all 27 (fp32 path), or (F16) the 5 taps 2p + h of this lane half
   // as [p][dy, dx, m] (tap 9 reads tap 8's values and is masked off)
   constexpr int NOM = F16 ? 15 : 27;
-  auto om_load = [&](int dgi, float* o) {
+  auto om_load = [&](int dgi, int mr, float* o) {
 #pragma unroll
-    for (int k = 0; k < NOM; ++k) {
-      if constexpr (F16) o[k] = omp[dgi * 27 + min(2 * (k / 3) + hf, 8) * 3 + k % 3];
-      else o[k] = omp[dgi * 27 + k];
-    }
+    for (int k = 0; k < NOM; ++k) o[k] = omp[mr][dgi * 27 + k];
   };
   // F16 variant: a group's 27 offset/mask floats (108 B, dword-aligned) as 6 x 16-B + 1 x 12-B loads
   // per lane instead of 15 scalar loads; lane half h picks its taps 2p + h at the group switch
   typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
   typedef float f32x3u __attribute__((ext_vector_type(3), aligned(4)));
-  auto om_raw = [&](int dgi, float* r) {
-    const float* p = omp + dgi * 27;
+  auto om_raw = [&](int dgi, int mr, float* r) {
+    const float* p = omp[mr] + dgi * 27;
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
       const f32x4u v = *reinterpret_cast<const f32x4u*>(p + 4 * i);
@@ -127,125 +137,123 @@ __global__ __launch_bounds__(64 * DCN_ROWS) void k_dcn(stif_dcn_args a) {
       o[k] = (k < 12 && hf) ? r[i0 + 3] : r[i0];
     }
   };
-  float omr[27];
-  float omc[NOM], omn[NOM];
-  if constexpr (F16) {
-    om_raw(0, omr);
-    om_pick(omr, omc);
-  } else {
-    om_load(0, omc);
+  float omr[MR][27];
+  float omc[MR][NOM], omn[MR][NOM];
+#pragma unroll
+  for (int mr = 0; mr < MR; ++mr) {
+    if constexpr (F16) {
+      om_raw(0, mr, omr[mr]);
+      om_pick(omr[mr], omc[mr]);
+    } else {
+      om_load(0, mr, omc[mr]);
+    }
   }
 
-  f32x16 acc0 = f32x16{0}, acc1 = f32x16{0};
+  // bilinear sample (dmcn_im2col_bilinear semantics) of 8 channels (F16: a0 = channels 0-3, a1 = 4-7)
+  // or of this lane half's 4 channels (fp32: a0) at tap `tap` of row mr, with the mask folded into
+  // the corner weights and the `> -1` / `< H` gate; global-load fallback outside the staged margin
+  auto sample = [&](const float* st, int dg, int mr, int tap, const float* oc, f32x4& a0, f32x4& a1) {
+    const int ky = tap / 3, kx = tap - 3 * ky;
+    const float h_im = (float)(oy[mr] - 1 + ky) + oc[0];
+    const float w_im = (float)(ox - 1 + kx) + oc[1];
+    const bool valid = pix_ok[mr] & (tap < 9) & (h_im > -1.f) & (w_im > -1.f) & (h_im < (float)H) & (w_im < (float)W);
+    const float fh = floorf(h_im), fw = floorf(w_im);
+    const float lh = h_im - fh, lw = w_im - fw, hh = 1.f - lh, hw = 1.f - lw;
+    const int h_low = (int)fh, w_low = (int)fw;
+    const int r0 = h_low - ty0, c0 = w_low - tx0;
+    const bool in_tile = ((unsigned)r0 < (unsigned)(TR - 1)) & ((unsigned)c0 < (unsigned)(TC - 1));
+    const float m = valid ? oc[2] : 0.f;
+    const float hm = hh * m, lm = lh * m;
+    const float w1 = hm * hw, w2 = hm * lw, w3 = lm * hw, w4 = lm * lw;
+    const int hsel = F16 ? 0 : hf;
+    const float* p0 = st + (((in_tile ? r0 : 0) * 2 + hsel) * TC + (in_tile ? c0 : 0)) * 4;
+    const float* p1 = p0 + 2 * TC * 4;                                                 // next row
+    a0 = w1 * ld4(p0) + w2 * ld4(p0 + 4) + w3 * ld4(p1) + w4 * ld4(p1 + 4);
+    if (F16) a1 = w1 * ld4(p0 + TC * 4) + w2 * ld4(p0 + TC * 4 + 4) + w3 * ld4(p1 + TC * 4) + w4 * ld4(p1 + TC * 4 + 4);
+    const bool fb = valid & !in_tile;
+    if (__builtin_amdgcn_ballot_w64(fb)) {
+      if (fb) {
+        const int h_high = h_low + 1, w_high = w_low + 1, co = dg * 8 + hsel * 4;
+        const bool b1 = h_low >= 0 && w_low >= 0, b2 = h_low >= 0 && w_high <= W - 1;
+        const bool b3 = h_high <= H - 1 && w_low >= 0, b4 = h_high <= H - 1 && w_high <= W - 1;
+        const float* q1 = in + ((size_t)h_low * W + w_low) * 64 + co;
+        const float* q2 = in + ((size_t)h_low * W + w_high) * 64 + co;
+        const float* q3 = in + ((size_t)h_high * W + w_low) * 64 + co;
+        const float* q4 = in + ((size_t)h_high * W + w_high) * 64 + co;
+        const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+        a0 = w1 * (b1 ? ld4(q1) : z) + w2 * (b2 ? ld4(q2) : z) + w3 * (b3 ? ld4(q3) : z) + w4 * (b4 ? ld4(q4) : z);
+        if (F16)
+          a1 = w1 * (b1 ? ld4(q1 + 4) : z) + w2 * (b2 ? ld4(q2 + 4) : z) + w3 * (b3 ? ld4(q3 + 4) : z) +
+               w4 * (b4 ? ld4(q4 + 4) : z);
+      }
+    }
+  };
+
+  f32x16 acc0[MR], acc1[MR];
+#pragma unroll
+  for (int mr = 0; mr < MR; ++mr) acc0[mr] = acc1[mr] = f32x16{0};
   stage(0, 0);
   lds_dma_barrier();
   for (int dg = 0; dg < 8; ++dg) {
     if (dg + 1 < 8) {
       stage(dg + 1, (dg + 1) & 1);
-      if constexpr (F16) om_raw(dg + 1, omr);
-      else om_load(dg + 1, omn);
+#pragma unroll
+      for (int mr = 0; mr < MR; ++mr) {
+        if constexpr (F16) om_raw(dg + 1, mr, omr[mr]);
+        else om_load(dg + 1, mr, omn[mr]);
+      }
     }
     const float* st = smem + (dg & 1) * BUF_F;
     const float* sw = st + T_F;
     if constexpr (F16) {
       // tap pair p: lane half h samples tap 2p + h for all 8 channels of the group -- one bilinear
-      // weight set per (pixel, tap) -- and supplies them as the 8 K values of its MFMA A operand
+      // weight set per (pixel, tap) -- and supplies them as the 8 K values of its MFMA A operand; the
+      // pair's B fragments (read once) feed both rows
 #pragma unroll
       for (int pp = 0; pp < 5; ++pp) {
-        const int tap = 2 * pp + hf;
-        const int ky = tap / 3, kx = tap - 3 * ky;
-        const float h_im = (float)(oy - 1 + ky) + omc[pp * 3];
-        const float w_im = (float)(ox - 1 + kx) + omc[pp * 3 + 1];
-        const bool valid =
-            pix_ok & (tap < 9) & (h_im > -1.f) & (w_im > -1.f) & (h_im < (float)H) & (w_im < (float)W);
-        const float fh = floorf(h_im), fw = floorf(w_im);
-        const float lh = h_im - fh, lw = w_im - fw, hh = 1.f - lh, hw = 1.f - lw;
-        const int h_low = (int)fh, w_low = (int)fw;
-        const int r0 = h_low - ty0, c0 = w_low - tx0;
-        const bool in_tile = ((unsigned)r0 < (unsigned)(TR - 1)) & ((unsigned)c0 < (unsigned)(TC - 1));
-        const float m = valid ? omc[pp * 3 + 2] : 0.f;
-        const float hm = hh * m, lm = lh * m;
-        const float w1 = hm * hw, w2 = hm * lw, w3 = lm * hw, w4 = lm * lw;
-        const float* p0 = st + (((in_tile ? r0 : 0) * 2) * TC + (in_tile ? c0 : 0)) * 4;   // channels 0-3
-        const float* p1 = p0 + 2 * TC * 4;                                                 // next row
-        f32x4 a0 = w1 * ld4(p0) + w2 * ld4(p0 + 4) + w3 * ld4(p1) + w4 * ld4(p1 + 4);
-        f32x4 a1 = w1 * ld4(p0 + TC * 4) + w2 * ld4(p0 + TC * 4 + 4) + w3 * ld4(p1 + TC * 4) + w4 * ld4(p1 + TC * 4 + 4);
-        const bool fb = valid & !in_tile;
-        if (__builtin_amdgcn_ballot_w64(fb)) {
-          if (fb) {
-            const int h_high = h_low + 1, w_high = w_low + 1, co = dg * 8;
-            const bool b1 = h_low >= 0 && w_low >= 0, b2 = h_low >= 0 && w_high <= W - 1;
-            const bool b3 = h_high <= H - 1 && w_low >= 0, b4 = h_high <= H - 1 && w_high <= W - 1;
-            const float* q1 = in + ((size_t)h_low * W + w_low) * 64 + co;
-            const float* q2 = in + ((size_t)h_low * W + w_high) * 64 + co;
-            const float* q3 = in + ((size_t)h_high * W + w_low) * 64 + co;
-            const float* q4 = in + ((size_t)h_high * W + w_high) * 64 + co;
-            const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
-            a0 = w1 * (b1 ? ld4(q1) : z) + w2 * (b2 ? ld4(q2) : z) + w3 * (b3 ? ld4(q3) : z) + w4 * (b4 ? ld4(q4) : z);
-            a1 = w1 * (b1 ? ld4(q1 + 4) : z) + w2 * (b2 ? ld4(q2 + 4) : z) + w3 * (b3 ? ld4(q3 + 4) : z) +
-                 w4 * (b4 ? ld4(q4 + 4) : z);
-          }
+        f16x8 ah[MR], al[MR];
+#pragma unroll
+        for (int mr = 0; mr < MR; ++mr) {
+          f32x4 a0, a1;
+          sample(st, dg, mr, 2 * pp + hf, omc[mr] + pp * 3, a0, a1);
+          split_f16x3(a0, a1, ah[mr], al[mr]);
         }
-        f16x8 ah, al;
-        split_f16x3(a0, a1, ah, al);
         const float* wp = sw + pp * 1024 + lane * 4;   // [pair][nt][plane][lane][8 halves]
         const f16x8 bh0 = ldh8(wp), bl0 = ldh8(wp + 256), bh1 = ldh8(wp + 512), bl1 = ldh8(wp + 768);
-        acc0 = mfma16h(ah, bh0, acc0);
-        acc1 = mfma16h(ah, bh1, acc1);
-        acc0 = mfma16h(ah, bl0, acc0);
-        acc1 = mfma16h(ah, bl1, acc1);
-        acc0 = mfma16h(al, bh0, acc0);
-        acc1 = mfma16h(al, bh1, acc1);
+#pragma unroll
+        for (int mr = 0; mr < MR; ++mr) {
+          acc0[mr] = mfma16h(ah[mr], bh0, acc0[mr]);
+          acc1[mr] = mfma16h(ah[mr], bh1, acc1[mr]);
+          acc0[mr] = mfma16h(ah[mr], bl0, acc0[mr]);
+          acc1[mr] = mfma16h(ah[mr], bl1, acc1[mr]);
+          acc0[mr] = mfma16h(al[mr], bh0, acc0[mr]);
+          acc1[mr] = mfma16h(al[mr], bh1, acc1[mr]);
+        }
       }
     } else {
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      // modulated_deformable_im2col (dcn_v2_im2col_cuda.cu:158-192) for this lane's pixel / tap.
-      // Common case without branches: the 2x2 footprint lies in the staged tile (zeros outside the
-      // frame = dmcn_im2col_bilinear's per-corner checks), the `> -1 / < H` gate and the mask are
-      // folded into the corner weights; a wave-uniform branch handles the rare lanes whose offset
-      // leaves the tile margin with global loads.
-      const float h_im = (float)(oy - 1 + tap / 3) + omc[tap * 3];
-      const float w_im = (float)(ox - 1 + tap % 3) + omc[tap * 3 + 1];
-      const bool valid = pix_ok & (h_im > -1.f) & (w_im > -1.f) & (h_im < (float)H) & (w_im < (float)W);
-      const float fh = floorf(h_im), fw = floorf(w_im);
-      const float lh = h_im - fh, lw = w_im - fw, hh = 1.f - lh, hw = 1.f - lw;
-      const int h_low = (int)fh, w_low = (int)fw;
-      const int r0 = h_low - ty0, c0 = w_low - tx0;
-      const bool in_tile = ((unsigned)r0 < (unsigned)(TR - 1)) & ((unsigned)c0 < (unsigned)(TC - 1));
-      const float m = valid ? omc[tap * 3 + 2] : 0.f;
-      const float hm = hh * m, lm = lh * m;
-      const float w1 = hm * hw, w2 = hm * lw, w3 = lm * hw, w4 = lm * lw;
-      const float* p0 = st + (((in_tile ? r0 : 0) * 2 + hf) * TC + (in_tile ? c0 : 0)) * 4;
-      const float* p1 = p0 + 2 * TC * 4;
-      f32x4 av = w1 * ld4(p0) + w2 * ld4(p0 + 4) + w3 * ld4(p1) + w4 * ld4(p1 + 4);
-      const bool fb = valid & !in_tile;
-      if (__builtin_amdgcn_ballot_w64(fb)) {
-        if (fb) {
-          const int h_high = h_low + 1, w_high = w_low + 1, co = dg * 8 + hf * 4;
-          const f32x4 v1 = (h_low >= 0 && w_low >= 0) ? ld4(in + ((size_t)h_low * W + w_low) * 64 + co) : f32x4{0};
-          const f32x4 v2 = (h_low >= 0 && w_high <= W - 1) ? ld4(in + ((size_t)h_low * W + w_high) * 64 + co) : f32x4{0};
-          const f32x4 v3 = (h_high <= H - 1 && w_low >= 0) ? ld4(in + ((size_t)h_high * W + w_low) * 64 + co) : f32x4{0};
-          const f32x4 v4 =
-              (h_high <= H - 1 && w_high <= W - 1) ? ld4(in + ((size_t)h_high * W + w_high) * 64 + co) : f32x4{0};
-          av = w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4;
+      for (int tap = 0; tap < 9; ++tap) {
+        // modulated_deformable_im2col (dcn_v2_im2col_cuda.cu:158-192) for this lane's pixel / tap
+        f32x4 av, unused;
+        sample(st, dg, 0, tap, omc[0] + tap * 3, av, unused);
+        const f32x4 b0 = ld4(sw + ((tap * 2 + 0) * 64 + lane) * 4);
+        const f32x4 b1 = ld4(sw + ((tap * 2 + 1) * 64 + lane) * 4);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          acc0[0] = mfma32(av[q], b0[q], acc0[0]);
+          acc1[0] = mfma32(av[q], b1[q], acc1[0]);
         }
       }
-      const f32x4 b0 = ld4(sw + ((tap * 2 + 0) * 64 + lane) * 4);
-      const f32x4 b1 = ld4(sw + ((tap * 2 + 1) * 64 + lane) * 4);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        acc0 = mfma32(av[q], b0[q], acc0);
-        acc1 = mfma32(av[q], b1[q], acc1);
-      }
-    }
     }
     if (dg + 1 < 8) {
-      if constexpr (F16) {
-        om_pick(omr, omc);
-      } else {
 #pragma unroll
-        for (int k = 0; k < NOM; ++k) omc[k] = omn[k];
+      for (int mr = 0; mr < MR; ++mr) {
+        if constexpr (F16) {
+          om_pick(omr[mr], omc[mr]);
+        } else {
+#pragma unroll
+          for (int k = 0; k < NOM; ++k) omc[mr][k] = omn[mr][k];
+        }
       }
     }
     lds_dma_barrier();
@@ -253,28 +261,31 @@ __global__ __launch_bounds__(64 * DCN_ROWS) void k_dcn(stif_dcn_args a) {
   // epilogue through a per-wave LDS block -> coalesced 16-B stores (see tile_to_lds)
   float* out = a.out[g] + (size_t)n * a.out_item;
   const float* bias = a.bias[g];
-  const int y = oy0 + wv;
   float* blk = smem + wv * 1024;
   const int rpx = lane >> 3, c4 = lane & 7;
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    const float bv = bias[nt * 32 + l32];
-    f32x16 v;
-    bool bad = false;
+  for (int mr = 0; mr < MR; ++mr) {
+    const int y = oy[mr];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      float t = (nt ? acc1[r] : acc0[r]) * (F16 ? F16X3_UNSCALE : 1.f) + bv;
-      if (F16) bad |= not_finite(t);
-      if (EPI == STIF_EPI_LRELU) t = lrelu01(t);
-      v[r] = t;
-    }
-    if (F16) report_range(a.status, bad);
-    tile_to_lds(blk, v, lane);
+    for (int nt = 0; nt < 2; ++nt) {
+      const float bv = bias[nt * 32 + l32];
+      f32x16 v;
+      bool bad = false;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int px = i * 8 + rpx, x = ox0 + px;
-      const f32x4 o = lds_row4(blk, px, c4);
-      if (y < H && x < W) st4(out + ((size_t)y * W + x) * 64 + nt * 32 + c4 * 4, o);
+      for (int r = 0; r < 16; ++r) {
+        float t = (nt ? acc1[mr][r] : acc0[mr][r]) * (F16 ? F16X3_UNSCALE : 1.f) + bv;
+        if (F16) bad |= not_finite(t);
+        if (EPI == STIF_EPI_LRELU) t = lrelu01(t);
+        v[r] = t;
+      }
+      if (F16) report_range(a.status, bad);
+      tile_to_lds(blk, v, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int px = i * 8 + rpx, x = ox0 + px;
+        const f32x4 o = lds_row4(blk, px, c4);
+        if (y < H && x < W) st4(out + ((size_t)y * W + x) * 64 + nt * 32 + c4 * 4, o);
+      }
     }
   }
 }
@@ -559,9 +570,17 @@ extern "C" int stif_dcn_nhwc(const stif_dcn_args* pa, void* stream) {
   const stif_dcn_args& a = *pa;
   if (a.ngroups < 1 || a.ngroups > STIF_MAX_GROUPS || a.nitems < 1 || a.H < 1 || a.W < 1)
     return stif_fail(STIF_E_INVALID, "stif_dcn_nhwc: bad sizes");
-  dim3 grid(((a.W + 31) / 32) * ((a.H + DCN_ROWS - 1) / DCN_ROWS), 1, a.ngroups * a.nitems);
   const bool f16 = a.flags & STIF_CONV_F16X3;
-  if (a.epi == STIF_EPI_LRELU && f16)
+  // two rows per wave when that still gives >= 4 workgroups per CU (1 fits per CU: 110 KB of LDS)
+  const long long wg2 = (long long)((a.W + 31) / 32) * ((a.H + 2 * DCN_ROWS - 1) / (2 * DCN_ROWS)) * a.ngroups * a.nitems;
+  const bool mr2 = f16 && wg2 >= 1024;
+  const int th = DCN_ROWS * (mr2 ? 2 : 1);   // output rows per workgroup
+  dim3 grid(((a.W + 31) / 32) * ((a.H + th - 1) / th), 1, a.ngroups * a.nitems);
+  if (a.epi == STIF_EPI_LRELU && mr2)
+    hipLaunchKernelGGL((k_dcn<STIF_EPI_LRELU, 1, 2>), grid, dim3(64 * DCN_ROWS), 0, (hipStream_t)stream, a);
+  else if (a.epi == STIF_EPI_NONE && mr2)
+    hipLaunchKernelGGL((k_dcn<STIF_EPI_NONE, 1, 2>), grid, dim3(64 * DCN_ROWS), 0, (hipStream_t)stream, a);
+  else if (a.epi == STIF_EPI_LRELU && f16)
     hipLaunchKernelGGL((k_dcn<STIF_EPI_LRELU, 1>), grid, dim3(64 * DCN_ROWS), 0, (hipStream_t)stream, a);
   else if (a.epi == STIF_EPI_NONE && f16)
     hipLaunchKernelGGL((k_dcn<STIF_EPI_NONE, 1>), grid, dim3(64 * DCN_ROWS), 0, (hipStream_t)stream, a);

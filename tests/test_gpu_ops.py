@@ -231,6 +231,28 @@ def test_dcn_fused(ops, L, epi, hw, oscale, f16):
     assert relmax(to_nchw(out), ref) < RTOL
 
 
+@pytest.mark.parametrize("oscale", [2.0, 7.0])
+def test_dcn_fused_two_rows_per_wave(ops, L, oscale):
+    """Launches of >= 1024 workgroups run k_dcn<., 1, 2> (two output rows per wave, 16-row tiles): 8
+    weight groups x 16 items of one 70x37 map and offset field (2 x 5 tiles each; rows past the map in
+    the last tile), every output against the oracle of item 0 -- all 128 are the same computation."""
+    H, W, G, N = 70, 37, 8, 16
+    x = rnd(1, 64, H, W, seed=34)
+    w = rnd(64, 64, 3, 3, seed=35, scale=0.05)
+    b = rnd(64, seed=36)
+    off, mask = _offsets(1, H, W, 37, oscale)
+    ref = O.lrelu(O.dcn_v2_forward(x, w, b, off, mask, 3, 3, 1, 1, 1, 1, 1, 1, 8))
+    o = off.reshape(1, 8, 9, 2, H, W).transpose(0, 4, 5, 1, 2, 3)
+    m = mask.reshape(1, 8, 9, H, W).transpose(0, 3, 4, 1, 2)
+    om = torch.from_numpy(np.ascontiguousarray(np.concatenate([o, m[..., None]], -1).reshape(1, H, W, 216))).cuda()
+    xs, oms = nhwc(x).repeat(N, 1, 1, 1), om.repeat(N, 1, 1, 1)
+    out = torch.full((G, N, H, W, 64), float("nan"), device="cuda")
+    lay = ops.pack_conv(w, b, L.PACK_PLAIN | L.PACK_F16X3)
+    ops.dcn([dict(layer=lay, inp=xs, offmask=oms, out=out[i]) for i in range(G)], epi=L.EPI_LRELU)
+    assert relmax(to_nchw(out[0, :1]), ref) < RTOL
+    assert bool((out == out[0, 0]).all())   # every group and item bit-identical to the checked one
+
+
 @pytest.mark.parametrize("cfg", [
     dict(B=2, C=64, Co=64, H=9, W=11, k=3, s=1, p=1, d=1, g=8),
     dict(B=1, C=16, Co=24, H=10, W=7, k=3, s=2, p=1, d=1, g=2),
