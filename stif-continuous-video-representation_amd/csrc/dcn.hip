@@ -63,7 +63,8 @@ __global__ __launch_bounds__(64 * DCN_ROWS) void k_dcn(stif_dcn_args a) {
   static_assert(MR == 1 || F16, "two rows per wave: split-fp16 path only");
   constexpr int NW = DCN_ROWS, TH = NW * MR, M = 4;
   constexpr int TR = TH + 2 + 2 * M, TC = 32 + 2 + 2 * M;   // tile rows / cols
-  constexpr int T_EL = TR * 2 * TC;                          // 16-B elements
+  constexpr int TP = TC;                                     // column pitch of the staged tile (16-B slots)
+  constexpr int T_EL = TR * 2 * TP;                          // 16-B elements
   constexpr int T_INST = (T_EL + 63) / 64;
   constexpr int T_F = T_INST * 256;
   constexpr int W_F = F16 ? 5 * 2 * 2 * 256 : 9 * 2 * 64 * 4;   // packed B fragments of one group
@@ -99,9 +100,9 @@ __global__ __launch_bounds__(64 * DCN_ROWS) void k_dcn(stif_dcn_args a) {
     float* sw = st + T_F;
     for (int i = wv; i < T_INST; i += NW) {
       const int e = i * 64 + lane;
-      const int col = e % TC, rh = e / TC, h = rh & 1, row = rh >> 1;
+      const int col = e % TP, rh = e / TP, h = rh & 1, row = rh >> 1;
       const int y = ty0 + row, x = tx0 + col;
-      const bool ok = e < T_EL && y >= 0 && y < H && x >= 0 && x < W;
+      const bool ok = e < T_EL && col < TC && y >= 0 && y < H && x >= 0 && x < W;
       const unsigned voff = ok ? (unsigned)((((size_t)y * W + x) * 64 + dg * 8 + h * 4) * 4) : 0x80000000u;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, st + i * 256, 16, voff, 0, 0, 0);
     }
@@ -166,10 +167,10 @@ __global__ __launch_bounds__(64 * DCN_ROWS) void k_dcn(stif_dcn_args a) {
     const float hm = hh * m, lm = lh * m;
     const float w1 = hm * hw, w2 = hm * lw, w3 = lm * hw, w4 = lm * lw;
     const int hsel = F16 ? 0 : hf;
-    const float* p0 = st + (((in_tile ? r0 : 0) * 2 + hsel) * TC + (in_tile ? c0 : 0)) * 4;
-    const float* p1 = p0 + 2 * TC * 4;                                                 // next row
+    const float* p0 = st + (((in_tile ? r0 : 0) * 2 + hsel) * TP + (in_tile ? c0 : 0)) * 4;
+    const float* p1 = p0 + 2 * TP * 4;                                                 // next row
     a0 = w1 * ld4(p0) + w2 * ld4(p0 + 4) + w3 * ld4(p1) + w4 * ld4(p1 + 4);
-    if (F16) a1 = w1 * ld4(p0 + TC * 4) + w2 * ld4(p0 + TC * 4 + 4) + w3 * ld4(p1 + TC * 4) + w4 * ld4(p1 + TC * 4 + 4);
+    if (F16) a1 = w1 * ld4(p0 + TP * 4) + w2 * ld4(p0 + TP * 4 + 4) + w3 * ld4(p1 + TP * 4) + w4 * ld4(p1 + TP * 4 + 4);
     const bool fb = valid & !in_tile;
     if (__builtin_amdgcn_ballot_w64(fb)) {
       if (fb) {
