@@ -455,6 +455,8 @@ extern "C" int stif_conv2d_nhwc(const stif_conv_args* pa, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (a.ngroups < 1 || a.ngroups > STIF_MAX_GROUPS || a.nitems < 1)
     return stif_fail(STIF_E_INVALID, "stif_conv2d_nhwc: bad ngroups/nitems");
+  if ((long long)a.H * a.W * std::max(a.C0, std::max(a.C1, a.cout)) * 4 >= 0x7fffffffLL)
+    return stif_fail(STIF_E_INVALID, "stif_conv2d_nhwc: item larger than 2 GB (buffer addressing)");
   const bool f16 = a.flags & STIF_CONV_F16X3;
   const bool f16_cat = a.in1_mode == 1 && a.C0 == 64 && a.C1 == 64;   // (64 | 64) -> 64k
   const bool f16_proj = a.in1_mode == 0 && a.C0 == 200;                 // the decoder's LR projection

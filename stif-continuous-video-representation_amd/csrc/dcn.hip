@@ -571,6 +571,8 @@ extern "C" int stif_dcn_nhwc(const stif_dcn_args* pa, void* stream) {
   const stif_dcn_args& a = *pa;
   if (a.ngroups < 1 || a.ngroups > STIF_MAX_GROUPS || a.nitems < 1 || a.H < 1 || a.W < 1)
     return stif_fail(STIF_E_INVALID, "stif_dcn_nhwc: bad sizes");
+  if ((long long)a.H * a.W * 64 * 4 >= 0x7fffffffLL)
+    return stif_fail(STIF_E_INVALID, "stif_dcn_nhwc: item larger than 2 GB (buffer addressing)");
   const bool f16 = a.flags & STIF_CONV_F16X3;
   // two rows per wave when that still gives >= 4 workgroups per CU (1 fits per CU: 110 KB of LDS)
   const long long wg2 = (long long)((a.W + 31) / 32) * ((a.H + 2 * DCN_ROWS - 1) / (2 * DCN_ROWS)) * a.ngroups * a.nitems;

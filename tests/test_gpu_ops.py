@@ -291,6 +291,29 @@ def test_dcn_zero_offset_kat_gpu(ops, golden):
     assert float((T(x) - 2 * out).abs().max()) < 1e-6
 
 
+def test_entry_points_reject_items_over_2gb(L):
+    """Items whose NHWC maps exceed the 32-bit buffer-descriptor range are refused before any launch
+    (the pointers are never dereferenced)."""
+    import ctypes as C
+    lib = L.lib()
+    H = W = 12000   # 144M px x 64 ch x 4 B > 2 GB
+    a = L.ConvArgs()
+    for f in ("in0", "in1", "w", "bias", "out", "res"):
+        getattr(a, f)[0] = 0x1000
+    a.ngroups = a.nitems = 1
+    a.H, a.W, a.C0, a.Ho, a.Wo, a.cout, a.ks, a.stride = H, W, 64, H, W, 64, 3, 1
+    for fn in (lib.stif_conv2d_nhwc, lib.stif_conv3x3_wino):
+        assert fn(C.byref(a), None) == L.E_INVALID
+        assert b"2 GB" in lib.stif_last_error()
+    d = L.DcnArgs()
+    for f in ("inp", "offmask", "w", "bias", "out"):
+        getattr(d, f)[0] = 0x1000
+    d.ngroups = d.nitems = 1
+    d.H, d.W = H, W
+    assert lib.stif_dcn_nhwc(C.byref(d), None) == L.E_INVALID
+    assert b"2 GB" in lib.stif_last_error()
+
+
 def test_dcn_dropin_rejects_bad_args(ops):
     x = torch.zeros(1, 4, 5, 5, device="cuda")
     with pytest.raises(RuntimeError, match="kernel channels"):
