@@ -77,6 +77,15 @@ STIF_DEV void stage_image(__amdgpu_buffer_rsrc_t rs, float* dst, int iy0, int ix
   }
 }
 
+// IN1 = 2 (the PCD cat(x, s * up2(c)) convs): the second input is the coarse map c [H/2][W/2][C1]; its
+// phases stage the 4 x 18 coarse pixels under a tile's 6 x 34 halo (coarse rows oy0/2 - 1 .. +2,
+// columns ox0/2 - 1 .. +16) into a scratch area by LDS-DMA, and between phases the workgroup expands
+// them into the phase image with F.interpolate(scale_factor=2, bilinear, align_corners=False)
+// arithmetic (k_up2's expression) times s -- the upsampled map is never written to HBM.
+constexpr int UP_R = 4, UP_C = 18;                    // coarse rows / columns per tile
+constexpr int SCR_F = UP_R * UP_C * 2 * PSUB * 4;      // scratch floats: [row][col][chunk][4]
+constexpr int SCR_INS = (UP_R * UP_C * 2 * PSUB + 63) / 64;
+
 struct Tile {
   int oy0, ox0, slice, g, n;
   const float* src0;   // the item's input maps (k_wino: in0 and in1 of group g, item n), loaded from the
@@ -90,7 +99,8 @@ struct Tile {
 // Wave i = transform row i for both 32-cout halves (2 waves per SIMD, ~250 VGPRs).
 template <int IN1, int EPI, int F16>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_wino(stif_conv_args a, int ntiles) {
-  __shared__ __attribute__((aligned(16))) float smem[2 * BUF_F];
+  __shared__ __attribute__((aligned(16))) float smem[2 * BUF_F + (IN1 == 2 ? SCR_F : 0)];
+  float* const scr = smem + 2 * BUF_F;                       // IN1 = 2: coarse patch of the next phase
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wi = __builtin_amdgcn_readfirstlane(tid >> 6);   // transform row i of this wave
@@ -134,16 +144,58 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 
   // staging image (stage_image): DMA instruction (r, m) = wave wi's ins = wi, wi + 4, ... of 30
   const int lpx = lane / 9, lck = lane - 9 * (lane / 9);
+  const int h1 = H >> 1, w1 = W >> 1;   // IN1 = 2: the coarse map's size
   auto stage = [&](const Tile& t, int p, int buf) {
     // a phase lies entirely in one input (NC0 % PSUB == 0, host-checked)
     const bool second = IN1 && p * PSUB >= NC0;
     const float* src = second ? t.src1 : t.src0;
     const int Cs = second ? C1 : C0;
     const int cbase = (second ? p * PSUB - NC0 : p * PSUB) * 8;
+    if (IN1 == 2 && second) {
+      // coarse patch [row 4][col 18][chunk 8] (lane-linear, out-of-map pixels zero: never weighted)
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, (int)((size_t)h1 * w1 * Cs * 4), 0x00020000);
+      const int cy0 = (t.oy0 >> 1) - 1, cx0 = (t.ox0 >> 1) - 1;
+      for (int ins = wi; ins < SCR_INS; ins += 4) {
+        const int e = ins * 64 + lane, ch = e & 7, pc = e >> 3;
+        const int y = cy0 + pc / UP_C, x = cx0 + pc % UP_C;
+        const bool ok = (e < UP_R * UP_C * 8) & ((unsigned)y < (unsigned)h1) & ((unsigned)x < (unsigned)w1);
+        const unsigned voff = ok ? (unsigned)(((y * w1 + x) * Cs + cbase + ch * 4) * 4) : 0x80000000u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, scr + ins * 256, 16, voff, 0, 0, 0);
+      }
+      return;
+    }
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, (int)((size_t)H * W * Cs * 4), 0x00020000);
     stage_image(rs, smem + buf * BUF_F, t.oy0 - 1, t.ox0 - 1, H, W, Cs, cbase, wi, 4, lpx, lck);
   };
+  // IN1 = 2: the staged coarse patch -> the phase image of the tile's 6 x 34 halo (zero outside the map)
+  auto expand = [&](const Tile& t, int buf) {
+    float* dst = smem + buf * BUF_F;
+    const int cy0 = (t.oy0 >> 1) - 1, cx0 = (t.ox0 >> 1) - 1;
+    const float sc = a.in1_scale;
+    for (int f = tid; f < HR * HC * 8; f += 256) {
+      const int ch = f & 7, pc = f >> 3, r = pc / HC, c = pc - HC * (pc / HC);
+      const int Y = t.oy0 - 1 + r, X = t.ox0 - 1 + c;
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (((unsigned)Y < (unsigned)H) & ((unsigned)X < (unsigned)W)) {
+        // k_up2 (resample.hip): align_corners=False source coordinates, clamped at 0
+        const float sy = fmaxf(0.5f * ((float)Y + 0.5f) - 0.5f, 0.f);
+        const float sx = fmaxf(0.5f * ((float)X + 0.5f) - 0.5f, 0.f);
+        const int y0 = min((int)sy, h1 - 1), x0 = min((int)sx, w1 - 1);
+        const int y1 = y0 + (y0 < h1 - 1 ? 1 : 0), x1 = x0 + (x0 < w1 - 1 ? 1 : 0);
+        const float ly1 = sy - (float)y0, lx1 = sx - (float)x0;
+        const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
+        const float* s0 = scr + ((y0 - cy0) * UP_C) * 32 + ch * 4;
+        const float* s1 = scr + ((y1 - cy0) * UP_C) * 32 + ch * 4;
+        const f32x4 v00 = ld4(s0 + (x0 - cx0) * 32), v01 = ld4(s0 + (x1 - cx0) * 32);
+        const f32x4 v10 = ld4(s1 + (x0 - cx0) * 32), v11 = ld4(s1 + (x1 - cx0) * 32);
+        v = (ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11)) * sc;
+      }
+      st4(dst + (r * OM_RP + col_slot(c) * PITCH + ch) * 4, v);
+    }
+  };
+  auto up_phase = [&](int p) { return IN1 == 2 && p * PSUB >= NC0; };
 
   // rows of the 4x4 patch feeding transform row i: (B^T d)_i = d[rA] + sB * d[rB]
   const int rA = (wi == 0) ? 0 : (wi == 2 ? 2 : 1);
@@ -264,6 +316,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         // them -- has landed
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         __syncthreads();
+        if (IN1 == 2 && p + 1 < NP && up_phase(p + 1)) {
+          expand(cur, (gp + 1) & 1);
+          __syncthreads();
+        }
       }
     } else
     for (int p = 0; p < NP; ++p, ++gp) {
@@ -298,6 +354,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       // them -- has landed; those 8 stay in flight across the barrier
       asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       __syncthreads();
+      if (IN1 == 2 && p + 1 < NP && up_phase(p + 1)) {
+        expand(cur, (gp + 1) & 1);
+        __syncthreads();
+      }
     }
 
     // ---- output transform, balanced over all waves.  Wave i holds P_i[b] = sum_j M[i][j] A[j][b]
@@ -677,8 +737,10 @@ extern "C" int stif_conv3x3_wino(const stif_conv_args* pa, void* stream) {
     return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: bad ngroups/nitems");
   if (a.ks != 3 || a.stride != 1 || a.Ho != a.H || a.Wo != a.W)
     return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: 3x3 stride-1 'same' convolution only");
-  if (a.C0 % 8 || a.C0 <= 0 || (a.in1_mode == 1 && (a.C1 % 8 || a.C1 <= 0)))
+  if (a.C0 % 8 || a.C0 <= 0 || (a.in1_mode && (a.C1 % 8 || a.C1 <= 0)))
     return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: channel counts must be multiples of 8");
+  if (a.in1_mode == 2 && (a.H % 2 || a.W % 2))
+    return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: x2 upsampled second input needs even H, W");
   if (a.epi == STIF_EPI_LSTM && (a.cout != 256 || a.in1_mode != 1 || !a.res[0] || !a.out2[0]))
     return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: LSTM conv must be 128->256 with res = c_cur, out2 = c_next");
   if (a.cout % 64 && a.epi != STIF_EPI_OFFMASK)
@@ -700,6 +762,10 @@ extern "C" int stif_conv3x3_wino(const stif_conv_args* pa, void* stream) {
   if (a.in1_mode == 1 && a.epi == STIF_EPI_LSTM) return launch<1, STIF_EPI_LSTM>(a, st);
   if (a.in1_mode == 0) { STIF_WINO_CASE(0) }
   else if (a.in1_mode == 1) { STIF_WINO_CASE(1) }
+  else if (a.in1_mode == 2) {   // the cat(., s * up2(.)) convs: NONE / LRELU
+    if (a.epi == STIF_EPI_NONE) return launch<2, STIF_EPI_NONE>(a, st);
+    if (a.epi == STIF_EPI_LRELU) return launch<2, STIF_EPI_LRELU>(a, st);
+  }
 #undef STIF_WINO_CASE
   return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: unsupported in1 mode / epilogue");
 }

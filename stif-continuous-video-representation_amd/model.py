@@ -409,15 +409,10 @@ class LunaTokis(nn.Module):
         E = enumerate
 
         def conv_up(make, coarse, scale, epi):
-            """conv on cat(x, scale * up2(coarse)) for every unit: fused x2 upsample in the direct
-            kernel, or a materialised upsample + the Winograd kernel"""
-            if not self.winograd:
-                conv([make(i, u, coarse[i]) for i, u in E(units)], epi=epi, in1_mode=2, in1_scale=scale)
-                return
-            g_, n_, h_, w_, c_ = coarse.shape
-            up = self._empty(g_, n_, 2 * h_, 2 * w_, c_)
-            ops.upsample2x(coarse.view(g_ * n_, h_, w_, c_), up.view(g_ * n_, 2 * h_, 2 * w_, c_), scale)
-            conv([make(i, u, up[i]) for i, u in E(units)], epi=epi, in1_mode=1)
+            """conv on cat(x, scale * up2(coarse)) for every unit, the x2 upsample fused into the
+            conv's staging (Winograd: expanded from an LDS-staged coarse patch per tile; direct
+            kernel: register-staged) -- the upsampled map never reaches HBM"""
+            conv([make(i, u, coarse[i]) for i, u in E(units)], epi=epi, in1_mode=2, in1_scale=scale)
         # ---- L3
         o = buf(2)
         conv([dict(layer=L_(u, "L3_offset_conv1"), in0=u[2][2], in1=u[3][2], out=o[i]) for i, u in E(units)],

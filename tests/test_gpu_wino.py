@@ -166,6 +166,32 @@ def test_wino_cat_upsampled_matches_fused_direct(stif, pf):
     assert relmax(to_nchw(o1), ref) < RTOL and relmax(to_nchw(o2), ref) < RTOL
 
 
+@pytest.mark.parametrize("epi", ["none", "lrelu"])
+@pytest.mark.parametrize("hw", [(12, 36), (4, 4), (2, 66), (34, 70), (64, 64)])
+def test_wino_fused_upsample(stif, epi, hw, pf):
+    """cat(x, s * up2(c)) conv with the x2 upsample fused into the Winograd staging (in1_mode 2: coarse
+    patch LDS-staged per tile and expanded between phases): two groups over strided coarse items,
+    maps with partial tiles in both directions and 1-coarse-row/column borders, against the oracle."""
+    L, ops = stif._lib, stif.ops
+    H, W = hw
+    x0 = rnd(4, 64, H, W, seed=60)
+    c = rnd(4, 64, H // 2, W // 2, seed=61)
+    wa, wb = rnd(64, 128, 3, 3, seed=62, scale=0.04), rnd(64, 128, 3, 3, seed=63, scale=0.04)
+    ba, bb = rnd(64, seed=64), rnd(64, seed=65)
+    e = L.EPI_LRELU if epi == "lrelu" else L.EPI_NONE
+    act = O.lrelu if epi == "lrelu" else (lambda v: v)
+    xt, ct = nhwc(x0), nhwc(c)
+    out = torch.full((2, 2, H, W, 64), float("nan"), device="cuda")
+    for scale in (2.0, 1.0):
+        ops.conv2d([dict(layer=ops.pack_conv(wa, ba, L.PACK_WINO | pf), in0=xt[0::2], in1=ct[1::2], out=out[0]),
+                    dict(layer=ops.pack_conv(wb, bb, L.PACK_WINO | pf), in0=xt[1::2], in1=ct[0::2], out=out[1])],
+                   epi=e, in1_mode=2, in1_scale=scale)
+        up = O.upsample2x(c.astype(np.float64)) * scale
+        refa = act(O.conv2d(np.concatenate([x0[0::2], up[1::2]], 1), wa, ba))
+        refb = act(O.conv2d(np.concatenate([x0[1::2], up[0::2]], 1), wb, bb))
+        assert relmax(to_nchw(out[0]), refa) < RTOL and relmax(to_nchw(out[1]), refb) < RTOL
+
+
 def test_wino_offmask_matches_direct(stif, pf):
     """64 -> 216 offset/mask conv (permuted [group][tap][dy,dx,sigmoid(m)] rows, 4 cout slices with
     the last one partial) on the Winograd kernel == the direct kernel, and == the oracle."""
