@@ -466,23 +466,28 @@ class LunaTokis(nn.Module):
         hs = self._empty(2, 3, B, H, Wd, 64)            # h of (direction, step)
         cs = torch.zeros(2, B, H, Wd, 64, device=self.device)
         zero = torch.zeros(B, H, Wd, 64, device=self.device)
+        # Easy_PCD pyramids (:148-160) of the inputs, once per (pcd, input): the forward direction reads
+        # X[t] and the reversed one X[2 - t] with the same weights, so per-step pyramids of the inputs
+        # would compute each of them twice (bit-identical results, half the work)
+        X3 = X.view(3 * B, H, Wd, 64)
+        xp2, xp3 = self._pyramid([(X3, pcds[0]), (X3, pcds[1])])   # [pcd][3B, ...]
+
+        def xpyr(p, level, fr):
+            return (xp2 if level == 2 else xp3)[p, fr * B:(fr + 1) * B]
+
         for t in range(3):
-            xin = [X[t], X[2 - t]]                       # forward / reversed sequence
+            fr = [t, 2 - t]                               # forward / reversed sequence
+            xin = [X[f] for f in fr]
             state = [[zero if t == 0 else hs[d, t - 1] for d in range(2)], [cs[d] for d in range(2)]]
-            # Easy_PCD pyramids (:148-160): groups (pcd, dir, which in {x, state})
-            srcs = []
-            for p in range(2):
-                for d in range(2):
-                    srcs.append((xin[d], pcds[p]))
-                    srcs.append((state[p][d], pcds[p]))
-            py2, py3 = self._pyramid(srcs)
+            # pyramids of the recurrent states: groups (pcd, dir)
+            py2, py3 = self._pyramid([(state[p][d], pcds[p]) for p in range(2) for d in range(2)])
             Y = self._empty(2, 2, 2, B, H, Wd, 64)       # (pcd, dir, align direction)
             units = []
             for p in range(2):
                 for d in range(2):
-                    gi = (p * 2 + d) * 2
-                    f1 = [xin[d], py2[gi], py3[gi]]
-                    f2 = [state[p][d], py2[gi + 1], py3[gi + 1]]
+                    gi = p * 2 + d
+                    f1 = [xin[d], xpyr(p, 2, fr[d]), xpyr(p, 3, fr[d])]
+                    f2 = [state[p][d], py2[gi], py3[gi]]
                     units.append((pcds[p] + "pcd_align.", 1, f1, f2, Y[p, d, 0]))
                     units.append((pcds[p] + "pcd_align.", 2, f2, f1, Y[p, d, 1]))
             self._pcd_align(units)
