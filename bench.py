@@ -262,7 +262,7 @@ def run_config(stif, sd, cfg, args, world, rank, device, dist, mfma, trace_dom=T
     a, b = shards[rank]
     total_pairs = total_frames - 1
     HH, WW = int(round(H * scale)), int(round(W * scale))
-    model = stif.LunaTokis(64, 6, 8, 5, 40, device=device, mfma=mfma)
+    model = stif.LunaTokis(64, 6, 8, 5, 40, device=device, mfma=mfma, lanes=args.lanes)
     model.load_state_dict(sd, strict=True)
     frames = synth_frames(a, b - a, H, W, device) if b > a else None
     tq = [torch.tensor([[t]], device=device) for t in times]
@@ -314,6 +314,8 @@ def main():
     ap.add_argument("--mfma", default="f16x3", choices=["f32", "f16x3"],
                     help="operand mode of the contractions (model.LunaTokis mfma=)")
     ap.add_argument("--kernel-report", action="store_true", help="time every launch kind (stderr)")
+    ap.add_argument("--lanes", type=int, default=1,
+                    help="concurrent HIP streams per rank, each a contiguous range of the pairs (LunaTokis lanes)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

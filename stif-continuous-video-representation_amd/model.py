@@ -37,6 +37,15 @@ def _np(v):
     return v.detach().cpu().numpy().astype(np.float32, copy=False)
 
 
+def _drain(gen):
+    """Run a stage generator (see LunaTokis._run_lanes) to completion; returns its return value."""
+    while True:
+        try:
+            next(gen)
+        except StopIteration as e:
+            return e.value
+
+
 class _Container(nn.Module):
     """A plain node of the reference's module tree (holds the reference parameters by their key)."""
 
@@ -52,7 +61,7 @@ class LunaTokis(nn.Module):
     the module), never the parameters themselves."""
 
     def __init__(self, nf=64, nframes=3, groups=8, front_RBs=5, back_RBs=10, device="cuda", winograd=True,
-                 mfma="f16x3", range_check="rerun", chunk_px=2 ** 21):
+                 mfma="f16x3", range_check="rerun", chunk_px=2 ** 21, lanes=1):
         super().__init__()
         if nf != 64 or groups != 8:
             raise ValueError("the gfx950 kernels implement nf=64, groups=8 (the shipped STIF configuration)")
@@ -98,6 +107,14 @@ class LunaTokis(nn.Module):
         # pairs per encoder pass: a window is processed in chunks of about chunk_px LR pixels, which
         # bounds the PCD / BiConvLSTM working set (~20 KB per pair-pixel) at large frames
         self.chunk_px = int(chunk_px)
+        # independent pair ranges run as `lanes` concurrent HIP streams (_run_lanes), so one lane's kernels
+        # could fill the others' tail waves and dispatch gaps; results do not depend on it.  Default 1:
+        # at C0, 2 lanes measured 5 % slower (82.5 -> 76.7, 84.6 -> 80.4 Mpix/s, same box) -- the
+        # persistent, XCD-mapped kernels lose more to sharing the CUs than the gaps cost
+        if int(lanes) < 1:
+            raise ValueError("lanes must be >= 1")
+        self.lanes = int(lanes)
+        self._lane_streams = {}
         self._active = False
 
     # ------------------------------------------------------------------ nn.Module API
@@ -354,14 +371,58 @@ class LunaTokis(nn.Module):
 
     def _frame_features(self, frames):
         """conv_first + feature_extraction + pyramid (:318-325) for frames [n,3,H,W] (NCHW)."""
+        return _drain(self._frame_features_steps(frames))
+
+    def _frame_features_steps(self, frames):
         n, _, H, Wd = frames.shape
         l1 = self._empty(n, H, Wd, 64)
         ops.conv_first(frames, self.layers["conv_first"].w, self.layers["conv_first"].b, l1)
         tmp = self._empty(n, H, Wd, 64)
         for i in range(self.front_RBs):
             self._resblock(l1, tmp, f"feature_extraction.{i}")
+            yield
         l2, l3 = self._pyramid([(l1, "")])
         return l1, l2[0], l3[0]
+
+    # ------------------------------------------------------------------ lanes
+    def _streams(self, k):
+        dev = self.device
+        ss = self._lane_streams.setdefault(str(dev), [])
+        while len(ss) < k:
+            ss.append(torch.cuda.Stream(device=dev))
+        return ss[:k]
+
+    def _run_lanes(self, n, make):
+        """Items [0, n) in up to ``self.lanes`` contiguous ranges; ``make(c0, c1)`` is a generator
+        issuing one range's launches (each ``yield`` a point where another lane may issue).  Each
+        range runs on its own stream, forked from and joined back into the current one, and the
+        generators advance round-robin, so every stream has queued work from the start and the
+        kernels of one lane fill the last waves and the dispatch gaps of the others.  Every kernel
+        computes each item independently of the batch it is launched in, so the results are
+        bit-identical for any lane count."""
+        k = max(1, min(self.lanes, n))
+        per = -(-n // k)
+        ranges = [(c0, min(n, c0 + per)) for c0 in range(0, n, per)]
+        if len(ranges) == 1:
+            _drain(make(0, n))
+            return
+        main = torch.cuda.current_stream()
+        streams = self._streams(len(ranges))
+        for s in streams:
+            s.wait_stream(main)
+        live = [(s, make(c0, c1)) for s, (c0, c1) in zip(streams, ranges)]
+        while live:
+            nxt = []
+            for s, g in live:
+                with torch.cuda.stream(s):
+                    try:
+                        next(g)
+                        nxt.append((s, g))
+                    except StopIteration:
+                        pass
+            live = nxt
+        for s in streams:
+            main.wait_stream(s)
 
     def _resblock(self, x, tmp, name):
         """ResidualBlock_noBN (module_util.py:48-52), x updated in place."""
@@ -457,6 +518,9 @@ class LunaTokis(nn.Module):
                 l2fea, 1.0, L.EPI_NONE)
 
     def _bilstm(self, X):
+        return _drain(self._bilstm_steps(X))
+
+    def _bilstm_steps(self, X):
         """BiDeformableConvLSTM.forward (:256-266) with DeformableConvLSTM.forward (:192-242) for
         both directions batched.  X: [3, B, H, W, 64] latent inputs (t-major).  Returns [3,B,H,W,64]."""
         _, B, H, Wd, _ = X.shape
@@ -497,13 +561,15 @@ class LunaTokis(nn.Module):
             # ConvLSTMCell (convlstm.py:42-58): combined = cat(x, h~); c_next = f*c~ + i*g
             self._conv([dict(layer=lay[pf + "cell_list.0.conv"], in0=xin[d], in1=T[0, d], res=T[1, d],
                              out=hs[d, t], out2=cs[d]) for d in range(2)], epi=L.EPI_LSTM, in1_mode=1)
+            yield
         feats = self._empty(3, B, H, Wd, 64)
         self._conv([dict(layer=lay["ConvBLSTM.conv_1x1"], in0=hs[0, t], in1=hs[1, 2 - t], out=feats[t])
                     for t in range(3)], in1_mode=1)
         return feats
 
-    def _gen_feat_core(self, fea1, fea2, out=None):
-        """Everything after the per-frame features: PCD + fusion, BiConvLSTM, recon trunk.
+    def _gen_feat_core(self, fea1, fea2, out):
+        """Everything after the per-frame features: PCD + fusion, BiConvLSTM, recon trunk, into
+        out [3, B, H, W, 64] (generator: yields between stages, see _run_lanes).
         fea1 / fea2: [L1, L2, L3] of the pairs' first / second frames (item = pair)."""
         B, H, Wd, _ = fea1[0].shape
         X = self._empty(3, B, H, Wd, 64)
@@ -513,32 +579,27 @@ class LunaTokis(nn.Module):
         self._pcd_align([("pcd_align.", 1, fea1, fea2, Y[0]), ("pcd_align.", 2, fea2, fea1, Y[1])])
         self._conv([dict(layer=self.layers["fusion"], in0=Y[0], in1=Y[1], out=X[1])], in1_mode=1)
         del Y
-        feats = self._bilstm(X)
+        yield
+        feats = yield from self._bilstm_steps(X)
         del X
         trunk = feats.view(3 * B, H, Wd, 64)
         tmp = self._empty(3 * B, H, Wd, 64)
         for i in range(self.back_RBs):
             self._resblock(trunk, tmp, f"recon_trunk.{i}")
-        if out is not None:
-            out.copy_(feats)
-            return out
-        return feats
+            yield
+        out.copy_(feats)
 
-    def _gen_feat_pairs(self, fea1, fea2):
+    def _gen_feat_pairs(self, fea1, fea2, out):
         """_gen_feat_core over chunks of about ``chunk_px`` LR pixels of pairs (balanced), so the
         working set stays bounded at large frames; pairs are independent, so chunking does not
-        change a bit of the result."""
+        change a bit of the result (generator)."""
         B, H, Wd, _ = fea1[0].shape
         per = max(1, self.chunk_px // (H * Wd))
-        if B <= per:
-            return self._gen_feat_core(fea1, fea2)
         nch = math.ceil(B / per)
         per = math.ceil(B / nch)
-        out = self._empty(3, B, H, Wd, 64)
         for c0 in range(0, B, per):
             c1 = min(B, c0 + per)
-            self._gen_feat_core([t[c0:c1] for t in fea1], [t[c0:c1] for t in fea2], out[:, c0:c1])
-        return out
+            yield from self._gen_feat_core([t[c0:c1] for t in fea1], [t[c0:c1] for t in fea2], out[:, c0:c1])
 
     # ------------------------------------------------------------------ reference API
     def _check_input(self, x):
@@ -557,10 +618,15 @@ class LunaTokis(nn.Module):
         x = self._check_input(x)
         self.inp = x
         B, N, C, H, Wd = x.shape
-        l1, l2, l3 = self._frame_features(x.view(B * N, C, H, Wd))
-        fea1 = [l1[0::2], l2[0::2], l3[0::2]]
-        fea2 = [l1[1::2], l2[1::2], l3[1::2]]
-        self._feat = self._gen_feat_pairs(fea1, fea2)
+        out = self._empty(3, B, H, Wd, 64)
+
+        def lane(c0, c1):
+            l1, l2, l3 = yield from self._frame_features_steps(x[c0:c1].reshape((c1 - c0) * N, C, H, Wd))
+            fea1 = [l1[0::2], l2[0::2], l3[0::2]]
+            fea2 = [l1[1::2], l2[1::2], l3[1::2]]
+            yield from self._gen_feat_pairs(fea1, fea2, out[:, c0:c1])
+        self._run_lanes(B, lane)
+        self._feat = out
         return None
 
     def frame_features(self, frames):
@@ -581,17 +647,30 @@ class LunaTokis(nn.Module):
         x = torch.stack([frames[:-1], frames[1:]], dim=1).contiguous()
         self.inp = self._check_input(x)
         F_ = frames.shape[0]
+        _, _, H, Wd = frames.shape
+        out = self._empty(3, F_ - 1, H, Wd, 64)
+        if frame_feats is None and last_frame_feats is None:
+            # lanes of pairs [c0, c1) each run the encoder on their frames c0..c1 (the frame two lanes
+            # share is encoded by both, so no lane waits for another)
+            def lane(c0, c1):
+                l1, l2, l3 = yield from self._frame_features_steps(frames[c0:c1 + 1])
+                yield from self._gen_feat_pairs([l1[:-1], l2[:-1], l3[:-1]], [l1[1:], l2[1:], l3[1:]],
+                                                out[:, c0:c1])
+            self._run_lanes(F_ - 1, lane)
+            self._feat = out
+            return None
         if frame_feats is not None:
             l1, l2, l3 = frame_feats
             if l1.shape[0] != F_:
                 raise ValueError(f"frame_feats hold {l1.shape[0]} frames, the window {F_}")
-        elif last_frame_feats is None:
-            l1, l2, l3 = self._frame_features(frames)
         else:
             a1, a2, a3 = self._frame_features(frames[:-1].contiguous())
             l1, l2, l3 = (torch.cat([a, b.reshape(1, *a.shape[1:]).to(a.device)])
                           for a, b in zip((a1, a2, a3), last_frame_feats))
-        self._feat = self._gen_feat_pairs([l1[:-1], l2[:-1], l3[:-1]], [l1[1:], l2[1:], l3[1:]])
+        self._run_lanes(F_ - 1, lambda c0, c1: self._gen_feat_pairs(
+            [l1[c0:c1], l2[c0:c1], l3[c0:c1]], [l1[c0 + 1:c1 + 1], l2[c0 + 1:c1 + 1], l3[c0 + 1:c1 + 1]],
+            out[:, c0:c1]))
+        self._feat = out
         return None
 
     @property
@@ -623,31 +702,37 @@ class LunaTokis(nn.Module):
             self._tables[key] = ops.DecTablesDev(H, Wd, HH, WW, self.device, shift)
         return self._tables[key]
 
-    def _projection(self, lr_image=True):
-        """LR projections P1..P4 of the current latent (stage 0 of every decoder variant)."""
+    def _projection(self, lr_image=True, c0=0, c1=None):
+        """LR projections P1..P4 of the current latent's items [c0, c1) (stage 0 of every decoder
+        variant)."""
         if self._feat is None:
             raise RuntimeError("decoding needs gen_feat first")
         feats, x = self._feat, self.inp
         _, B, H, Wd, _ = feats.shape
+        c1 = B if c1 is None else c1
+        f, x, B = feats[:, c0:c1], x[c0:c1], c1 - c0
         src = self._empty(B, H, Wd, 200)
-        ops.dec_pack_lr(feats[0], feats[1], feats[2], x, src)
+        ops.dec_pack_lr(f[0], f[1], f[2], x, src)
         proj = self._empty(B, H, Wd, 256)
         self._conv([dict(layer=self.layers["dec.proj" if lr_image else "dec.proj_hrimg"], in0=src, out=proj)])
         return proj
 
-    def _decode(self, proj, times, HH, WW, tab, image=None):
+    def _decode_steps(self, proj, tvs, HH, WW, tab, outs, image=None):
+        """Decoder stages 1-2 of every query time (time vectors ``tvs``) into ``outs`` (generator)."""
         B = proj.shape[0]
         mlp = self.layers["dec.mlp"]
-        preds = []
         hrf = self._empty(B, HH, WW, 64)
         flow = self._empty(B, HH, WW, 4)
-        for tq in times:
-            t = self._time_vec(tq, B)
+        for t, out in zip(tvs, outs):
             ops.dec_stage1(proj, mlp, tab, t, hrf, flow, image, flags=self._dec_flags, status=self._status)
-            out = self._empty(B, 3, HH, WW)
             ops.dec_stage2(proj, mlp, hrf, flow, tab, t, out, image, flags=self._dec_flags, status=self._status)
-            preds.append(out)
-        return preds
+            yield
+
+    def _decode(self, proj, times, HH, WW, tab, image=None):
+        B = proj.shape[0]
+        outs = [self._empty(B, 3, HH, WW) for _ in times]
+        _drain(self._decode_steps(proj, [self._time_vec(tq, B) for tq in times], HH, WW, tab, outs, image))
+        return outs
 
     def decoding(self, times=None, scale=None):
         """LunaTokis.decoding (:364-459): list over times of [B,3,HH,WW] (unclamped)."""
@@ -656,10 +741,20 @@ class LunaTokis(nn.Module):
     def _decoding(self, times=None, scale=None):
         if times is None:
             raise ValueError("times must be a list of query times")
-        proj = self._projection()
-        _, H, Wd, _ = proj.shape
+        if self._feat is None:
+            raise RuntimeError("decoding needs gen_feat first")
+        _, B, H, Wd, _ = self._feat.shape
         HH, WW = (H * 4, Wd * 4) if scale is None else (int(scale[0]), int(scale[1]))
-        return self._decode(proj, times, HH, WW, self._tab(H, Wd, HH, WW))
+        tab = self._tab(H, Wd, HH, WW)
+        tvs = [self._time_vec(tq, B) for tq in times]
+        outs = [self._empty(B, 3, HH, WW) for _ in times]
+
+        def lane(c0, c1):
+            proj = self._projection(True, c0, c1)
+            yield
+            yield from self._decode_steps(proj, [t[c0:c1] for t in tvs], HH, WW, tab, [o[c0:c1] for o in outs])
+        self._run_lanes(B, lane)
+        return outs
 
     def decoding_test(self, times=None, scale=None):
         """LunaTokis.decoding_test (:461-598), what forward(test=True) returns: the flow and encode

@@ -121,6 +121,32 @@ def test_chunked_window_is_bit_identical(models):
     assert torch.equal(a, b)
 
 
+def test_lanes_are_bit_identical(models):
+    """Lanes (concurrent streams over pair ranges, LunaTokis(lanes=)) do not change a bit: the
+    window path (shared boundary frames encoded per lane), the gen_feat(x) path and decoding, for
+    1 / 2 / 4 lanes (4 lanes over 5 pairs: ranges 2, 2, 1)."""
+    m = models["f16x3"]
+    fr = synth(20, 6, 64, 96)
+    x = torch.stack([fr[:-1], fr[1:]], 1)
+    keep = m.lanes
+    res = {}
+    with torch.no_grad():
+        try:
+            for k in (1, 2, 4):
+                m.lanes = k
+                m.gen_feat_window(fr)
+                f = m.feat.clone()
+                d = [o.clone() for o in m.decoding([0.25, 0.5])]
+                g = m(x, [0.75])[0].clone()
+                res[k] = (f, d, g)
+        finally:
+            m.lanes = keep
+    for k in (2, 4):
+        assert torch.equal(res[k][0], res[1][0]), k
+        assert all(torch.equal(a, b) for a, b in zip(res[k][1], res[1][1])), k
+        assert torch.equal(res[k][2], res[1][2]), k
+
+
 def test_halo_features_are_bit_identical(models, stif):
     """The multi-GPU halo path: the boundary frame's encoder features handed in (last_frame_feats /
     frame_feats, what parallel.halo_exchange delivers) give bit-identical latents and outputs."""

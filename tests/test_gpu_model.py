@@ -55,11 +55,11 @@ def test_intermediates_match_reference(model, golden):
     g = golden["model_16x20"]
     x = torch.from_numpy(g["x"]).cuda()
     cap = {}
-    orig_bilstm, orig_pcd = model._bilstm, model._pcd_align
+    orig_bilstm, orig_pcd = model._bilstm_steps, model._pcd_align
 
-    def bilstm(X, *a, **k):
+    def bilstm(X, *a, **k):                             # a stage generator (LunaTokis._run_lanes)
         cap["fusion"] = X[1].detach().clone()           # fusion output = latent step 1 input
-        out = orig_bilstm(X, *a, **k)
+        out = yield from orig_bilstm(X, *a, **k)
         cap["bilstm"] = out.detach().clone()
         return out
 
@@ -67,12 +67,12 @@ def test_intermediates_match_reference(model, golden):
         orig_pcd(units)
         if units[0][0] == "pcd_align." and "pcd" not in cap:
             cap["pcd"] = [u[4].detach().clone() for u in units]
-    model._bilstm, model._pcd_align = bilstm, pcd
+    model._bilstm_steps, model._pcd_align = bilstm, pcd
     try:
         with torch.no_grad():
             model.gen_feat(x)
     finally:
-        del model._bilstm, model._pcd_align
+        del model._bilstm_steps, model._pcd_align
     nchw = lambda t: t.permute(0, 3, 1, 2)[0].cpu().numpy()
     pcd_out = np.concatenate([nchw(cap["pcd"][0]), nchw(cap["pcd"][1])], 0)     # cat(y1, y2) (:130)
     for name, got, ref in (("pcd_align", pcd_out, g["pcd_align"]), ("fusion", nchw(cap["fusion"]), g["fusion"]),
