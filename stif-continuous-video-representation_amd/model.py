@@ -448,9 +448,14 @@ class LunaTokis(nn.Module):
                    epi=L.EPI_LRELU)
         return b2, b3
 
-    def _pcd_align(self, units):
+    def _pcd_align(self, units, zero_l1=()):
         """PCD_Align.forward (:71-130) for up to 8 independent (module, direction) units.
-        unit = (prefix, d, fa[L1,L2,L3], fb[L1,L2,L3], y_out)."""
+        unit = (prefix, d, fa[L1,L2,L3], fb[L1,L2,L3], y_out).  ``zero_l1``: indices of units whose
+        fa L1 map is all zeros (the ConvLSTM's initial state, convlstm.py:60-63, sampled by the
+        reversed-direction alignment of the first step): their L1 DCN samples only zeros, so its output
+        is its bias wherever the offsets land (DCN_sep, dcn_v2.py:127-140: sum of 0 * w + b), and the
+        L1 offset branch that only steers it (L1_offset_conv1..3, conv_offset_mask) is not run for
+        them -- bit-identical to running it (for finite offsets)."""
         G = len(units)
         n, H, Wd, _ = units[0][2][0].shape
         lay = self.layers
@@ -501,19 +506,26 @@ class LunaTokis(nn.Module):
         l2fea = buf(1)
         conv_up(lambda i, u, c: dict(layer=L_(u, "L2_fea_conv"), in0=d2[i], in1=c, out=l2fea[i]),
                 l3fea, 1.0, L.EPI_LRELU)
-        # ---- L1
-        o1 = buf(0)
-        conv([dict(layer=L_(u, "L1_offset_conv1"), in0=u[2][0], in1=u[3][0], out=o1[i]) for i, u in E(units)],
-             epi=L.EPI_LRELU, in1_mode=1)
-        o2 = buf(0)
-        conv_up(lambda i, u, c: dict(layer=L_(u, "L1_offset_conv2"), in0=o1[i], in1=c, out=o2[i]),
-                l2off, 2.0, L.EPI_LRELU)
-        l1off = buf(0)
-        conv([dict(layer=L_(u, "L1_offset_conv3"), in0=o2[i], out=l1off[i]) for i, u in E(units)], epi=L.EPI_LRELU)
-        om = buf(0, 216)
-        conv([dict(layer=LO(u, "L1_dcnpack"), in0=l1off[i], out=om[i]) for i, u in E(units)], epi=L.EPI_OFFMASK)
+        # ---- L1 (offset branch and DCN for the units whose fa L1 is not all zeros; k = their index)
+        live = [(i, u) for i, u in E(units) if i not in zero_l1]
         d1 = buf(0)
-        dcn([dict(layer=L_(u, "L1_dcnpack"), inp=u[2][0], offmask=om[i], out=d1[i]) for i, u in E(units)])
+        if live:
+            o1 = self._empty(len(live), n, H, Wd, 64)
+            conv([dict(layer=L_(u, "L1_offset_conv1"), in0=u[2][0], in1=u[3][0], out=o1[k])
+                  for k, (i, u) in E(live)], epi=L.EPI_LRELU, in1_mode=1)
+            o2 = self._empty(len(live), n, H, Wd, 64)
+            conv([dict(layer=L_(u, "L1_offset_conv2"), in0=o1[k], in1=l2off[i], out=o2[k]) for k, (i, u) in E(live)],
+                 epi=L.EPI_LRELU, in1_mode=2, in1_scale=2.0)
+            l1off = self._empty(len(live), n, H, Wd, 64)
+            conv([dict(layer=L_(u, "L1_offset_conv3"), in0=o2[k], out=l1off[k]) for k, (i, u) in E(live)],
+                 epi=L.EPI_LRELU)
+            del o1, o2
+            om = self._empty(len(live), n, H, Wd, 216)
+            conv([dict(layer=LO(u, "L1_dcnpack"), in0=l1off[k], out=om[k]) for k, (i, u) in E(live)],
+                 epi=L.EPI_OFFMASK)
+            dcn([dict(layer=L_(u, "L1_dcnpack"), inp=u[2][0], offmask=om[k], out=d1[i]) for k, (i, u) in E(live)])
+        for i in zero_l1:
+            d1[i].copy_(L_(units[i], "L1_dcnpack").b.view(1, 1, 1, 64).expand_as(d1[i]))
         conv_up(lambda i, u, c: dict(layer=L_(u, "L1_fea_conv"), in0=d1[i], in1=c, out=u[4]),
                 l2fea, 1.0, L.EPI_NONE)
 
@@ -543,8 +555,13 @@ class LunaTokis(nn.Module):
             fr = [t, 2 - t]                               # forward / reversed sequence
             xin = [X[f] for f in fr]
             state = [[zero if t == 0 else hs[d, t - 1] for d in range(2)], [cs[d] for d in range(2)]]
-            # pyramids of the recurrent states: groups (pcd, dir)
-            py2, py3 = self._pyramid([(state[p][d], pcds[p]) for p in range(2) for d in range(2)])
+            # pyramids of the recurrent states: groups (pcd, dir); at step 0 both directions' states are the
+            # same zeros, so each pcd's pyramid is computed once and shared (groups (pcd, pcd))
+            if t == 0:
+                z2, z3 = self._pyramid([(zero, pcds[p]) for p in range(2)])
+                py2, py3 = [z2[p] for p in range(2) for d in range(2)], [z3[p] for p in range(2) for d in range(2)]
+            else:
+                py2, py3 = self._pyramid([(state[p][d], pcds[p]) for p in range(2) for d in range(2)])
             Y = self._empty(2, 2, 2, B, H, Wd, 64)       # (pcd, dir, align direction)
             units = []
             for p in range(2):
@@ -554,7 +571,8 @@ class LunaTokis(nn.Module):
                     f2 = [state[p][d], py2[gi], py3[gi]]
                     units.append((pcds[p] + "pcd_align.", 1, f1, f2, Y[p, d, 0]))
                     units.append((pcds[p] + "pcd_align.", 2, f2, f1, Y[p, d, 1]))
-            self._pcd_align(units)
+            # step 0: the reversed alignments (odd units) sample the all-zero initial state at L1
+            self._pcd_align(units, zero_l1=range(1, 8, 2) if t == 0 else ())
             T = self._empty(2, 2, B, H, Wd, 64)          # Easy_PCD.fusion outputs: (pcd, dir)
             self._conv([dict(layer=lay[pcds[p] + "fusion"], in0=Y[p, d, 0], in1=Y[p, d, 1], out=T[p, d])
                         for p in range(2) for d in range(2)], in1_mode=1)

@@ -147,6 +147,29 @@ def test_lanes_are_bit_identical(models):
         assert torch.equal(res[k][2], res[1][2]), k
 
 
+@pytest.mark.parametrize("mf", ["f16x3", "f32"])
+def test_zero_state_l1_skip_is_bit_identical(models, mf):
+    """PCD alignment of the ConvLSTM's first step: a unit whose sampled L1 map is the all-zero initial
+    state gets its L1 DCN bias without running the L1 offset branch (_pcd_align zero_l1) -- the
+    same bits as running it."""
+    m = models[mf]
+    B, H, W = 2, 32, 48
+    g = torch.Generator(device="cuda").manual_seed(5)
+    lv = [(H, W), (H // 2, W // 2), (H // 4, W // 4)]
+    x = [torch.rand(B, h, w, 64, device="cuda", generator=g) for h, w in lv]
+    st = [torch.zeros(B, H, W, 64, device="cuda")] + [torch.rand(B, h, w, 64, device="cuda", generator=g)
+                                                      for h, w in lv[1:]]
+    pf = "ConvBLSTM.forward_net.pcd_c.pcd_align."
+    outs = []
+    for zl in ((), (1,)):
+        y = torch.full((2, B, H, W, 64), float("nan"), device="cuda")
+        with torch.no_grad():
+            m._call(m._pcd_align, [(pf, 1, x, st, y[0]), (pf, 2, st, x, y[1])], zero_l1=zl)
+        outs.append(y)
+    assert bool(torch.isfinite(outs[1]).all())
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_halo_features_are_bit_identical(models, stif):
     """The multi-GPU halo path: the boundary frame's encoder features handed in (last_frame_feats /
     frame_feats, what parallel.halo_exchange delivers) give bit-identical latents and outputs."""

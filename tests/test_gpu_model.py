@@ -63,8 +63,8 @@ def test_intermediates_match_reference(model, golden):
         cap["bilstm"] = out.detach().clone()
         return out
 
-    def pcd(units):
-        orig_pcd(units)
+    def pcd(units, **kw):
+        orig_pcd(units, **kw)
         if units[0][0] == "pcd_align." and "pcd" not in cap:
             cap["pcd"] = [u[4].detach().clone() for u in units]
     model._bilstm_steps, model._pcd_align = bilstm, pcd
