@@ -257,3 +257,25 @@ def test_wino_offmask_groups_items(stif, hw, pf):
         a1, a2 = out[g].cpu().numpy(), ref.cpu().numpy()
         assert np.isfinite(a1).all()
         assert np.abs(a1 - a2).max() <= 1e-5 * np.abs(a2).max()
+
+
+@pytest.mark.parametrize("kind", ["plain", "offmask"])
+@pytest.mark.parametrize("pos", [(0, 0, 0), (12, 69, 63), (5, 33, 17), (6, 1, 40)])
+def test_wino_f16x3_range_status_single_element(stif, kind, pos):
+    """One input element past the split range (|x| * 2^4 > 65504) anywhere in the map -- tile
+    corners, tile row 0 / 1, any channel -- sets the status word (k_wino and k_wino_om), and an
+    in-range map leaves it clear."""
+    L, ops = stif._lib, stif.ops
+    H, W = 13, 70
+    x = rnd(2, 64, H, W, seed=7)
+    cout, mode, epi = (64, L.PACK_WINO, L.EPI_RELU) if kind == "plain" else (216, L.PACK_WINO_OFFMASK, L.EPI_OFFMASK)
+    layer = ops.pack_conv(rnd(cout, 64, 3, 3, seed=8, scale=0.05), rnd(cout, seed=9), mode | L.PACK_F16X3)
+    for big, want in ((0.0, 0), (1e5, 1)):
+        xx = x.copy()
+        if big:
+            y, xc, c = pos
+            xx[1, c, y, xc] = big
+        st = torch.zeros(1, dtype=torch.int32, device="cuda")
+        out = torch.empty(2, H, W, cout, device="cuda")
+        ops.conv2d([dict(layer=layer, in0=nhwc(xx), out=out)], epi=epi, status=st)
+        assert int(st.item()) == want, (big, pos)
