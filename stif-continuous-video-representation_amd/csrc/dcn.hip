@@ -56,12 +56,18 @@ STIF_DEV f32x4 dcn_sample4(const float* __restrict__ img, int H, int W, float h,
 #define DCN_TH 8   // 8 waves per workgroup (C1 L1 438.7 -> 414.9 us against 4, same-box A/B)
 #endif
 constexpr int DCN_ROWS = DCN_TH;   // waves per workgroup
+#ifndef DCN_M
+// staged margin (pixels) around the 3x3 footprint; samples beyond it use the global-load fallback.
+// C0 L1 (same-box A/B over the full bench): margin 2 / 3 / 4 / 6 / 8 -> 248 / 250 / 257 / 266 / 289 us --
+// staging a wider tile costs more than the fallbacks it saves
+#define DCN_M 2
+#endif
 
 // MR: output rows per wave (2 only with F16; the launcher picks it by grid size, see stif_dcn_nhwc)
 template <int EPI, int F16, int MR = 1>
 __global__ __launch_bounds__(64 * DCN_ROWS) void k_dcn(stif_dcn_args a) {
   static_assert(MR == 1 || F16, "two rows per wave: split-fp16 path only");
-  constexpr int NW = DCN_ROWS, TH = NW * MR, M = 4;
+  constexpr int NW = DCN_ROWS, TH = NW * MR, M = DCN_M;
   constexpr int TR = TH + 2 + 2 * M, TC = 32 + 2 + 2 * M;   // tile rows / cols
   constexpr int TP = TC;                                     // column pitch of the staged tile (16-B slots)
   constexpr int T_EL = TR * 2 * TP;                          // 16-B elements
