@@ -1,4 +1,4 @@
-"""Multi-process (gloo, world_size 2, CPU) coverage of the frame-pair sharding and the
+"""Multi-process (gloo, CPU) coverage of the frame-pair sharding and the
 optional boundary-frame halo exchange (stif_amd.parallel), with the oracle as compute."""
 import os
 import socket
@@ -64,3 +64,42 @@ def test_sharded_window_equals_single_process(sd):
         got = np.concatenate([np.load(os.path.join(d, f"r{r}.npy")) for r in range(2)])
     assert got.shape == ref.shape
     assert np.abs(got - ref).max() <= 1e-9 * np.abs(ref).max()
+
+
+def _halo_worker(rank, world, port, nframes, outdir):
+    """Rank r's shard of an nframes sequence; its 'features' are tagged with the global frame index,
+    so the received halo must be the right neighbour's first frame."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import stif_pkg
+    P = stif_pkg.load().parallel
+    shards = P.pair_shards(nframes, world)
+    a, b = shards[rank]
+    got = None
+    if b > a:
+        first = [torch.full((1, 2, 3, 4 * (lv + 1)), float(a * 10 + lv)) for lv in range(3)]
+        recv = P.halo_exchange(first, rank, world, shards=shards)
+        got = None if recv is None else [float(t.flatten()[0]) for t in recv]
+    np.save(os.path.join(outdir, f"h{rank}.npy"), np.array(got if got is not None else [-1.0]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("nframes,world", [(3, 4), (7, 3), (9, 4)], ids=["empty_shards", "uneven", "even"])
+def test_halo_exchange_neighbours(nframes, world):
+    """Rehearsal of the N-rank halo exchange (gloo): every rank with frames receives its last frame's
+    L1/L2/L3 features from the next rank with frames; ranks past the last pair (more ranks than pairs)
+    take no part and nobody waits on them."""
+    import stif_pkg
+    P = stif_pkg.load().parallel
+    shards = P.pair_shards(nframes, world)
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_halo_worker, args=(world, _free_port(), nframes, d), nprocs=world, join=True)
+        got = [np.load(os.path.join(d, f"h{r}.npy")).tolist() for r in range(world)]
+    for r, (a, b) in enumerate(shards):
+        nxt = shards[r + 1] if r + 1 < world else (0, 0)
+        if b > a and nxt[1] > nxt[0]:
+            assert nxt[0] == b - 1                                   # the shared boundary frame
+            assert got[r] == [nxt[0] * 10 + lv for lv in range(3)], (r, got[r])
+        else:
+            assert got[r] == [-1.0], (r, got[r])
