@@ -63,11 +63,12 @@ constexpr int DCN_ROWS = DCN_TH;   // waves per workgroup
 #define DCN_M 2
 #endif
 
-// MR: output rows per wave (2 only with F16; the launcher picks it by grid size, see stif_dcn_nhwc)
-template <int EPI, int F16, int MR = 1>
-__global__ __launch_bounds__(64 * DCN_ROWS) void k_dcn(stif_dcn_args a) {
+// MR: output rows per wave (2 only with F16); NW: waves per workgroup (4 for small F16 launches: twice
+// the workgroups, two per CU).  The launcher picks both by grid size, see stif_dcn_nhwc.
+template <int EPI, int F16, int MR = 1, int NW = DCN_ROWS>
+__global__ __launch_bounds__(64 * NW) void k_dcn(stif_dcn_args a) {
   static_assert(MR == 1 || F16, "two rows per wave: split-fp16 path only");
-  constexpr int NW = DCN_ROWS, TH = NW * MR, M = DCN_M;
+  constexpr int TH = NW * MR, M = DCN_M;
   constexpr int TR = TH + 2 + 2 * M, TC = 32 + 2 + 2 * M;   // tile rows / cols
   constexpr int TP = TC;                                     // column pitch of the staged tile (16-B slots)
   constexpr int T_EL = TR * 2 * TP;                          // 16-B elements
@@ -570,6 +571,16 @@ bool stif_dcn_shape(int channels, int channels_out, int kh, int kw, int sh, int 
 }
 constexpr size_t DCN_WPACK = 36864, DCN_BPACK = 64;
 
+int num_cus_dcn() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
 }  // namespace
 
 extern "C" int stif_dcn_nhwc(const stif_dcn_args* pa, void* stream) {
@@ -583,12 +594,21 @@ extern "C" int stif_dcn_nhwc(const stif_dcn_args* pa, void* stream) {
   // two rows per wave when that still gives >= 4 workgroups per CU (1 fits per CU: 110 KB of LDS)
   const long long wg2 = (long long)((a.W + 31) / 32) * ((a.H + 2 * DCN_ROWS - 1) / (2 * DCN_ROWS)) * a.ngroups * a.nitems;
   const bool mr2 = f16 && wg2 >= 1024;
-  const int th = DCN_ROWS * (mr2 ? 2 : 1);   // output rows per workgroup
+  // one row per wave and fewer workgroups than CUs (the PCD's L3 / pair-level L2 maps): 4-wave
+  // workgroups of 4 rows, so every CU gets work and each workgroup's 8 sequential groups are shorter
+  const int ncu = num_cus_dcn();
+  const long long wg1 = (long long)((a.W + 31) / 32) * ((a.H + DCN_ROWS - 1) / DCN_ROWS) * a.ngroups * a.nitems;
+  const bool nw4 = f16 && !mr2 && wg1 < ncu;
+  const int th = nw4 ? 4 : DCN_ROWS * (mr2 ? 2 : 1);   // output rows per workgroup
   dim3 grid(((a.W + 31) / 32) * ((a.H + th - 1) / th), 1, a.ngroups * a.nitems);
   if (a.epi == STIF_EPI_LRELU && mr2)
     hipLaunchKernelGGL((k_dcn<STIF_EPI_LRELU, 1, 2>), grid, dim3(64 * DCN_ROWS), 0, (hipStream_t)stream, a);
   else if (a.epi == STIF_EPI_NONE && mr2)
     hipLaunchKernelGGL((k_dcn<STIF_EPI_NONE, 1, 2>), grid, dim3(64 * DCN_ROWS), 0, (hipStream_t)stream, a);
+  else if (a.epi == STIF_EPI_LRELU && nw4)
+    hipLaunchKernelGGL((k_dcn<STIF_EPI_LRELU, 1, 1, 4>), grid, dim3(64 * 4), 0, (hipStream_t)stream, a);
+  else if (a.epi == STIF_EPI_NONE && nw4)
+    hipLaunchKernelGGL((k_dcn<STIF_EPI_NONE, 1, 1, 4>), grid, dim3(64 * 4), 0, (hipStream_t)stream, a);
   else if (a.epi == STIF_EPI_LRELU && f16)
     hipLaunchKernelGGL((k_dcn<STIF_EPI_LRELU, 1>), grid, dim3(64 * DCN_ROWS), 0, (hipStream_t)stream, a);
   else if (a.epi == STIF_EPI_NONE && f16)

@@ -232,11 +232,15 @@ def test_dcn_fused(ops, L, epi, hw, oscale, f16):
 
 
 @pytest.mark.parametrize("oscale", [2.0, 7.0])
-def test_dcn_fused_two_rows_per_wave(ops, L, oscale):
-    """Launches of >= 1024 workgroups run k_dcn<., 1, 2> (two output rows per wave, 16-row tiles): 8
-    weight groups x 16 items of one 70x37 map and offset field (2 x 5 tiles each; rows past the map in
-    the last tile), every output against the oracle of item 0 -- all 128 are the same computation."""
-    H, W, G, N = 70, 37, 8, 16
+@pytest.mark.parametrize("G,N", [(8, 16), (8, 2), (1, 2)], ids=["two_rows", "one_row_8waves", "one_row_4waves"])
+def test_dcn_fused_two_rows_per_wave(ops, L, oscale, G, N):
+    """The three f16x3 launch shapes of k_dcn, picked by grid size (stif_dcn_nhwc): >= 1024 two-row
+    workgroups run k_dcn<., 1, 2> (two output rows per wave, 16-row tiles: 8 weight groups x 16 items of
+    one 70x37 map, 2 x 5 tiles each, rows past the map in the last tile); fewer one-row 8-wave
+    workgroups than CUs run the 4-wave k_dcn<., 1, 1, 4> (G = 1, N = 2: 36 workgroups of 8 rows); in
+    between the 8-wave one-row kernel (G = 8, N = 2: 288).  Every output against the oracle of item 0 --
+    all G x N are the same computation."""
+    H, W = 70, 37
     x = rnd(1, 64, H, W, seed=34)
     w = rnd(64, 64, 3, 3, seed=35, scale=0.05)
     b = rnd(64, seed=36)
