@@ -49,11 +49,17 @@ STIF_DEV f32x4 dcn_sample4(const float* __restrict__ img, int H, int W, float h,
 // each (pixel, tap) computes its bilinear weights once; weights packed STIF_PACK_PLAIN |
 // STIF_PACK_F16X3 ([group][pair][nt][plane][lane][8 halves]).  On large maps each wave owns MR = 2
 // output rows (two M-tiles): every B fragment read from LDS feeds both rows' MFMAs, which halves the
-// weight traffic through LDS -- the kernel is bound by LDS bandwidth (bilinear corner reads at
-// data-dependent addresses conflict) -- and the 16-row tile stages 2.1x its pixels instead of 2.95x
-// (C0 L1 shape 342 -> 322 us); small maps keep MR = 1, where the halved grid would leave CUs idle.
+// weight traffic through LDS (the bilinear corner reads at data-dependent addresses conflict) and
+// stages fewer halo pixels per output (with 8 waves: C0 L1 shape 342 -> 322 us); small maps keep
+// MR = 1, where the halved grid would leave CUs idle.  The kernel is latency-bound (waves parked on
+// memory waits and group barriers 43 % of their cycles, profiles/r02_dcn_sq_c0l1.txt), so two
+// independent 4-wave workgroups per CU beat one 8-wave workgroup.
 #ifndef DCN_TH
-#define DCN_TH 8   // 8 waves per workgroup (C1 L1 438.7 -> 414.9 us against 4, same-box A/B)
+// 4 waves per workgroup: with two rows per wave an 8-row tile, two workgroups per CU (74 KB of LDS each)
+// whose group barriers and memory waits overlap -- C0 L1 DCN 240 -> 223 us against 8 waves (one
+// 16-row workgroup per CU), same-box A/B (profiles/r02_dcn_th_ab.log); round 1's one-row kernel was
+// faster with 8 (C1 L1 438.7 -> 414.9 us against 4)
+#define DCN_TH 4
 #endif
 constexpr int DCN_ROWS = DCN_TH;   // waves per workgroup
 #ifndef DCN_M
@@ -63,12 +69,11 @@ constexpr int DCN_ROWS = DCN_TH;   // waves per workgroup
 #define DCN_M 2
 #endif
 
-// MR: output rows per wave (2 only with F16); NW: waves per workgroup (4 for small F16 launches: twice
-// the workgroups, two per CU).  The launcher picks both by grid size, see stif_dcn_nhwc.
-template <int EPI, int F16, int MR = 1, int NW = DCN_ROWS>
-__global__ __launch_bounds__(64 * NW) void k_dcn(stif_dcn_args a) {
+// MR: output rows per wave (2 only with F16; the launcher picks it by grid size, see stif_dcn_nhwc)
+template <int EPI, int F16, int MR = 1>
+__global__ __launch_bounds__(64 * DCN_ROWS) void k_dcn(stif_dcn_args a) {
   static_assert(MR == 1 || F16, "two rows per wave: split-fp16 path only");
-  constexpr int TH = NW * MR, M = DCN_M;
+  constexpr int NW = DCN_ROWS, TH = NW * MR, M = DCN_M;
   constexpr int TR = TH + 2 + 2 * M, TC = 32 + 2 + 2 * M;   // tile rows / cols
   constexpr int TP = TC;                                     // column pitch of the staged tile (16-B slots)
   constexpr int T_EL = TR * 2 * TP;                          // 16-B elements
@@ -571,15 +576,6 @@ bool stif_dcn_shape(int channels, int channels_out, int kh, int kw, int sh, int 
 }
 constexpr size_t DCN_WPACK = 36864, DCN_BPACK = 64;
 
-int num_cus_dcn() {
-  static int n = 0;
-  if (!n) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-  }
-  return n;
-}
 
 }  // namespace
 
@@ -591,24 +587,15 @@ extern "C" int stif_dcn_nhwc(const stif_dcn_args* pa, void* stream) {
   if ((long long)a.H * a.W * 64 * 4 >= 0x7fffffffLL)
     return stif_fail(STIF_E_INVALID, "stif_dcn_nhwc: item larger than 2 GB (buffer addressing)");
   const bool f16 = a.flags & STIF_CONV_F16X3;
-  // two rows per wave when that still gives >= 4 workgroups per CU (1 fits per CU: 110 KB of LDS)
+  // two rows per wave (8-row workgroups, two per CU) when that still gives >= 4 workgroups per CU
   const long long wg2 = (long long)((a.W + 31) / 32) * ((a.H + 2 * DCN_ROWS - 1) / (2 * DCN_ROWS)) * a.ngroups * a.nitems;
   const bool mr2 = f16 && wg2 >= 1024;
-  // one row per wave and fewer workgroups than CUs (the PCD's L3 / pair-level L2 maps): 4-wave
-  // workgroups of 4 rows, so every CU gets work and each workgroup's 8 sequential groups are shorter
-  const int ncu = num_cus_dcn();
-  const long long wg1 = (long long)((a.W + 31) / 32) * ((a.H + DCN_ROWS - 1) / DCN_ROWS) * a.ngroups * a.nitems;
-  const bool nw4 = f16 && !mr2 && wg1 < ncu;
-  const int th = nw4 ? 4 : DCN_ROWS * (mr2 ? 2 : 1);   // output rows per workgroup
+  const int th = DCN_ROWS * (mr2 ? 2 : 1);   // output rows per workgroup
   dim3 grid(((a.W + 31) / 32) * ((a.H + th - 1) / th), 1, a.ngroups * a.nitems);
   if (a.epi == STIF_EPI_LRELU && mr2)
     hipLaunchKernelGGL((k_dcn<STIF_EPI_LRELU, 1, 2>), grid, dim3(64 * DCN_ROWS), 0, (hipStream_t)stream, a);
   else if (a.epi == STIF_EPI_NONE && mr2)
     hipLaunchKernelGGL((k_dcn<STIF_EPI_NONE, 1, 2>), grid, dim3(64 * DCN_ROWS), 0, (hipStream_t)stream, a);
-  else if (a.epi == STIF_EPI_LRELU && nw4)
-    hipLaunchKernelGGL((k_dcn<STIF_EPI_LRELU, 1, 1, 4>), grid, dim3(64 * 4), 0, (hipStream_t)stream, a);
-  else if (a.epi == STIF_EPI_NONE && nw4)
-    hipLaunchKernelGGL((k_dcn<STIF_EPI_NONE, 1, 1, 4>), grid, dim3(64 * 4), 0, (hipStream_t)stream, a);
   else if (a.epi == STIF_EPI_LRELU && f16)
     hipLaunchKernelGGL((k_dcn<STIF_EPI_LRELU, 1>), grid, dim3(64 * DCN_ROWS), 0, (hipStream_t)stream, a);
   else if (a.epi == STIF_EPI_NONE && f16)

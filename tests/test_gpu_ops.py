@@ -232,13 +232,12 @@ def test_dcn_fused(ops, L, epi, hw, oscale, f16):
 
 
 @pytest.mark.parametrize("oscale", [2.0, 7.0])
-@pytest.mark.parametrize("G,N", [(8, 16), (8, 2), (1, 2)], ids=["two_rows", "one_row_8waves", "one_row_4waves"])
+@pytest.mark.parametrize("G,N", [(8, 16), (8, 2), (1, 2)], ids=["two_rows", "one_row", "one_row_small"])
 def test_dcn_fused_two_rows_per_wave(ops, L, oscale, G, N):
-    """The three f16x3 launch shapes of k_dcn, picked by grid size (stif_dcn_nhwc): >= 1024 two-row
-    workgroups run k_dcn<., 1, 2> (two output rows per wave, 16-row tiles: 8 weight groups x 16 items of
-    one 70x37 map, 2 x 5 tiles each, rows past the map in the last tile); fewer one-row 8-wave
-    workgroups than CUs run the 4-wave k_dcn<., 1, 1, 4> (G = 1, N = 2: 36 workgroups of 8 rows); in
-    between the 8-wave one-row kernel (G = 8, N = 2: 288).  Every output against the oracle of item 0 --
+    """The f16x3 launch shapes of k_dcn, picked by grid size (stif_dcn_nhwc): >= 1024 two-row workgroups
+    run k_dcn<., 1, 2> (two output rows per wave, 8-row tiles: 8 weight groups x 16 items of one 70x37
+    map, 2 x 9 tiles each, rows past the map in the last tile); fewer run the one-row kernel (G = 8,
+    N = 2: 576 workgroups of 4 rows; G = 1, N = 2: 72).  Every output against the oracle of item 0 --
     all G x N are the same computation."""
     H, W = 70, 37
     x = rnd(1, 64, H, W, seed=34)
