@@ -589,7 +589,10 @@ extern "C" int stif_dcn_nhwc(const stif_dcn_args* pa, void* stream) {
   const bool f16 = a.flags & STIF_CONV_F16X3;
   // two rows per wave (8-row workgroups, two per CU) when that still gives >= 4 workgroups per CU
   const long long wg2 = (long long)((a.W + 31) / 32) * ((a.H + 2 * DCN_ROWS - 1) / (2 * DCN_ROWS)) * a.ngroups * a.nitems;
-  const bool mr2 = f16 && wg2 >= 1024;
+#ifndef DCN_MR2_MIN
+#define DCN_MR2_MIN 1024   // 512 (two-row kernel also at the C0 L2 maps) measured no faster
+#endif
+  const bool mr2 = f16 && wg2 >= DCN_MR2_MIN;
   const int th = DCN_ROWS * (mr2 ? 2 : 1);   // output rows per workgroup
   dim3 grid(((a.W + 31) / 32) * ((a.H + th - 1) / th), 1, a.ngroups * a.nitems);
   if (a.epi == STIF_EPI_LRELU && mr2)
