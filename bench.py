@@ -202,6 +202,35 @@ def synth_frames(first, count, H, W, device):
     return out.to(device)
 
 
+# moving gratings (synthetic input (ii)): channel c of frame k is
+# 0.5 + 0.5 sin(2 pi (F_c x + G_c y) + PHI_c + V_c k), x / y in LR pixel units -- real, known motion,
+# and a ground truth at any HR pixel and continuous time (gratings_gt)
+GRATING_F = (0.05, 0.07, 0.03)
+GRATING_G = (0.04, -0.02, 0.06)
+GRATING_PHI = (0.0, 1.0, 2.0)
+GRATING_V = (0.3, -0.2, 0.25)
+
+
+def _grating(y, x, k):
+    return np.stack([0.5 + 0.5 * np.sin(2 * np.pi * (GRATING_F[c] * x + GRATING_G[c] * y) + GRATING_PHI[c]
+                                        + GRATING_V[c] * k) for c in range(3)])
+
+
+def gratings(first, count, H, W):
+    """frames [count, 3, H, W] (float32) of the moving gratings, frames first .. first + count - 1"""
+    y, x = np.meshgrid(np.arange(H, dtype=np.float64), np.arange(W, dtype=np.float64), indexing="ij")
+    return np.stack([_grating(y, x, first + i) for i in range(count)]).astype(np.float32)
+
+
+def gratings_gt(k0, t, H, W, HH, WW):
+    """ground truth [3, HH, WW] of the pair (k0, k0 + 1) at time t: the pattern at the HR pixel centres
+    ((X + 0.5) W / WW - 0.5 in LR units) and frame time k0 + t"""
+    yy = (np.arange(HH) + 0.5) * (H / HH) - 0.5
+    xx = (np.arange(WW) + 0.5) * (W / WW) - 0.5
+    y, x = np.meshgrid(yy, xx, indexing="ij")
+    return _grating(y, x, k0 + t)
+
+
 def _threads():
     try:
         from threadpoolctl import threadpool_info
@@ -210,49 +239,116 @@ def _threads():
         return int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
 
 
-def cpu_baseline(sd, x, times, scale):
-    """The numpy oracle (fp32) on a bounded sample of the same workload: one pair of the window
-    cropped to 128 x 128 LR pixels (FLOP per output pixel does not depend on the frame size), on
-    all host BLAS threads.  Returns (baseline record, oracle output)."""
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+CPU_SAMPLE = 64   # LR crop of the CPU-baseline sample (FLOP per output pixel does not depend on it)
+
+
+def _oracle_timed(threads=None):
+    """time the numpy oracle on the sample pair (frames 0-1 of the window cropped to CPU_SAMPLE^2,
+    4x, t = 0.5); threads=None: every host BLAS thread"""
     from oracle import stif_oracle as O
+    sd = __import__("stif_pkg").load().weights.make_state_dict(seed=0)
+    x = np.ascontiguousarray(synth_frames(0, 2, 128, 128, "cpu")[:, :, :CPU_SAMPLE, :CPU_SAMPLE].numpy()[None])
+    ctx = None
+    if threads:
+        from threadpoolctl import threadpool_limits
+        ctx = threadpool_limits(threads)
     t0 = time.perf_counter()
-    ref = O.forward(x, times, sd, dtype=np.float32)
+    O.forward(x, [0.5], sd, dtype=np.float32)
     dt = time.perf_counter() - t0
-    H, W = x.shape[-2:]
-    mpix = len(times) * H * scale * W * scale / 1e6
+    if ctx is not None:
+        ctx.unregister()
+    return dt
+
+
+def _pinned_child():
+    """child process: pinned to CPUs 0-7 (as taskset -c 0-7), 8 BLAS threads; prints the seconds"""
+    os.sched_setaffinity(0, range(8))
+    print(json.dumps({"s": _oracle_timed(8)}), flush=True)
+
+
+def cpu_baseline():
+    """The numpy oracle (fp32) on a bounded sample of the same workload -- one pair of the window
+    cropped to CPU_SAMPLE x CPU_SAMPLE LR pixels, 4x, t = 0.5 -- on all host BLAS threads, and again
+    in a child process pinned to 8 cores (the survey container's count, where the reference's own torch
+    CPU path was timed).  The child is a fresh interpreter that never touches the GPU."""
+    import subprocess
+    dt = _oracle_timed()
+    mpix = 16 * CPU_SAMPLE * CPU_SAMPLE / 1e6
+    pinned = None
+    try:
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-pinned-child"], capture_output=True,
+                           text=True, timeout=300, env=dict(os.environ, HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="8"))
+        pinned = json.loads(r.stdout.strip().splitlines()[-1])["s"]
+    except Exception as e:  # noqa: BLE001 -- the pinned leg is informational
+        print(f"pinned CPU baseline failed: {e}", file=sys.stderr)
+    sample = (f"1 pair (frames 0-1) of the window cropped to {CPU_SAMPLE}x{CPU_SAMPLE} -> {4 * CPU_SAMPLE}x"
+              f"{4 * CPU_SAMPLE}, t=0.5, numpy fp32 restatement (oracle/stif_oracle.py)")
     rec = {"value": round(mpix / dt, 6), "unit": "Mpix/s", "cores": _threads(), "kind": "port",
-           "sample": f"1 pair (frames 0-1) of the same window cropped to {H}x{W} -> {int(H * scale)}x{int(W * scale)}, "
-                     f"t={times}, numpy fp32 restatement (oracle/stif_oracle.py), {dt:.1f} s",
+           "sample": f"{sample}, {dt:.1f} s on all host threads", "cpu_model": cpu_model(),
+           "host_cpus": os.cpu_count(),
+           "pinned_8_cores": None if pinned is None else {
+               "value": round(mpix / pinned, 6), "unit": "Mpix/s", "cores": 8, "seconds": round(pinned, 2),
+               "how": "child process, sched_setaffinity CPUs 0-7 (as taskset -c 0-7), 8 BLAS threads"},
            "reference_torch_cpu": {"value": REF_TORCH_CPU_MPIX_S, "unit": "Mpix/s", "cores": 8,
                                    "note": "the reference's own torch CPU path (Sakuya_arch_test.LunaTokis, torch 2.10 "
                                            "+ mkldnn, 8 threads), one 128x128 pair -> 512x512 at t=0.5, measured in the "
                                            "survey container (BASELINE.md section 2); not re-run on the GPU box, where "
                                            "the reference is absent"}}
-    return rec, ref
+    return rec
 
 
-def parity_record(out, ref):
-    """GPU output vs the CPU oracle on the same pair: max errors, the north star's elementwise bar
-    (|a - b| <= 1e-4 |b| + 1e-6), PSNR vs the oracle, and the PSNR delta vs a ground truth."""
+def _psnr(x, gt):
+    m = float(np.mean((np.asarray(x, np.float64) - gt) ** 2))
+    return 10 * np.log10(1.0 / m) if m > 0 else float("inf")
+
+
+def parity_record(out, ref, gt, what, gt_desc):
+    """GPU output vs the reference model's own output on the same pair (fixture made by running the
+    reference here, tests/golden/make_golden.py): max errors, the north star's elementwise bar
+    (|a - b| <= 1e-4 |b| + 1e-6), PSNR vs the reference, and the PSNR criterion: both PSNRs against a
+    ground truth (calc_psnr form, myutils.py:269-271, data range 1) and their difference."""
     a = np.asarray(out, np.float64)
     b = np.asarray(ref, np.float64)
     d = np.abs(a - b)
     ok = d <= 1e-4 * np.abs(b) + 1e-6
     mse = float(np.mean(d ** 2))
-    # ground truth for the PSNR criterion (calc_psnr form, myutils.py:269-271, data range 1): the
-    # oracle's output rounded to 8-bit levels, the precision the harness writes frames in
-    gt = np.round(np.clip(b, 0, 1) * 255) / 255
-
-    def psnr(x):
-        m = float(np.mean((x - gt) ** 2))
-        return 10 * np.log10(1.0 / m) if m > 0 else float("inf")
-    return {"pair": "frames 0-1, 128x128 crop", "max_abs_err": float(d.max()),
+    return {"pair": what, "vs": "the reference model's own output (tests/golden)", "max_abs_err": float(d.max()),
             "max_err_rel_to_max_ref": float(d.max() / np.abs(b).max()),
             "elementwise_rtol1e-4_atol1e-6_frac": float(ok.mean()),
-            "psnr_vs_oracle_db": round(10 * np.log10(1.0 / mse), 2) if mse > 0 else None,
-            "psnr_gpu_vs_gt_db": round(psnr(a), 6), "psnr_oracle_vs_gt_db": round(psnr(b), 6),
-            "psnr_delta_db": abs(psnr(a) - psnr(b)),
-            "gt": "oracle output quantised to 8-bit levels (the harness's uint8 output precision)"}
+            "psnr_vs_reference_db": round(10 * np.log10(1.0 / mse), 2) if mse > 0 else None,
+            "psnr_gpu_vs_gt_db": round(_psnr(a, gt), 6), "psnr_reference_vs_gt_db": round(_psnr(b, gt), 6),
+            "psnr_delta_db": abs(_psnr(a, gt) - _psnr(b, gt)), "gt": gt_desc}
+
+
+def parity_records(stif, sd, device, mfma):
+    """the metric's pair (U[0,1) frames 0-1 at 128x128) and the moving-grating pair, 4x, t = 0.5"""
+    m = stif.LunaTokis(64, 6, 8, 5, 40, device=device, mfma=mfma)
+    m.load_state_dict(sd, strict=True)
+    recs = []
+    gd = os.path.join(REPO, "tests", "golden")
+    for name, what in (("c0_pair_128", "frames 0-1 of the C0 window (U[0,1), 128x128)"),
+                       ("gratings_128", "moving gratings, frames 0-1 (128x128)")):
+        g = np.load(os.path.join(gd, name + ".npz"))
+        with torch.no_grad():
+            out = m(torch.from_numpy(g["x"]).to(device), [0.5])[0][0].cpu().numpy()
+        ref = g["out"]
+        if name == "gratings_128":
+            gt, desc = gratings_gt(0, 0.5, 128, 128, 512, 512), "analytic moving-grating pattern at t = 0.5 (gratings_gt)"
+        else:
+            gt = np.round(np.clip(ref.astype(np.float64), 0, 1) * 255) / 255
+            desc = "the reference output quantised to 8-bit levels (the harness's uint8 output precision)"
+        recs.append(parity_record(out, ref, gt, what, desc))
+    return recs
 
 
 def run_config(stif, sd, cfg, args, world, rank, device, dist, mfma, trace_dom=True):
@@ -270,7 +366,8 @@ def run_config(stif, sd, cfg, args, world, rank, device, dist, mfma, trace_dom=T
     a, b = shards[rank]
     total_pairs = total_frames - 1
     HH, WW = int(round(H * scale)), int(round(W * scale))
-    model = stif.LunaTokis(64, 6, 8, 5, 40, device=device, mfma=mfma, lanes=args.lanes)
+    model = stif.LunaTokis(64, 6, 8, 5, 40, device=device, mfma=mfma, lanes=args.lanes,
+                           range_check=getattr(args, "range_check", "rerun"))
     model.load_state_dict(sd, strict=True)
     frames = synth_frames(a, b - a, H, W, device) if b > a else None
     tq = [torch.tensor([[t]], device=device) for t in times]
@@ -306,7 +403,42 @@ def run_config(stif, sd, cfg, args, world, rank, device, dist, mfma, trace_dom=T
     return elapsed, probe, timer, model, frames, tq, out_pix
 
 
+def host_inclusive(stif, sd, cfg, device, mfma, steps=3):
+    """End to end with the PCIe legs: the window's frames start in pinned host memory and every output
+    frame is copied back to pinned host memory inside the timed region (H2D + encoder + decoder + D2H);
+    not the headline value, whose inputs are resident in HBM."""
+    nframes, H, W, scale, times, _ = CONFIGS[cfg]
+    HH, WW = int(round(H * scale)), int(round(W * scale))
+    m = stif.LunaTokis(64, 6, 8, 5, 40, device=device, mfma=mfma)
+    m.load_state_dict(sd, strict=True)
+    host = synth_frames(0, nframes, H, W, "cpu").pin_memory()
+    outs = [torch.empty(nframes - 1, 3, HH, WW).pin_memory() for _ in times]
+    tq = [torch.tensor([[t]], device=device) for t in times]
+
+    def step():
+        fr = host.to(device, non_blocking=True)
+        m.gen_feat_window(fr)
+        for o, d in zip(outs, m.decoding(tq, None if scale == 4.0 else (HH, WW))):
+            o.copy_(d, non_blocking=True)
+
+    with torch.no_grad():
+        step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+    px = (nframes - 1) * len(times) * HH * WW
+    return {"value": round(px * steps / el / 1e6, 4), "unit": "Mpix/s", "ms_per_step": round(el / steps * 1e3, 3),
+            "steps": steps, "h2d_bytes": host.numel() * 4, "d2h_bytes": sum(o.numel() for o in outs) * 4,
+            "note": "frames H2D from pinned host memory and outputs D2H to pinned host memory inside the timed region"}
+
+
 def main():
+    if sys.argv[1:] == ["--cpu-pinned-child"]:
+        _pinned_child()
+        return
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -324,6 +456,9 @@ def main():
     ap.add_argument("--kernel-report", action="store_true", help="time every launch kind (stderr)")
     ap.add_argument("--time-every", type=int, default=1,
                     help="HIP-event-time every N-th launch of the dominant kernel in the timed region")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N>1 process group: nccl (= RCCL over xGMI, one GPU per rank) or gloo (host-staged halo; "
+                         "ranks may share a GPU -- the multi-rank GPU test on a one-GPU box)")
     ap.add_argument("--lanes", type=int, default=1,
                     help="concurrent HIP streams per rank, each a contiguous range of the pairs (LunaTokis lanes)")
     args = ap.parse_args()
@@ -332,10 +467,17 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     td = None
+    if args.backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         import torch.distributed as td
         torch.cuda.set_device(local)
-        td.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            # eager communicator (device_id): the halo exchange's batch_isend_irecv is not every rank's
+            # first collective (parallel.halo_exchange)
+            td.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            td.init_process_group("gloo")
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
@@ -348,7 +490,7 @@ def main():
     dom = timer.kind
     hot = hot_path_kernels(probe, args.mfma)
     if td is not None:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=device if args.backend == "nccl" else "cpu", dtype=torch.float64)
         td.all_reduce(t, op=td.ReduceOp.MAX)
         elapsed = float(t.item())
     n_launch, avg_ms, avg_flops, avg_bytes = timer.summary()
@@ -403,36 +545,43 @@ def main():
                                    f"{scale}x spatial, t={times}",
                        "name": args.config, "frames": nframes, "lr_hw": [H, W], "scale": scale, "times": times,
                        "parallelism": (f"sequence pair-sharded x{world}, boundary-frame features by "
-                                       f"{'RCCL P2P halo exchange' if args.halo == 'exchange' else 'recompute'}"
+                                       f"{('RCCL P2P halo exchange' if args.backend == 'nccl' else 'gloo host-staged halo exchange') if args.halo == 'exchange' else 'recompute'}"
                                        if world > 1 else "1 GPU")},
             "roofline": roofline(kname, kdesc, dom, peak, achieved, avg_ms, avg_flops, avg_bytes, timer.seen,
                                  traffic, n_timed=n_launch),
             "hot_path_kernels": hot,
         }
     if world == 1 and not args.no_extras:
-        # the same workload with every contraction on fp32 MFMA, then the C1 / C2 configs
+        # the same workload with every contraction on fp32 MFMA and without the per-call f16x3 range sync,
+        # then the other configs on this one GPU (C3 / C4: the whole sequence -- the 1-GPU denominators
+        # of the strong-scaling runs), and the host-inclusive line (frames from host memory, outputs back)
         extras = {}
-        runs = [(args.config, "f32" if args.mfma == "f16x3" else "f16x3")]
-        runs += [(c, args.mfma) for c in ("c1", "c2") if c != args.config and args.config in ("c0", "c1", "c2")]
-        for cfg, mf in runs:
+        runs = [(args.config, "f32" if args.mfma == "f16x3" else "f16x3", "rerun")]
+        if args.mfma == "f16x3":
+            runs.append((args.config, "f16x3", "off"))
+        runs += [(c, args.mfma, "rerun") for c in ("c1", "c2", "c3", "c4") if c != args.config]
+        reps = {"c0": (3, 1), "c1": (3, 1), "c2": (2, 1), "c3": (1, 1), "c4": (1, 1)}
+        for cfg, mf, rc in runs:
             a2 = argparse.Namespace(**vars(args))
-            a2.steps, a2.warmup = (3, 1) if cfg != "c2" else (2, 1)
+            a2.steps, a2.warmup = reps[cfg]
+            a2.range_check = rc
             del model
             torch.cuda.empty_cache()
             el, _, _, model, _, _, px = run_config(stif, sd, cfg, a2, 1, 0, device, None, mf, trace_dom=False)
-            extras[f"{cfg}_{mf}"] = {"value": round(px * a2.steps / el / 1e6, 4), "unit": "Mpix/s",
-                                     "ms_per_step": round(el / a2.steps * 1e3, 3), "steps": a2.steps}
+            key = f"{cfg}_{mf}" + ("_range_check_off" if rc == "off" else "")
+            extras[key] = {"value": round(px * a2.steps / el / 1e6, 4), "unit": "Mpix/s",
+                           "ms_per_step": round(el / a2.steps * 1e3, 3), "steps": a2.steps}
+            if cfg in ("c3", "c4"):
+                extras[key]["workload"] = (f"{CONFIGS[cfg][0]}-frame {CONFIGS[cfg][1]}x{CONFIGS[cfg][2]} sequence "
+                                           f"({CONFIGS[cfg][0] - 1} pairs), {CONFIGS[cfg][3]}x, t={CONFIGS[cfg][4]}, "
+                                           "all on 1 GPU (strong-scaling denominator)")
+        del model
+        torch.cuda.empty_cache()
+        extras[f"{args.config}_host_inclusive"] = host_inclusive(stif, sd, args.config, device, args.mfma)
         res["extra_lines"] = extras
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        fr = synth_frames(0, 2, H, W, "cpu")[:, :, :128, :128]
-        x = np.ascontiguousarray(fr.numpy()[None])
-        rec, ref = cpu_baseline(sd, x, [0.5], 4)
-        res["cpu_baseline"] = rec
-        m = stif.LunaTokis(64, 6, 8, 5, 40, device=device, mfma=args.mfma)
-        m.load_state_dict(sd, strict=True)
-        with torch.no_grad():
-            out = m(torch.from_numpy(x).to(device), [0.5])[0].cpu().numpy()
-        res["parity"] = parity_record(out, ref)
+        res["parity"], res["parity_gratings"] = parity_records(stif, sd, device, args.mfma)
+        res["cpu_baseline"] = cpu_baseline()
     if rank == 0:
         print(json.dumps(res), flush=True)
     if td is not None:

@@ -209,9 +209,10 @@ int stif_dec_stage2(const float* proj, const float* mlp, const float* hrfeat, co
                     int n, int h, int w, int HH, int WW, void* stream);
 /* The same stages with flags = STIF_CONV_F16X3: every SIREN layer on split-fp16 MFMA (mlp packed by
  * stif_pack_dec_mlp_ex with the same flag); flags = 0 is stif_dec_stage1 / stif_dec_stage2.
- * status: optional device word (NULL = none), set to 1 by stage 2 when an RGB output is not finite
- * in f16x3 mode (an HRfeat / hidden activation outside the split range propagates to the RGB:
- * every split operand of both stages feeds encode_imnet). */
+ * status: optional device word (NULL = none), set to 1 by stage 2 in f16x3 mode when an RGB output or
+ * the stage-1 flow it reads is not finite (an HRfeat / hidden activation outside the split range
+ * propagates to the RGB; a flow_imnet one to the flow, which the warpgrid clamp would otherwise turn
+ * into a finite grid). */
 int stif_dec_stage1_ex(const float* proj, const float* mlp, const stif_dec_tables* tab, const stif_dec_image* img,
                        const float* t, float* hrfeat, float* flow, int n, int h, int w, int HH, int WW, int flags,
                        int* status, void* stream);

@@ -532,6 +532,96 @@ def _decode(feat, inp, times, sd, HH, WW, dtype, capture=None, img=None, shift=N
     return preds, area
 
 
+def _bilinear_pts(get, H, W, gx, gy, dtype=np.float64):
+    """bilinear_sample at n points: F.grid_sample(bilinear, zeros, align_corners=False) with the
+    image read through ``get(yi, xi) -> [n, C]`` (fp32 source values) -> [n, C] in dtype."""
+    ix = ((np.asarray(gx, dtype) + 1) * W - 1) / 2
+    iy = ((np.asarray(gy, dtype) + 1) * H - 1) / 2
+    x0 = np.floor(ix)
+    y0 = np.floor(iy)
+    x1, y1 = x0 + 1, y0 + 1
+    out = 0
+    for xx, yy, ww in ((x0, y0, (x1 - ix) * (y1 - iy)), (x1, y0, (ix - x0) * (y1 - iy)),
+                       (x0, y1, (x1 - ix) * (iy - y0)), (x1, y1, (ix - x0) * (iy - y0))):
+        xi = xx.astype(np.int64)
+        yi = yy.astype(np.int64)
+        ok = (xi >= 0) & (xi < W) & (yi >= 0) & (yi < H)
+        v = np.asarray(get(np.clip(yi, 0, H - 1), np.clip(xi, 0, W - 1)), dtype)
+        out = out + np.where(ok[:, None], v, 0) * ww[:, None]
+    return out
+
+
+def decoding_at(feat, inp, times, sd, HH, WW, py, px, dtype=np.float64, stats=None):
+    """LunaTokis.decoding (Sakuya_arch_test.py:364-459) evaluated only at the HR pixels
+    (py[i], px[i]) -> list over times of [B, 3, n].  Same arithmetic as ``_decode``: every HR pixel's
+    stage 1 (feat_imnet -> HRfeat, flow_imnet -> flow, :380-422) depends only on that pixel's
+    coordinates, so the HRfeat the warped bilinear gathers of stage 2 read (:424-457) is evaluated at
+    just the corner pixels they touch.  ``feat`` [B,3,64,H,W] may be any strided view (it is read by
+    gathers only, never copied whole: full-size latents from the GPU engine); ``stats`` (a dict)
+    receives the number of warped samples whose grid was clamped at the frame edge (:428,441)."""
+    B = feat.shape[0]
+    H, W = feat.shape[-2:]
+    py = np.asarray(py, np.int64)
+    px = np.asarray(px, np.int64)
+    lo, hi = F32(-1 + 1e-6), F32(1 - 1e-6)
+    cy = np.clip(make_coord_1d(HH), lo, hi)
+    cx = np.clip(make_coord_1d(WW), lo, hi)
+    ly, lx = make_coord_1d(H), make_coord_1d(W)
+    iy = np.clip(nearest_index(cy, H), 0, H - 1)
+    ix = np.clip(nearest_index(cx, W), 0, W - 1)
+    rel_y = ((cy - ly[iy]) * F32(H)).astype(F32)
+    rel_x = ((cx - lx[ix]) * F32(W)).astype(F32)
+    assert (np.clip(nearest_index(cy, HH), 0, HH - 1) == np.arange(HH)).all()   # q_feat = HRfeat (:406-409)
+    assert (np.clip(nearest_index(cx, WW), 0, WW - 1) == np.arange(WW)).all()
+    gxs, gys = linspace_f32(WW), linspace_f32(HH)
+    preds = [np.empty((B, 3, len(py)), dtype) for _ in times]
+    clamped = 0
+    for b in range(B):
+        lat = lambda yy, xx: np.asarray(feat[b, :, :, yy, xx], F32).reshape(len(yy), 192)   # cat(feat[:,0..2])
+        img = lambda yy, xx: np.asarray(inp[b, :, :, yy, xx], F32).reshape(len(yy), 6)
+
+        def stage1_in(qy, qx, t):
+            """the 201 inputs of feat_imnet at HR pixels (qy, qx) (:382-399)"""
+            return np.concatenate([np.asarray(lat(iy[qy], ix[qx]), dtype), np.asarray(img(iy[qy], ix[qx]), dtype),
+                                   np.stack([rel_y[qy], rel_x[qx]], -1).astype(dtype),
+                                   np.full((len(qy), 1), t, dtype)], -1)
+
+        for ti, t in enumerate(times):
+            hrf = siren(stage1_in(py, px, t), sd, "feat_imnet.", 3, dtype)                      # (:400)
+            gx, gy = cx[px], cy[py]
+            q_inp2 = _bilinear_pts(img, H, W, gx, gy, dtype)                                    # (:410-413)
+            q_feat0 = _bilinear_pts(lat, H, W, gx, gy, dtype)                                   # (:414-417)
+            pe = np.full((len(py), 1), t, dtype)
+            flow = siren(np.concatenate([hrf, q_feat0, q_inp2, pe], -1), sd, "flow_imnet.", 3, dtype)
+            bx, by = gxs[px].astype(dtype), gys[py].astype(dtype)
+            grids = []
+            for k in range(2):                                                                  # warpgrid + clamp
+                ux = bx + flow[:, 2 * k] / ((WW - 1.0) / 2.0)
+                uy = by + flow[:, 2 * k + 1] / ((HH - 1.0) / 2.0)
+                clamped += int(((ux < lo) | (ux > hi) | (uy < lo) | (uy > hi)).sum())
+                grids.append((np.clip(ux, lo, hi), np.clip(uy, lo, hi)))
+            # HRfeat at every corner pixel the two warped gathers touch
+            cyx = []
+            for g_x, g_y in grids:
+                fx = np.floor(((g_x + 1) * WW - 1) / 2).astype(np.int64)
+                fy = np.floor(((g_y + 1) * HH - 1) / 2).astype(np.int64)
+                for dy in (0, 1):
+                    for dx in (0, 1):
+                        cyx.append(np.clip(fy + dy, 0, HH - 1) * WW + np.clip(fx + dx, 0, WW - 1))
+            uniq = np.unique(np.concatenate(cyx))
+            hrc = siren(stage1_in(uniq // WW, uniq % WW, t), sd, "feat_imnet.", 3, dtype)
+            hr_get = lambda yy, xx: hrc[np.searchsorted(uniq, yy * WW + xx)]
+            feats, imgs = [], []
+            for g_x, g_y in grids:
+                feats.append((_bilinear_pts(hr_get, HH, WW, g_x, g_y, dtype), _bilinear_pts(lat, H, W, g_x, g_y, dtype)))
+                imgs.append(_bilinear_pts(img, H, W, g_x, g_y, dtype))
+            x3 = np.concatenate([feats[0][0], feats[1][0], feats[0][1], feats[1][1], imgs[0], imgs[1], pe], -1)
+            preds[ti][b] = siren(x3, sd, "encode_imnet.", 4, dtype).T                              # (:456)
+    if stats is not None:
+        stats["clamped"] = clamped
+    return preds
+
+
 def decoding(feat, inp, times, sd, scale=None, dtype=np.float64, capture=None):
     """LunaTokis.decoding (Sakuya_arch_test.py:364-459).
     feat [B,3,64,H,W], inp [B,2,3,H,W], times: list of floats -> list of [B,3,HH,WW]."""

@@ -76,7 +76,7 @@ STIF_DEV f32x16 bias_sin(f32x16 z, const Bias32& bb) {
 #pragma unroll
   for (int v = 0; v < 4; ++v)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) z[4 * v + e] = stif_sin(fmaf(z[4 * v + e], ACC_S<F16>, bb.v[v][e]));
+    for (int e = 0; e < 4; ++e) z[4 * v + e] = siren_sin<F16>(fmaf(z[4 * v + e], ACC_S<F16>, bb.v[v][e]));
   return z;
 }
 template <int F16>
@@ -300,7 +300,7 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
         const int f = ot * 32 + 8 * v + 4 * hf;
         const f32x4 z = ld4(p1 + f) + ld4(mlp + F_WRY + f) * ry + ld4(mlp + F_WRX + f) * rx + ld4(mlp + F_WT + f) * t;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) x0[ot][4 * v + e] = stif_sin(z[e]);
+        for (int e = 0; e < 4; ++e) x0[ot][4 * v + e] = siren_sin<F16>(z[e]);
       }
   }
   auto seg_feat23 = [&](float* dst, int kt) {   // W2 rows kt (2 tiles), W3 (0, kt), (1, kt)
@@ -418,7 +418,7 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) tile_mma<F16>(z[ot], B1 + (ot * 2 + kt) * T, hs[kt], lane);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) z[ot][r] = stif_sin(z[ot][r] * ACC_S<F16>);
+      for (int r = 0; r < 16; ++r) z[ot][r] = siren_sin<F16>(z[ot][r] * ACC_S<F16>);
     }
   }
   {
@@ -538,7 +538,7 @@ __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DE
 #pragma unroll
       for (int kt = 2; kt < 4; ++kt) tile_mma<F16>(z[ot], B0 + (ot * 4 + kt) * T, qs[kt - 2], lane);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) x0[ot][r] = stif_sin(z[ot][r] * ACC_S<F16>);
+      for (int r = 0; r < 16; ++r) x0[ot][r] = siren_sin<F16>(z[ot][r] * ACC_S<F16>);
     }
   }
   lds_dma_barrier();
@@ -604,7 +604,9 @@ __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DE
   if (valid && hf == 0) {
     const size_t plane = (size_t)HH * WW;
     float* o = out + (size_t)item * 3 * plane + (size_t)py * WW + px;
-    bool bad = false;
+    // stage 1's flow counts too: the warpgrid clamp above maps a NaN flow to a finite grid, so an
+    // out-of-range flow_imnet operand would otherwise leave a finite but wrong pixel
+    bool bad = not_finite((fv[0] + fv[1]) + (fv[2] + fv[3]));
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const float v = o4[c] + mlp[E_B4 + c];
@@ -696,7 +698,7 @@ void launch_dec1(bool f16, long long blocks, hipStream_t st, const float* proj, 
 extern "C" int stif_dec_stage1_ex(const float* proj, const float* mlp, const stif_dec_tables* tab,
                                   const stif_dec_image* img, const float* t, float* hrfeat, float* flow, int n, int h,
                                   int w, int HH, int WW, int flags, int* status, void* stream) {
-  (void)status;   // stage 1's split operands all feed stage 2 (see stif.h)
+  (void)status;   // stage 2 checks both stage-1 outputs it reads (flow, and HRfeat through the RGB; stif.h)
   const bool f16 = flags & STIF_CONV_F16X3;
   if (!proj || !mlp || !tables_ok(tab) || !image_ok(img) || !t || !hrfeat || !flow || n < 1 || h < 1 || w < 1 ||
       HH < 2 || WW < 2 || (!tab->hr_y) != (!tab->hr_x))

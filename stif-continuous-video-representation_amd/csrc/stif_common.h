@@ -99,6 +99,30 @@ STIF_DEV float stif_sin(float x) {
   return __builtin_amdgcn_sinf(r * 0.159154943091895335769f);
 }
 
+// sin(x) for the fp32-operand decoder (F16 = 0, the fp32 re-run the range guard promises): quadrant
+// reduction by pi/2 (q = rint(x 2/pi), 3-part Cody-Waite constant, exact products for |q| < 2^12,
+// i.e. |x| < 6400) and minimax-free Taylor polynomials on [-pi/4, pi/4] through r^9 (sin) / r^8 (cos):
+// ~1e-7 absolute, the accuracy of the reference's torch.sin within a few ulp; ~20 VALU, no
+// transcendental.  The f16x3 decoder keeps the faster stif_sin above.
+__host__ __device__ __forceinline__ float stif_sin_poly(float x) {
+  const float qm = fmaf(x, 0.636619772367581343076f, 12582912.0f);   // round(x * 2/pi) by the magic add
+  const float q = qm - 12582912.0f;
+  float r = fmaf(q, -1.5703125f, x);                                   // pi/2 = P1 + P2 + P3, P1 8 bits
+  r = fmaf(q, -4.837512969970703125e-4f, r);
+  r = fmaf(q, -7.54978995489188216e-8f, r);
+  const float s = r * r;
+  const float ps = fmaf(fmaf(fmaf(fmaf(s, 2.75573192e-6f, -1.98412698e-4f), s, 8.33333333e-3f), s, -1.66666667e-1f) * s, r, r);
+  const float pc = fmaf(fmaf(fmaf(fmaf(s, 2.48015873e-5f, -1.38888889e-3f), s, 4.16666667e-2f), s, -0.5f), s, 1.0f);
+  const int qi = (int)q;
+  const float v = (qi & 1) ? pc : ps;
+  return (qi & 2) ? -v : v;
+}
+template <int F16>
+STIF_DEV float siren_sin(float x) {
+  if constexpr (F16) return stif_sin(x);
+  else return stif_sin_poly(x);
+}
+
 // Epilogue helper: write one 32 px x 32 cout accumulator tile (lane = cout, regs = px) into the
 // wave's private 4-KB LDS block as [px][co] with the 16-B slot XOR-swizzled by px & 3 (bank-conflict
 // free for both the b32 writes and the b128 row reads), so the global stores become coalesced

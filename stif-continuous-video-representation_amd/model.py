@@ -61,7 +61,7 @@ class LunaTokis(nn.Module):
     the module), never the parameters themselves."""
 
     def __init__(self, nf=64, nframes=3, groups=8, front_RBs=5, back_RBs=10, device="cuda", winograd=True,
-                 mfma="f16x3", range_check="rerun", chunk_px=2 ** 21, lanes=1):
+                 mfma="f16x3", range_check="rerun", chunk_px=2 ** 21, lanes=1, dec_chunk_px=2 ** 25):
         super().__init__()
         if nf != 64 or groups != 8:
             raise ValueError("the gfx950 kernels implement nf=64, groups=8 (the shipped STIF configuration)")
@@ -107,6 +107,8 @@ class LunaTokis(nn.Module):
         # pairs per encoder pass: a window is processed in chunks of about chunk_px LR pixels, which
         # bounds the PCD / BiConvLSTM working set (~20 KB per pair-pixel) at large frames
         self.chunk_px = int(chunk_px)
+        # HR pixels per decoder pass (decoding): bounds the decoder's scratch (~9 GB at the default)
+        self.dec_chunk_px = int(dec_chunk_px)
         # independent pair ranges run as `lanes` concurrent HIP streams (_run_lanes), so one lane's kernels
         # could fill the others' tail waves and dispatch gaps; results do not depend on it.  Default 1:
         # at C0, 2 lanes measured 5 % slower (82.5 -> 76.7, 84.6 -> 80.4 Mpix/s, same box) -- the
@@ -767,10 +769,19 @@ class LunaTokis(nn.Module):
         tvs = [self._time_vec(tq, B) for tq in times]
         outs = [self._empty(B, 3, HH, WW) for _ in times]
 
+        # items per decode pass: the LR projections (1 KB per LR pixel) and the HRfeat / flow scratch
+        # (272 B per HR pixel) of at most dec_chunk_px HR pixels -- a 63-pair 720p sequence on one GPU
+        # would otherwise need ~300 GB of scratch; every pixel is decoded independently, so chunking
+        # does not change a bit
+        per = max(1, self.dec_chunk_px // (HH * WW))
+
         def lane(c0, c1):
-            proj = self._projection(True, c0, c1)
-            yield
-            yield from self._decode_steps(proj, [t[c0:c1] for t in tvs], HH, WW, tab, [o[c0:c1] for o in outs])
+            for a in range(c0, c1, per):
+                b = min(c1, a + per)
+                proj = self._projection(True, a, b)
+                yield
+                yield from self._decode_steps(proj, [t[a:b] for t in tvs], HH, WW, tab, [o[a:b] for o in outs])
+                del proj
         self._run_lanes(B, lane)
         return outs
 

@@ -42,25 +42,36 @@ def halo_exchange(first_frame_feats: Sequence[torch.Tensor], rank: int, world: i
                   shards: Sequence[Tuple[int, int]] = None):
     """Send this rank's first-frame features to rank-1 and receive rank+1's (which is this rank's
     last frame): one neighbour exchange per rank, issued as one batched P2P group (RCCL over xGMI
-    with the nccl backend, gloo on CPU).  Returns the received tensors, or None when this rank has
-    no right neighbour with frames.  ``shards`` (pair_shards) lets ranks whose shard is empty --
-    more ranks than pairs -- drop out of the exchange instead of waiting on a peer that sends
-    nothing."""
+    with the nccl backend, gloo on CPU).  Returns the received tensors (on the device of the sent
+    ones), or None when this rank has no right neighbour with frames.  ``shards`` (pair_shards) lets
+    ranks whose shard is empty -- more ranks than pairs -- drop out of the exchange instead of
+    waiting on a peer that sends nothing.
+
+    With the gloo backend device tensors are staged through host memory (gloo's send/recv move CPU
+    tensors), so several ranks can share one GPU (the multi-rank GPU test).  With nccl the group's
+    communicator must exist before the first exchange -- ``init_process_group(..., device_id=...)``
+    (eager init, as bench.py does) or any collective run beforehand: ranks with an empty shard (or no
+    neighbour) never enter ``batch_isend_irecv``, and a lazily created NCCL communicator needs every
+    rank of the group in its first collective."""
     def has(r):
         return 0 <= r < world and (shards is None or shards[r][1] > shards[r][0])
 
     if not has(rank):
         return None
+    stage = dist.get_backend(group) == "gloo"
     ops = []
     recv = None
     if has(rank + 1):
-        recv = [torch.empty_like(t) for t in first_frame_feats]
+        recv = [torch.empty_like(t, device="cpu" if stage else t.device) for t in first_frame_feats]
         ops += [dist.P2POp(dist.irecv, t, rank + 1, group) for t in recv]
     if has(rank - 1):
-        ops += [dist.P2POp(dist.isend, t.contiguous(), rank - 1, group) for t in first_frame_feats]
+        ops += [dist.P2POp(dist.isend, (t.cpu() if stage else t).contiguous(), rank - 1, group)
+                for t in first_frame_feats]
     if ops:
         for q in dist.batch_isend_irecv(ops):
             q.wait()
+    if recv is not None and stage:
+        recv = [r.to(t.device) for r, t in zip(recv, first_frame_feats)]
     return recv
 
 

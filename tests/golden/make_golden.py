@@ -24,6 +24,7 @@ Usage:  python tests/golden/make_golden.py             (model, window and per-op
         python tests/golden/make_golden.py harness     (custom_video_test's imresize_np input resize)
         python tests/golden/make_golden.py single      (custom_video_test's single_forward, 11x13 pair)
         python tests/golden/make_golden.py c0          (BASELINE config C0: one full 128x128 pair, t=0.5)
+        python tests/golden/make_golden.py gratings    (C0-sized moving-grating pair, analytic ground truth)
 """
 import json
 import os
@@ -368,7 +369,27 @@ def c0():
     print("c0 pair:", tuple(out.shape), float(out.min()), float(out.max()))
 
 
+def gratings_c0():
+    """The moving-grating pair of bench.py (frames 0 and 1 of bench.gratings at 128 x 128, SURVEY.md
+    section 8d input (ii)) through the reference model, 4x, t = 0.5 -> gratings_128.npz; bench.py
+    measures the PSNR criterion against its analytic ground truth (bench.gratings_gt)."""
+    if not os.path.isdir(REF):
+        print("reference absent; nothing to do")
+        return
+    sys.path.insert(0, REPO)
+    from bench import gratings
+    model = _reference_model()
+    x = torch.from_numpy(gratings(0, 2, 128, 128))[None]
+    with torch.no_grad():
+        out = model(x, [torch.tensor([[0.5]])])[0]
+    np.savez_compressed(os.path.join(HERE, "gratings_128.npz"), x=f32(x), out=f32(out[0]))
+    print("gratings pair:", tuple(out.shape), float(out.min()), float(out.max()))
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["gratings"]:
+        gratings_c0()
+        sys.exit(0)
     if sys.argv[1:] == ["single"]:
         single()
         sys.exit(0)

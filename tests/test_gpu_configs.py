@@ -107,7 +107,8 @@ def test_config_full_size_f16x3_vs_f32(models, cfg):
 
 
 def test_chunked_window_is_bit_identical(models):
-    """Pair chunking (chunk_px: bounded working set at 720p/1080p) does not change a bit."""
+    """Pair chunking of the encoder (chunk_px) and of the decoder (dec_chunk_px): bounded working sets at
+    720p / 1080p, not a bit changed."""
     m = models["f16x3"]
     fr = synth(3, 5, 64, 96)
     with torch.no_grad():
@@ -118,7 +119,12 @@ def test_chunked_window_is_bit_identical(models):
         m.gen_feat_window(fr)
         b = m.decoding([0.5])[0]
         m.chunk_px = keep
+        keep = m.dec_chunk_px
+        m.dec_chunk_px = 2 * 256 * 384      # decoder passes of two pairs (2, 2, 0 + the last one)
+        c = m.decoding([0.5])[0]
+        m.dec_chunk_px = keep
     assert torch.equal(a, b)
+    assert torch.equal(a, c)
 
 
 def test_lanes_are_bit_identical(models):

@@ -267,3 +267,34 @@ def test_f32_mfma_larger_size_vs_oracle(model_f32, sd):
         out = model_f32(torch.from_numpy(x).cuda(), [0.3])[0]
     ok, err, mx = close(out, ref)
     assert ok, (err, mx)
+
+
+def test_decoder_stage2_flags_nonfinite_flow(stif, sd, golden):
+    """f16x3 range guard through the decoder's stage boundary: a flow_imnet operand outside the split
+    range makes that pixel's flow NaN; stage 2's warpgrid clamp would turn it into a finite grid, so
+    stage 2 reports the flow it reads (status word -> the fp32 re-run) instead of a finite wrong pixel."""
+    m = stif.LunaTokis(64, 6, 8, 5, 40)
+    m.load_state_dict(sd, strict=True)
+    g = golden["model_16x20"]
+    ops = stif.ops
+    with torch.no_grad():
+        m.gen_feat(torch.from_numpy(g["x"]).cuda())
+        proj = m._projection()
+        _, H, W, _ = proj.shape
+        HH, WW = 4 * H, 4 * W
+        tab = m._tab(H, W, HH, WW)
+        t = torch.full((1,), 0.5, device="cuda")
+        hrf = torch.empty(1, HH, WW, 64, device="cuda")
+        flow = torch.empty(1, HH, WW, 4, device="cuda")
+        mlp = m.layers["dec.mlp"]
+        assert m._dec_flags & stif._lib.CONV_F16X3
+        ops.dec_stage1(proj, mlp, tab, t, hrf, flow, flags=m._dec_flags)
+        out = torch.empty(1, 3, HH, WW, device="cuda")
+        for poison in (False, True):
+            st = torch.zeros(1, dtype=torch.int32, device="cuda")
+            f = flow.clone()
+            if poison:
+                f[0, 7, 11, 2] = float("nan")
+            ops.dec_stage2(proj, mlp, hrf, f, tab, t, out, flags=m._dec_flags, status=st)
+            assert int(st.item()) == int(poison)
+            assert bool(torch.isfinite(out).all())      # the clamp keeps the pixel finite: only the flag tells

@@ -1,0 +1,125 @@
+"""a training step through the `_ext` drop-in.
+
+A DCN_sep-bearing module (dcn_v2.py:110-140: conv_offset_mask, chunk / cat / sigmoid, the _DCNv2
+autograd wiring of dcn_v2.py:15-47 on `_ext.dcn_v2_forward` / `_ext.dcn_v2_backward`) takes one
+VideoSRBaseModel.optimize_parameters step (VideoSR_base_model.py:113-134): the Charbonnier loss
+(loss.py:7-17, sum of sqrt(d^2 + 1e-6)), backward, Adam with the shipped options (train_zsm.yml:56-59:
+lr 2e-5, betas (0.9, 0.99), no weight decay).  GPU: integration/_ext.py (stif_dcn_v2_forward /
+stif_dcn_v2_backward).  Oracle: the same step in float64 on the CPU with the DCN op restated
+(oracle dcn_v2_forward / dcn_v2_backward); conv, sigmoid, loss and Adam by torch (float64).
+"""
+import importlib.util
+import os
+
+import numpy as np
+import pytest
+import torch
+from torch import nn
+
+from oracle import stif_oracle as O
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _ext():
+    spec = importlib.util.spec_from_file_location("_ext", os.path.join(REPO, "integration", "_ext.py"))
+    ext = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ext)
+    return ext
+
+
+class _OracleBackend:
+    """the oracle as an `_ext` (float64 numpy in, torch float64 out)"""
+
+    @staticmethod
+    def dcn_v2_forward(inp, w, b, off, msk, *dims):
+        n = lambda t: t.detach().cpu().numpy()
+        return torch.from_numpy(O.dcn_v2_forward(n(inp), n(w), n(b), n(off), n(msk), *dims))
+
+    @staticmethod
+    def dcn_v2_backward(inp, w, b, off, msk, go, *dims):
+        n = lambda t: t.detach().cpu().numpy()
+        return [torch.from_numpy(np.asarray(g, np.float64)) for g in
+                O.dcn_v2_backward(n(inp), n(w), n(b), n(off), n(msk), n(go), *dims)]
+
+
+def make_dcn_conv(backend):
+    class _DCNv2(torch.autograd.Function):   # dcn_v2.py:15-47 wiring
+        @staticmethod
+        def forward(ctx, inp, offset, mask, weight, bias, dg):
+            ctx.dg = dg
+            ctx.save_for_backward(inp, offset, mask, weight, bias)
+            return backend.dcn_v2_forward(inp, weight, bias, offset, mask, 3, 3, 1, 1, 1, 1, 1, 1, dg)
+
+        @staticmethod
+        def backward(ctx, go):
+            inp, offset, mask, weight, bias = ctx.saved_tensors
+            gi, goff, gm, gw, gb = backend.dcn_v2_backward(inp, weight, bias, offset, mask, go.contiguous(),
+                                                           3, 3, 1, 1, 1, 1, 1, 1, ctx.dg)
+            return gi, goff, gm, gw, gb, None
+    return _DCNv2.apply
+
+
+class DcnSep(nn.Module):
+    """DCN_sep(64, 64, 3, stride=1, padding=1, deformable_groups=8) (dcn_v2.py:110-140)"""
+
+    def __init__(self, conv_fn, dtype, device):
+        super().__init__()
+        self.conv_fn = conv_fn
+        kw = dict(dtype=dtype, device=device)
+        self.weight = nn.Parameter(torch.empty(64, 64, 3, 3, **kw))
+        self.bias = nn.Parameter(torch.empty(64, **kw))
+        self.conv_offset_mask = nn.Conv2d(64, 216, 3, 1, 1, bias=True, **kw)
+
+    def forward(self, inp, fea):
+        out = self.conv_offset_mask(fea)
+        o1, o2, mask = torch.chunk(out, 3, dim=1)
+        offset = torch.cat((o1, o2), dim=1)
+        return self.conv_fn(inp, offset.contiguous(), torch.sigmoid(mask).contiguous(), self.weight, self.bias, 8)
+
+
+def charbonnier(x, y, eps=1e-6):   # loss.py:14-17
+    d = x - y
+    return torch.sum(torch.sqrt(d * d + eps))
+
+
+def _step(net, inp, fea, gt):
+    opt = torch.optim.Adam(net.parameters(), lr=2e-5, weight_decay=0, betas=(0.9, 0.99))
+    opt.zero_grad()
+    loss = charbonnier(net(inp, fea), gt)
+    loss.backward()
+    grads = {k: p.grad.detach().clone() for k, p in net.named_parameters()}
+    opt.step()
+    return float(loss.detach()), grads, {k: p.detach().clone() for k, p in net.named_parameters()}
+
+
+def test_training_step_through_ext_shim_matches_oracle(sd):
+    rng = np.random.default_rng(21)
+    B, H, W = 2, 12, 17
+    p = "pcd_align.L1_dcnpack_1"
+    init = {"weight": sd[p + ".weight"], "bias": sd[p + ".bias"],
+            "conv_offset_mask.weight": sd[p + ".conv_offset_mask.weight"] * 0.2,   # offsets of a few pixels
+            "conv_offset_mask.bias": sd[p + ".conv_offset_mask.bias"]}
+    inp = rng.standard_normal((B, 64, H, W)).astype(np.float32)
+    fea = rng.standard_normal((B, 64, H, W)).astype(np.float32)
+    gt = rng.standard_normal((B, 64, H, W)).astype(np.float32)
+    res = {}
+    for name, backend, dt, dev in (("gpu", _ext(), torch.float32, "cuda"), ("oracle", _OracleBackend, torch.float64, "cpu")):
+        net = DcnSep(make_dcn_conv(backend), dt, dev)
+        with torch.no_grad():
+            for k, v in net.named_parameters():
+                v.copy_(torch.from_numpy(np.asarray(init[k])))
+        T = lambda a: torch.from_numpy(a).to(dev, dt)
+        res[name] = _step(net, T(inp), T(fea), T(gt))
+    (lg, gg, pg), (lo, go, po) = res["gpu"], res["oracle"]
+    assert abs(lg - lo) <= 1e-5 * abs(lo)
+    for k in go:
+        g, r = gg[k].double().cpu(), go[k]
+        assert float((g - r).abs().max()) <= 2e-5 * float(r.abs().max()), k
+        # Adam's first step moves each parameter by ~lr * sign(grad): equal wherever the gradient's sign
+        # is not decided by rounding
+        d = (pg[k].double().cpu() - po[k]).abs()
+        firm = r.abs() > 1e-3 * r.abs().max()
+        assert float(d[firm].max()) <= 1e-6, k
+        assert float(d.max()) <= 2 * 2e-5 + 1e-6, k

@@ -180,3 +180,30 @@ def test_dcn_backward_oracle_matches_finite_differences(case):
             assert smooth.mean() > 0.98
             g, num = g[smooth], num[smooth]
         np.testing.assert_allclose(g, num, **tol)
+
+
+@pytest.mark.parametrize("size", [None, (40, 50)], ids=["4x", "2.5x"])
+def test_decoding_at_pixels_equals_full_decode(golden, sd, size):
+    """decoding_at (the pixel-subset decoder the full-size GPU tests pin against) = the full oracle
+    decode at every pixel it is asked for, incl. the 2.5x round-half-even tie rows/columns, the last
+    row/column and samples whose warped grid is clamped at the frame edge; and the full decode is the
+    reference's own output (fixture)."""
+    g = golden["model_16x20"]
+    feat, x = g["feat"].reshape(1, 3, 64, *g["feat"].shape[-2:]), g["x"]
+    H, W = feat.shape[-2:]
+    HH, WW = size or (4 * H, 4 * W)
+    full = O.decoding(feat, x, [0.5, 0.25], sd, size)
+    rng = np.random.default_rng(3)
+    py = np.concatenate([rng.integers(0, HH, 300), np.full(20, HH - 1), np.arange(20) % HH, [0, HH - 1]])
+    px = np.concatenate([rng.integers(0, WW, 300), rng.integers(0, WW, 20), np.full(20, WW - 1), [WW - 1, 0]])
+    # a strided view, as the GPU engine's latent arrives ([3,B,H,W,64] NHWC permuted)
+    fv = np.ascontiguousarray(feat.transpose(1, 0, 3, 4, 2)).transpose(1, 0, 4, 2, 3)
+    st = {}
+    sub = O.decoding_at(fv, x, [0.5, 0.25], sd, HH, WW, py, px, stats=st)
+    for a, b in zip(sub, full):
+        assert relmax(a, b[:, :, py, px]) < 1e-12
+    assert st["clamped"] > 0
+    if size is None:
+        assert relmax(full[0][0], g["out"][2]) < 1e-5                    # t = 0.5
+    else:
+        assert relmax(full[0], g["out_scale_40x50"]) < 1e-5

@@ -1,0 +1,9 @@
+# Round-3 check: GPU suite + the default bench (all extra lines, CPU baseline, parity) + C0 launch report.
+set -e
+R=$GRAFT_REPO_ROOT
+mkdir -p $R/gpurun_out/r3
+cd $R
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread > gpurun_out/r3/gpu_tests.log 2>&1 || { tail -40 gpurun_out/r3/gpu_tests.log; exit 1; }
+tail -2 gpurun_out/r3/gpu_tests.log
+timeout -k 10 600 python -u bench.py > gpurun_out/r3/bench.json 2> gpurun_out/r3/bench.err
+tail -c 3000 gpurun_out/r3/bench.json
