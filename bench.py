@@ -67,6 +67,10 @@ def kernel_desc(kind, mfma="f32"):
         _, ks, s, epi, in1, cout = kind
         return (f"k_conv<{ks}, {s}, ...>", f"{ks}x{ks}/s{s} conv -> {cout}, in1 mode {in1}, EPI_{EPI_NAMES[epi]}, "
                 "direct implicit GEMM on fp32 MFMA", FP32_PEAK_TFLOPS)
+    if kind[0] == "dcnsep":
+        return (f"k_dcn_sep<{kind[1]}>", "fused DCN_sep: offset/mask conv (direct, split-fp16 MFMA, offsets kept in the "
+                "accumulators) + sigmoid + modulated deformable conv; algorithmic = both convolutions' FLOPs, peak = fp16 "
+                "MFMA dense peak / 3", F16X3_PEAK_TFLOPS)
     if kind[0] == "dcn":
         if f16:
             return (f"k_dcn<{kind[1]}, 1>", "fused modulated deformable conv, split-fp16 MFMA (peak = fp16 MFMA / 3)",
@@ -181,14 +185,14 @@ def hot_path_kernels(probe, mfma):
     dec_peak = 2500.0 / 3 if mfma == "f16x3" else 157.3
     out = {}
     for k, (nl, ms, fl, nb) in probe.per_kind().items():
-        if k[0] not in ("dcn", "dec1", "dec2") or not ms:
+        if k[0] not in ("dcn", "dcnsep", "dec1", "dec2") or not ms:
             continue
         e = {"launches": nl, "avg_us": round(ms / nl * 1e3, 1), "tflops": round(fl / (ms * 1e-3) / 1e12, 1)}
         if nb:
             gbps = nb / (ms * 1e-3) / 1e9
             e.update(hbm_gbps_algorithmic=round(gbps, 1), hbm_frac=round(gbps / HBM_PEAK_GBPS, 3))
         if k[0] != "dcn":
-            e["mfma_frac"] = round(fl / (ms * 1e-3) / 1e12 / dec_peak, 3)
+            e["mfma_frac"] = round(fl / (ms * 1e-3) / 1e12 / dec_peak, 3)   # dcnsep / decoder: split-fp16 pipe
         out["_".join(str(x) for x in k)] = e
     return out
 
@@ -367,7 +371,7 @@ def run_config(stif, sd, cfg, args, world, rank, device, dist, mfma, trace_dom=T
     total_pairs = total_frames - 1
     HH, WW = int(round(H * scale)), int(round(W * scale))
     model = stif.LunaTokis(64, 6, 8, 5, 40, device=device, mfma=mfma, lanes=args.lanes,
-                           range_check=getattr(args, "range_check", "rerun"))
+                           range_check=getattr(args, "range_check", "rerun"), fused_dcn=bool(args.fused_dcn))
     model.load_state_dict(sd, strict=True)
     frames = synth_frames(a, b - a, H, W, device) if b > a else None
     tq = [torch.tensor([[t]], device=device) for t in times]
@@ -456,6 +460,8 @@ def main():
     ap.add_argument("--kernel-report", action="store_true", help="time every launch kind (stderr)")
     ap.add_argument("--time-every", type=int, default=1,
                     help="HIP-event-time every N-th launch of the dominant kernel in the timed region")
+    ap.add_argument("--fused-dcn", type=int, default=1, choices=[0, 1],
+                    help="f16x3: DCN_sep as one kernel (k_dcn_sep, default) or offset/mask conv + DCN core (0)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="N>1 process group: nccl (= RCCL over xGMI, one GPU per rank) or gloo (host-staged halo; "
                          "ranks may share a GPU -- the multi-rank GPU test on a one-GPU box)")

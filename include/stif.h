@@ -124,6 +124,29 @@ typedef struct {
 
 int stif_dcn_nhwc(const stif_dcn_args* args, void* stream);
 
+/* Fused DCN_sep (dcn_v2.py:127-140) in one launch: conv_offset_mask (64 -> 216, 3x3) + chunk / cat /
+ * sigmoid + the modulated deformable conv (64 -> 64, 3x3, 8 groups) -- the offset/mask map never leaves
+ * the registers (split-fp16 MFMA only, flags = STIF_CONV_F16X3).  fea: the offset branch's feature
+ * (NHWC 64 ch); in: the deformable conv's input (NHWC 64 ch); w_om / b_om: conv_offset_mask packed
+ * with STIF_PACK_DCNSEP | STIF_PACK_F16X3; w / bias: the DCN weight packed STIF_PACK_PLAIN |
+ * STIF_PACK_F16X3.  Replaces the pair conv (STIF_EPI_OFFMASK) -> stif_dcn_nhwc. */
+typedef struct {
+  const float* fea[STIF_MAX_GROUPS];
+  const float* in[STIF_MAX_GROUPS];
+  const float* w_om[STIF_MAX_GROUPS];
+  const float* b_om[STIF_MAX_GROUPS];
+  const float* w[STIF_MAX_GROUPS];
+  const float* bias[STIF_MAX_GROUPS];
+  float* out[STIF_MAX_GROUPS];
+  long long fea_item, in_item, out_item;
+  int ngroups, nitems, H, W;
+  int epi;                              /* STIF_EPI_NONE or STIF_EPI_LRELU */
+  int flags;                            /* must be STIF_CONV_F16X3 */
+  int* status;                          /* optional device word, as stif_conv_args.status */
+} stif_dcn_sep_args;
+
+int stif_dcn_sep_nhwc(const stif_dcn_sep_args* args, void* stream);
+
 /* Drop-in for `_ext.dcn_v2_forward` (dcn_v2.h:9-23): NCHW fp32 input [b,c,h,w],
  * weight [co,c,kh,kw], bias [co], offset [b, dg*2*kh*kw, ho, wo],
  * mask [b, dg*kh*kw, ho, wo]; output [b, co, ho, wo] (caller-allocated).
@@ -243,7 +266,7 @@ int stif_frames_to_u8(const float* nchw, unsigned char* hwc, int n, int H, int W
 
 /* ---- host-side weight packing (pure CPU, callable without a GPU) ---- */
 enum { STIF_PACK_PLAIN = 0, STIF_PACK_OFFMASK = 1, STIF_PACK_LSTM = 2, STIF_PACK_WINO = 3, STIF_PACK_WINO_OFFMASK = 4,
-       STIF_PACK_WINO_LSTM = 5 };
+       STIF_PACK_WINO_LSTM = 5, STIF_PACK_DCNSEP = 6 };
 /* OR'ed into a STIF_PACK_WINO* mode: the f16x3 split packing for stif_conv3x3_wino with
  * flags = STIF_CONV_F16X3 (same size in bytes) */
 #define STIF_PACK_F16X3 16
@@ -269,7 +292,13 @@ size_t stif_conv_bias_floats(int cout, int mode);
  * input channel 16 q + 8 (e >> 2) + 4 (l >> 5) + (e & 3) (the chunk pair of one f16 MFMA).
  * STIF_PACK_PLAIN | STIF_PACK_F16X3 (64 -> 64 3x3 only: the stif_dcn_nhwc core, and the 3x3
  * stride-2 convs of stif_conv2d_nhwc, with flags = STIF_CONV_F16X3): [group 8][tap pair 5][nt 2][plane h|l][lane 64][8 halves], element e
- * of lane l holding tap 2p + (l >> 5) (tap 9 = 0), input channel 8 group + e. */
+ * of lane l holding tap 2p + (l >> 5) (tap 9 = 0), input channel 8 group + e.
+ * STIF_PACK_DCNSEP | STIF_PACK_F16X3 (conv_offset_mask 64 -> 216, 3x3, for stif_dcn_sep_nhwc): the MFMA
+ * A operands [k 36][group 8][plane h|l][lane 64][8 halves] of W * 2^10, step k = 9 c + tap, lane l
+ * holding packed row i = l & 31 of the group and input channel 16 c + 8 (l >> 5) + e; row i is
+ * component r % 3 (dy, dx, mask) of tap 2 (r / 3) + ((i >> 2) & 1) with r = (i & 3) + 4 (i >> 3)
+ * (zero for r = 15 and tap 9) -- the accumulator register r of the lane half that samples that tap.
+ * Bias: [group 8][32] in the same row order. */
 int stif_pack_conv_weight(const float* w_oihw, const float* b, int cout, int cin, int ks, int mode,
                           float* w_dst, float* b_dst);
 
@@ -278,8 +307,11 @@ size_t stif_dec_proj_floats(void);   /* packed fp32 1x1 weight of the LR project
 int stif_pack_dec_proj(const float* feat_w0, const float* feat_b0, const float* flow_w0,
                        const float* enc_w0, float* w_dst, float* b_dst);
 /* lr_image bit 0 clear: P2..P4 without the image columns (decoding_test samples a high-resolution
- * image); lr_image | STIF_PACK_F16X3: the PLAIN | F16X3 1x1 packing for stif_conv2d_nhwc with
+ * image); lr_image | STIF_DEC_REVOLUTIONS: the sine-layer factor is omega_0 / (2 pi) instead of omega_0
+ * (pre-activations in revolutions), as the decoder stages run with STIF_CONV_F16X3 expect -- set it iff
+ * the mlp was packed with that flag; lr_image | STIF_PACK_F16X3: the PLAIN | F16X3 1x1 packing for stif_conv2d_nhwc with
  * flags = STIF_CONV_F16X3 (split-fp16 k_conv1x1) */
+#define STIF_DEC_REVOLUTIONS 2
 int stif_pack_dec_proj_ex(const float* feat_w0, const float* feat_b0, const float* flow_w0,
                           const float* enc_w0, int lr_image, float* w_dst, float* b_dst);
 size_t stif_dec_mlp_floats(void);
@@ -290,7 +322,8 @@ int stif_pack_dec_mlp(const float* const* feat, const float* const* flow, const 
                       float* dst);
 /* flags = STIF_CONV_F16X3: every 32x32 MFMA weight tile as a split-fp16 tile ([m 2][plane h|l][lane 64]
  * [8 halves] of W * 2^10, element e of half-tile m = feature F(8m + e, lane >> 5)) and the image tiles
- * scaled by 2^14, for stif_dec_stage1_ex / stif_dec_stage2_ex with the same flag. */
+ * scaled by 2^14, and the sine layers scaled by omega_0 / (2 pi) (revolutions: the stages evaluate
+ * v_sin_f32(x - rint(x))), for stif_dec_stage1_ex / stif_dec_stage2_ex with the same flag. */
 int stif_pack_dec_mlp_ex(const float* const* feat, const float* const* flow, const float* const* enc,
                          float* dst, int flags);
 

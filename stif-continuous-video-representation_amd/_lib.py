@@ -13,9 +13,10 @@ LIB_PATH = os.environ.get("STIF_HIP_LIB") or os.path.join(os.path.dirname(os.pat
 
 MAXG = 8
 EPI_NONE, EPI_LRELU, EPI_RELU, EPI_RES, EPI_OFFMASK, EPI_LSTM = range(6)
-PACK_PLAIN, PACK_OFFMASK, PACK_LSTM, PACK_WINO, PACK_WINO_OFFMASK, PACK_WINO_LSTM = range(6)
+PACK_PLAIN, PACK_OFFMASK, PACK_LSTM, PACK_WINO, PACK_WINO_OFFMASK, PACK_WINO_LSTM, PACK_DCNSEP = range(7)
 PACK_F16X3 = 16          # OR'ed into a PACK_WINO* mode (stif.h STIF_PACK_F16X3)
 CONV_F16X3 = 1           # stif_conv_args.flags
+DEC_REVOLUTIONS = 2      # stif_pack_dec_proj_ex lr_image bit (stif.h STIF_DEC_REVOLUTIONS)
 
 _P = C.c_void_p
 _PA = _P * MAXG
@@ -43,6 +44,15 @@ class DcnArgs(C.Structure):
     ]
 
 
+class DcnSepArgs(C.Structure):
+    _fields_ = [
+        ("fea", _PA), ("inp", _PA), ("w_om", _PA), ("b_om", _PA), ("w", _PA), ("bias", _PA), ("out", _PA),
+        ("fea_item", C.c_longlong), ("in_item", C.c_longlong), ("out_item", C.c_longlong),
+        ("ngroups", C.c_int), ("nitems", C.c_int), ("H", C.c_int), ("W", C.c_int), ("epi", C.c_int),
+        ("flags", C.c_int), ("status", _P),
+    ]
+
+
 class DecTables(C.Structure):
     _fields_ = [(n, _P) for n in ("near_y", "rel_y", "by0", "by1", "wy0", "wy1", "lin_y",
                                   "near_x", "rel_x", "bx0", "bx1", "wx0", "wx1", "lin_x", "hr_y", "hr_x")]
@@ -61,6 +71,7 @@ EXPORTS = {
                                        C.c_longlong, _P]),
     "stif_conv_first": (C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, C.c_int, _P]),
     "stif_dcn_nhwc": (C.c_int, [C.POINTER(DcnArgs), _P]),
+    "stif_dcn_sep_nhwc": (C.c_int, [C.POINTER(DcnSepArgs), _P]),
     "stif_dcn_v2_workspace_size": (C.c_size_t, [C.c_int] * 14),
     "stif_dcn_v2_forward": (C.c_int, [_P] * 6 + [C.c_int] * 14 + [_P, C.c_size_t, _P]),
     "stif_dcn_v2_backward_workspace_size": (C.c_size_t, [C.c_int] * 14),

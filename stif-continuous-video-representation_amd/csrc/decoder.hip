@@ -276,7 +276,7 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
     dma_tiles<DEC_NW>(B1 + 4 * T, rm, L_W1, 4, wv, lane);
   }
   const long long total = (long long)n * HH * WW;
-  const long long p = ((long long)blockIdx.x * DEC_NW + wv) * 32 + (lane & 31);
+  const long long p = ((long long)xcd_block(blockIdx.x, gridDim.x) * DEC_NW + wv) * 32 + (lane & 31);
   const bool valid = p < total;
   const long long pc = valid ? p : total - 1;
   const int item = (int)(pc / ((long long)HH * WW));
@@ -476,7 +476,7 @@ __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DE
   // then [W4: 8]
   dma_tiles<DEC2_NW>(B0, rm, E_W0, 8, wv, lane);
   const long long total = (long long)n * HH * WW;
-  const long long p = ((long long)blockIdx.x * DEC2_NW + wv) * 32 + (lane & 31);
+  const long long p = ((long long)xcd_block(blockIdx.x, gridDim.x) * DEC2_NW + wv) * 32 + (lane & 31);
   const bool valid = p < total;
   const long long pc = valid ? p : total - 1;
   const int item = (int)(pc / ((long long)HH * WW));

@@ -85,17 +85,23 @@ void column(float* dst, const float* W, int ld, int rows, int col) {
 
 // SineLayer: sin(omega_0 * (W x + b)) with omega_0 = 30 (SIREN.py:44-51): the packed copies of every
 // sine layer's weights and bias carry the factor (computed in double, rounded once), so the kernels
-// evaluate sin(W' x + b') without the multiply
+// evaluate sin(W' x + b') without the multiply.  `rev`: the factor is omega_0 / (2 pi), i.e. the
+// pre-activations come out in revolutions, the unit of the hardware sine (v_sin_f32), and the kernel's
+// range reduction is x - rint(x) (the f16x3 decoder: stif_sin_rev)
 constexpr double OMEGA0 = 30.0;
-std::vector<float> omega(const float* src, size_t n) {
+constexpr double TWO_PI = 6.283185307179586476925286766559;
+std::vector<float> omega(const float* src, size_t n, bool rev) {
+  const double s = rev ? OMEGA0 / TWO_PI : OMEGA0;
   std::vector<float> d(n);
-  for (size_t i = 0; i < n; ++i) d[i] = (float)(OMEGA0 * (double)src[i]);
+  for (size_t i = 0; i < n; ++i) d[i] = (float)(s * (double)src[i]);
   return d;
 }
 
 }  // namespace
 
 extern "C" size_t stif_conv_weight_floats(int cout, int cin, int ks, int mode) {
+  // DCNSEP | F16X3 (the fused DCN_sep's offset/mask conv): 36 steps x 8 groups x 2 planes x 1 KB
+  if (mode == (STIF_PACK_DCNSEP | STIF_PACK_F16X3)) return (size_t)36 * 8 * 2 * 256;
   // PLAIN | F16X3 (the DCN core, 64 -> 64 3x3): 5 tap pairs x 2 nt x 2 planes x 1 KB per 8-channel group
   if (mode == (STIF_PACK_PLAIN | STIF_PACK_F16X3) && ks == 3) return (size_t)(cin / 8) * 5 * 2 * 2 * 256;
   // PLAIN | F16X3 1x1 (k_conv1x1): 2 nt x 2 planes x 1 KB per (64-cout slice, 16-channel chunk)
@@ -107,6 +113,7 @@ extern "C" size_t stif_conv_weight_floats(int cout, int cin, int ks, int mode) {
 }
 
 extern "C" size_t stif_conv_bias_floats(int cout, int mode) {
+  if (mode == (STIF_PACK_DCNSEP | STIF_PACK_F16X3)) return 256;
   mode &= ~STIF_PACK_F16X3;
   return (mode == STIF_PACK_WINO || mode == STIF_PACK_WINO_OFFMASK || mode == STIF_PACK_WINO_LSTM)
              ? (size_t)round64(cout)
@@ -245,6 +252,43 @@ int pack_1x1_f16x3(const float* w, const float* b, int cout, int cin, float* w_d
     for (int j = 0; j < cout; ++j) b_dst[j] = b ? b[j] : 0.f;
   return STIF_OK;
 }
+// DCNSEP | F16X3: conv_offset_mask (216 x 64 x 3 x 3) as the A operands of k_dcn_sep's phase 1,
+// [k = 9 c + tap][group][plane][lane][8 halves]; packed row i of a group's 32-row block is component
+// r % 3 of tap 2 (r / 3) + ((i >> 2) & 1), r = (i & 3) + 4 (i >> 3) -- the MFMA accumulator register r
+// of lane half (i >> 2) & 1 -- with the reference channel of (group q, tap k): offset dy q*18 + 2k,
+// dx q*18 + 2k + 1, mask 144 + q*9 + k (dcn_v2.py:134-138, dcn_v2_im2col_cuda.cu:160-167)
+int dcnsep_src_row(int q, int i) {
+  const int hh = (i >> 2) & 1, r = (i & 3) + 4 * (i >> 3);
+  if (r >= 15) return -1;
+  const int tap = 2 * (r / 3) + hh, comp = r % 3;
+  if (tap > 8) return -1;
+  return comp == 0 ? q * 18 + 2 * tap : (comp == 1 ? q * 18 + 2 * tap + 1 : 144 + q * 9 + tap);
+}
+int pack_dcnsep_f16x3(const float* w, const float* b, int cout, int cin, int ks, float* w_dst, float* b_dst) {
+  if (cout != 216 || cin != 64 || ks != 3)
+    return stif_fail(STIF_E_INVALID, "STIF_PACK_DCNSEP packing needs the 64 -> 216 3x3 conv_offset_mask weight");
+  for (size_t i = 0; i < (size_t)cout * cin * 9; ++i)
+    if (!f16x3_ok(w[i])) return range_fail("stif_pack_conv_weight: a weight is outside the f16x3 range (|w| < 64); pack it without STIF_PACK_F16X3");
+  _Float16* dst = reinterpret_cast<_Float16*>(w_dst);
+  for (int k = 0; k < 36; ++k)
+    for (int q = 0; q < 8; ++q)
+      for (int l = 0; l < 64; ++l) {
+        const int src = dcnsep_src_row(q, l & 31), c = k / 9, t = k % 9;
+        for (int e = 0; e < 8; ++e) {
+          const int ci = 16 * c + 8 * (l >> 5) + e;
+          const double x = src >= 0 ? (double)w[((size_t)src * cin + ci) * 9 + t] : 0.0;
+          const size_t o = (((size_t)k * 8 + q) * 2) * 512 + l * 8 + e;
+          split_f16x3_host(x, dst + o, dst + o + 512);
+        }
+      }
+  if (b_dst)
+    for (int q = 0; q < 8; ++q)
+      for (int i = 0; i < 32; ++i) {
+        const int src = dcnsep_src_row(q, i);
+        b_dst[q * 32 + i] = (src >= 0 && b) ? b[src] : 0.f;
+      }
+  return STIF_OK;
+}
 }  // namespace
 
 extern "C" int stif_pack_conv_weight(const float* w, const float* b, int cout, int cin, int ks, int mode,
@@ -253,6 +297,10 @@ extern "C" int stif_pack_conv_weight(const float* w, const float* b, int cout, i
     return stif_fail(STIF_E_INVALID, "stif_pack_conv_weight: bad arguments");
   const bool f16x3 = (mode & STIF_PACK_F16X3) != 0;
   mode &= ~STIF_PACK_F16X3;
+  if (mode == STIF_PACK_DCNSEP) {
+    if (!f16x3) return stif_fail(STIF_E_INVALID, "STIF_PACK_DCNSEP exists for split-fp16 operands only (| STIF_PACK_F16X3)");
+    return pack_dcnsep_f16x3(w, b, cout, cin, ks, w_dst, b_dst);
+  }
   if ((mode == STIF_PACK_OFFMASK || mode == STIF_PACK_WINO_OFFMASK) && cout != 216)
     return stif_fail(STIF_E_INVALID, "offmask pack needs cout=216");
   if ((mode == STIF_PACK_LSTM || mode == STIF_PACK_WINO_LSTM) && cout != 256)
@@ -318,8 +366,9 @@ extern "C" int stif_pack_dec_proj_ex(const float* feat_w0, const float* feat_b0,
   const int C = stif_dec::SRC_C;
   std::vector<float> W((size_t)256 * C, 0.f), B(256, 0.f);
   // first layers are sine layers: omega_0-scaled (see stif_pack_dec_mlp)
-  const std::vector<float> fw = omega(feat_w0, 64 * 201), fb = omega(feat_b0, 64), lw = omega(flow_w0, 64 * 263),
-                           ew = omega(enc_w0, 64 * 525);
+  const bool rev = (lr_image & STIF_DEC_REVOLUTIONS) != 0;
+  const std::vector<float> fw = omega(feat_w0, 64 * 201, rev), fb = omega(feat_b0, 64, rev),
+                           lw = omega(flow_w0, 64 * 263, rev), ew = omega(enc_w0, 64 * 525, rev);
   feat_w0 = fw.data();
   feat_b0 = fb.data();
   flow_w0 = lw.data();
@@ -391,13 +440,13 @@ extern "C" int stif_pack_dec_mlp_ex(const float* const* f, const float* const* l
   const float* Lw[8];
   const float* E[10];
   for (int i = 0; i < 6; ++i) {
-    fs[i] = omega(f[i], fn[i]);
-    ls[i] = omega(l[i], ln[i]);
+    fs[i] = omega(f[i], fn[i], flags & STIF_CONV_F16X3);
+    ls[i] = omega(l[i], ln[i], flags & STIF_CONV_F16X3);
     F[i] = fs[i].data();
     Lw[i] = ls[i].data();
   }
   for (int i = 0; i < 8; ++i) {
-    es[i] = omega(e[i], en[i]);
+    es[i] = omega(e[i], en[i], flags & STIF_CONV_F16X3);
     E[i] = es[i].data();
   }
   F[6] = f[6]; F[7] = f[7];

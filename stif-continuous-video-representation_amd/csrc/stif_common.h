@@ -83,27 +83,20 @@ STIF_DEV float sigmoid_fast(float x) {
 enum { STIF_ACT_NONE = 0, STIF_ACT_LRELU = 1, STIF_ACT_RELU = 2, STIF_ACT_RES = 3,
        STIF_ACT_OFFMASK = 4, STIF_ACT_LSTM = 5 };
 
-// sin(x): one Cody-Waite step by 2 pi in radians (q = rint(x / 2 pi) by magic-number rounding; 2-part
-// constant, q * P1 exact for |q| < 2^16, |P1 + P2 - 2 pi| < 1.2e-10), then the hardware v_sin_f32 on
-// r / 2 pi in [-1/2, 1/2] revolutions.  5 VALU ops + one transcendental (8 issue cycles) instead of
-// a 15-op polynomial: the SIREN decoder is VALU-issue-bound and evaluates one sine per hidden unit.
-// v_sin_f32 alone, on x / 2 pi, loses accuracy with |x| (the rounding of x / 2 pi: 1.4e-6 at |x| = 16,
-// 2.8e-5 at 400); reduced first it stays within ~4e-7 of sin over |x| <= 3000
-// (tools/experiments/sin_acc.hip).  Used instead of ocml sinf, whose Payne-Hanek path costs ~200
-// VGPRs in the MLP kernels.
-STIF_DEV float stif_sin(float x) {
-  const float qm = fmaf(x, 0.159154943091895335769f, 12582912.0f);   // + 1.5 * 2^23 rounds to integer
-  const float q = qm - 12582912.0f;
-  float r = fmaf(q, -6.28125f, x);                                    // exact (P1 has 8 significant bits)
-  r = fmaf(q, -1.93530717958e-3f, r);
-  return __builtin_amdgcn_sinf(r * 0.159154943091895335769f);
-}
+// sin(2 pi x) for pre-activations in revolutions (the f16x3 decoder: omega_0 / (2 pi) is folded into
+// the packed sine-layer weights, stif_pack_dec_mlp_ex): x - rint(x) is exact, so the one rounding of
+// the reduction is the fp32 accumulation of x itself, as for a pre-activation in radians; then the
+// hardware v_sin_f32 on [-1/2, 1/2] revolutions (~4e-7 absolute, tools/experiments/sin_acc.hip).
+// 2 VALU + one transcendental (8 issue cycles): the SIREN decoder is VALU-issue-bound and evaluates one
+// sine per hidden unit.  Used instead of ocml sinf, whose Payne-Hanek path costs ~200 VGPRs in the MLP
+// kernels.
+STIF_DEV float stif_sin_rev(float x) { return __builtin_amdgcn_sinf(x - __builtin_rintf(x)); }
 
 // sin(x) for the fp32-operand decoder (F16 = 0, the fp32 re-run the range guard promises): quadrant
 // reduction by pi/2 (q = rint(x 2/pi), 3-part Cody-Waite constant, exact products for |q| < 2^12,
 // i.e. |x| < 6400) and minimax-free Taylor polynomials on [-pi/4, pi/4] through r^9 (sin) / r^8 (cos):
 // ~1e-7 absolute, the accuracy of the reference's torch.sin within a few ulp; ~20 VALU, no
-// transcendental.  The f16x3 decoder keeps the faster stif_sin above.
+// transcendental.  The f16x3 decoder uses the faster stif_sin_rev above.
 __host__ __device__ __forceinline__ float stif_sin_poly(float x) {
   const float qm = fmaf(x, 0.636619772367581343076f, 12582912.0f);   // round(x * 2/pi) by the magic add
   const float q = qm - 12582912.0f;
@@ -119,8 +112,18 @@ __host__ __device__ __forceinline__ float stif_sin_poly(float x) {
 }
 template <int F16>
 STIF_DEV float siren_sin(float x) {
-  if constexpr (F16) return stif_sin(x);
+  if constexpr (F16) return stif_sin_rev(x);
   else return stif_sin_poly(x);
+}
+
+// XCD-aware block order for grids of independent pixel blocks: workgroups are dealt round-robin over
+// the 8 XCDs (blocks b and b + 8 share one; each XCD has its own L2), so block b takes logical block
+// start(b % 8) + b / 8 -- every XCD walks a contiguous range of blocks, and maps read by neighbouring
+// blocks (halos, bilinear gathers) stay in one L2 instead of being fetched by several.  A bijection of
+// [0, nb) for any nb; speed only, never correctness.
+STIF_DEV int xcd_block(int b, int nb) {
+  const int x = b & 7, q = nb >> 3, r = nb & 7;
+  return x * q + min(x, r) + (b >> 3);
 }
 
 // Epilogue helper: write one 32 px x 32 cout accumulator tile (lane = cout, regs = px) into the

@@ -61,7 +61,8 @@ class LunaTokis(nn.Module):
     the module), never the parameters themselves."""
 
     def __init__(self, nf=64, nframes=3, groups=8, front_RBs=5, back_RBs=10, device="cuda", winograd=True,
-                 mfma="f16x3", range_check="rerun", chunk_px=2 ** 21, lanes=1, dec_chunk_px=2 ** 25):
+                 mfma="f16x3", range_check="rerun", chunk_px=2 ** 21, lanes=1, dec_chunk_px=2 ** 25,
+                 fused_dcn=True):
         super().__init__()
         if nf != 64 or groups != 8:
             raise ValueError("the gfx950 kernels implement nf=64, groups=8 (the shipped STIF configuration)")
@@ -98,6 +99,9 @@ class LunaTokis(nn.Module):
         if mfma not in ("f32", "f16x3"):
             raise ValueError("mfma must be 'f32' or 'f16x3'")
         self.mfma = mfma
+        # f16x3: DCN_sep as one kernel (offset/mask conv + sigmoid + deformable conv, k_dcn_sep); False =
+        # the offset/mask conv (k_wino_om) and the deformable conv (k_dcn) as two launches
+        self.fused_dcn = bool(fused_dcn)
         self._dec_flags = L.CONV_F16X3 if mfma == "f16x3" else 0   # decoder SIREN layers likewise
         # f16x3 activations outside the split range: "rerun" the call in fp32 (warning), "raise", or "off"
         if range_check not in ("rerun", "raise", "off"):
@@ -210,7 +214,17 @@ class LunaTokis(nn.Module):
                     n = f"{prefix}{ln}_{d}"
                     if cin is None:
                         conv(n, L.PACK_PLAIN | f16)     # the DCN core (k_dcn)
-                        conv(n + ".conv_offset_mask", (L.PACK_WINO_OFFMASK | f16) if self.winograd else L.PACK_OFFMASK)
+                        om = n + ".conv_offset_mask"
+                        if f16 and self.fused_dcn:
+                            # the fused DCN_sep kernel (k_dcn_sep); out of the split range -> the two-kernel path
+                            try:
+                                put(om, ops.pack_conv(h[om + ".weight"], h[om + ".bias"],
+                                                      L.PACK_DCNSEP | L.PACK_F16X3, dev, range_fallback=False))
+                                continue
+                            except L.StifError as e:
+                                if e.code != L.E_RANGE:
+                                    raise
+                        conv(om, (L.PACK_WINO_OFFMASK | f16) if self.winograd else L.PACK_OFFMASK)
                     else:
                         conv(n, wino)
 
@@ -228,11 +242,12 @@ class LunaTokis(nn.Module):
         for i in range(self.back_RBs):
             conv(f"recon_trunk.{i}.conv1", wino)
             conv(f"recon_trunk.{i}.conv2", wino)
-        # decoder: LR projections + the SIREN MLPs
-        for lr_image in (True, False):
-            put("dec.proj" if lr_image else "dec.proj_hrimg", self._pack_proj(lr_image))
+        # decoder: the SIREN MLPs, then the LR projections (their sine-layer scale follows the MLP's
+        # operand mode: omega_0 / (2 pi) -- revolutions -- with f16x3, stif.h STIF_DEC_REVOLUTIONS)
         mlp, flags = self._pack_mlp(self._dec_flags)
         self._dec_flags = flags
+        for lr_image in (True, False):
+            put("dec.proj" if lr_image else "dec.proj_hrimg", self._pack_proj(lr_image, bool(flags & L.CONV_F16X3)))
         meta["dec.mlp"] = (len(bufs), flags)
         bufs.append(mlp)
         bufs.append(torch.zeros(1, device=dev))
@@ -268,9 +283,10 @@ class LunaTokis(nn.Module):
             L.check(lib.stif_pack_dec_mlp_ex(fp, lp, ep, mlp.ctypes.data, 0), "stif_pack_dec_mlp_ex")
         return torch.from_numpy(mlp).to(self.device), flags
 
-    def _pack_proj(self, lr_image=True):
+    def _pack_proj(self, lr_image=True, revolutions=False):
         """LR projection of the decoder's first layers (stif_pack_dec_proj_ex); lr_image=False leaves
-        the LR frames out of P2..P4 for decoding_test, which samples the x4-upsampled frames."""
+        the LR frames out of P2..P4 for decoding_test, which samples the x4-upsampled frames;
+        revolutions: sine-layer scale omega_0 / (2 pi), matching an f16x3-packed MLP."""
         h, dev, lib = self._host, self.device, L.lib()
 
         def pack(mode):
@@ -280,7 +296,8 @@ class LunaTokis(nn.Module):
                                               h["feat_imnet.net.0.linear.bias"].ctypes.data,
                                               h["flow_imnet.net.0.linear.weight"].ctypes.data,
                                               h["encode_imnet.net.0.linear.weight"].ctypes.data,
-                                              int(lr_image) | (mode & L.PACK_F16X3), wd.ctypes.data, bd.ctypes.data),
+                                              int(lr_image) | (mode & L.PACK_F16X3) | (L.DEC_REVOLUTIONS if revolutions else 0),
+                                              wd.ctypes.data, bd.ctypes.data),
                     "stif_pack_dec_proj_ex")
             return ops.PackedConv(torch.from_numpy(wd).to(dev), torch.from_numpy(bd).to(dev), 256, 200, 1, mode)
 
@@ -367,6 +384,23 @@ class LunaTokis(nn.Module):
 
     def _dcn(self, groups, **kw):
         ops.dcn(groups, status=self._status, **kw)
+
+    def _dcn_sep(self, items, epi=L.EPI_NONE):
+        """DCN_sep.forward (dcn_v2.py:127-140) for a launch group of items (layer name, fea, inp, out):
+        the fused kernel where both layers are packed for it, else conv_offset_mask (OFFMASK epilogue)
+        into a 216-channel map and the deformable conv."""
+        lay = self.layers
+        fused = [it for it in items if ops.dcn_sep_fusable(lay[it[0] + ".conv_offset_mask"], lay[it[0]])]
+        rest = [it for it in items if not ops.dcn_sep_fusable(lay[it[0] + ".conv_offset_mask"], lay[it[0]])]
+        if fused:
+            ops.dcn_sep([dict(om_layer=lay[n + ".conv_offset_mask"], layer=lay[n], fea=f, inp=x, out=o)
+                         for n, f, x, o in fused], epi=epi, status=self._status)
+        if rest:
+            n0, f0 = rest[0][0], rest[0][1]
+            om = self._empty(len(rest), *f0.shape[:3], 216)
+            self._conv([dict(layer=lay[n + ".conv_offset_mask"], in0=f, out=om[i]) for i, (n, f, x, o) in enumerate(rest)],
+                       epi=L.EPI_OFFMASK)
+            self._dcn([dict(layer=lay[n], inp=x, offmask=om[i], out=o) for i, (n, f, x, o) in enumerate(rest)], epi=epi)
 
     def _empty(self, *shape):
         return torch.empty(*shape, device=self.device, dtype=torch.float32)
@@ -470,10 +504,7 @@ class LunaTokis(nn.Module):
         def L_(u, name):
             return lay[f"{u[0]}{name}_{u[1]}"]
 
-        def LO(u, name):
-            return lay[f"{u[0]}{name}_{u[1]}.conv_offset_mask"]
-
-        conv, dcn = self._conv, self._dcn
+        conv = self._conv
         E = enumerate
 
         def conv_up(make, coarse, scale, epi):
@@ -487,11 +518,8 @@ class LunaTokis(nn.Module):
              epi=L.EPI_LRELU, in1_mode=1)
         l3off = buf(2)
         conv([dict(layer=L_(u, "L3_offset_conv2"), in0=o[i], out=l3off[i]) for i, u in E(units)], epi=L.EPI_LRELU)
-        om = buf(2, 216)
-        conv([dict(layer=LO(u, "L3_dcnpack"), in0=l3off[i], out=om[i]) for i, u in E(units)], epi=L.EPI_OFFMASK)
         l3fea = buf(2)
-        dcn([dict(layer=L_(u, "L3_dcnpack"), inp=u[2][2], offmask=om[i], out=l3fea[i]) for i, u in E(units)],
-            epi=L.EPI_LRELU)
+        self._dcn_sep([(f"{u[0]}L3_dcnpack_{u[1]}", l3off[i], u[2][2], l3fea[i]) for i, u in E(units)], L.EPI_LRELU)
         # ---- L2
         o1 = buf(1)
         conv([dict(layer=L_(u, "L2_offset_conv1"), in0=u[2][1], in1=u[3][1], out=o1[i]) for i, u in E(units)],
@@ -501,10 +529,8 @@ class LunaTokis(nn.Module):
                 l3off, 2.0, L.EPI_LRELU)
         l2off = buf(1)
         conv([dict(layer=L_(u, "L2_offset_conv3"), in0=o2[i], out=l2off[i]) for i, u in E(units)], epi=L.EPI_LRELU)
-        om = buf(1, 216)
-        conv([dict(layer=LO(u, "L2_dcnpack"), in0=l2off[i], out=om[i]) for i, u in E(units)], epi=L.EPI_OFFMASK)
         d2 = buf(1)
-        dcn([dict(layer=L_(u, "L2_dcnpack"), inp=u[2][1], offmask=om[i], out=d2[i]) for i, u in E(units)])
+        self._dcn_sep([(f"{u[0]}L2_dcnpack_{u[1]}", l2off[i], u[2][1], d2[i]) for i, u in E(units)])
         l2fea = buf(1)
         conv_up(lambda i, u, c: dict(layer=L_(u, "L2_fea_conv"), in0=d2[i], in1=c, out=l2fea[i]),
                 l3fea, 1.0, L.EPI_LRELU)
@@ -522,10 +548,7 @@ class LunaTokis(nn.Module):
             conv([dict(layer=L_(u, "L1_offset_conv3"), in0=o2[k], out=l1off[k]) for k, (i, u) in E(live)],
                  epi=L.EPI_LRELU)
             del o1, o2
-            om = self._empty(len(live), n, H, Wd, 216)
-            conv([dict(layer=LO(u, "L1_dcnpack"), in0=l1off[k], out=om[k]) for k, (i, u) in E(live)],
-                 epi=L.EPI_OFFMASK)
-            dcn([dict(layer=L_(u, "L1_dcnpack"), inp=u[2][0], offmask=om[k], out=d1[i]) for k, (i, u) in E(live)])
+            self._dcn_sep([(f"{u[0]}L1_dcnpack_{u[1]}", l1off[k], u[2][0], d1[i]) for k, (i, u) in E(live)])
         for i in zero_l1:
             d1[i].copy_(L_(units[i], "L1_dcnpack").b.view(1, 1, 1, 64).expand_as(d1[i]))
         conv_up(lambda i, u, c: dict(layer=L_(u, "L1_fea_conv"), in0=d1[i], in1=c, out=u[4]),

@@ -214,6 +214,50 @@ def dcn(groups, *, epi=L.EPI_NONE, status=None):
         tr.end()
 
 
+def dcn_sep_fusable(om_layer: PackedConv, layer: PackedConv) -> bool:
+    """Both layers of a DCN_sep packed for the fused kernel (stif_dcn_sep_nhwc)."""
+    return om_layer.mode == (L.PACK_DCNSEP | L.PACK_F16X3) and layer.mode == (L.PACK_PLAIN | L.PACK_F16X3)
+
+
+def dcn_sep(groups, *, epi=L.EPI_NONE, status=None):
+    """Fused DCN_sep (dcn_v2.py:127-140): offset/mask conv + sigmoid + deformable conv in one launch.
+    groups: list of {om_layer: PackedConv (STIF_PACK_DCNSEP | F16X3), layer: PackedConv (64->64 3x3,
+    PLAIN | F16X3), fea, inp, out} with NHWC [nitems, H, W, 64] tensors."""
+    if not 1 <= len(groups) <= L.MAXG:
+        raise ValueError("dcn_sep: 1..8 groups")
+    g0 = groups[0]
+    nitems, H, W, Cc = g0["inp"].shape
+    a = L.DcnSepArgs()
+    for i, g in enumerate(groups):
+        if not dcn_sep_fusable(g["om_layer"], g["layer"]):
+            raise ValueError("dcn_sep: layers not packed for the fused kernel")
+        for k in ("fea", "inp", "out"):
+            if tuple(g[k].shape) != (nitems, H, W, 64):
+                raise ValueError(f"dcn_sep: {k} shape {tuple(g[k].shape)} != {(nitems, H, W, 64)}")
+        a.fea[i] = _vp(g["fea"])
+        a.inp[i] = _vp(g["inp"])
+        a.w_om[i] = _vp(g["om_layer"].w)
+        a.b_om[i] = _vp(g["om_layer"].b)
+        a.w[i] = _vp(g["layer"].w)
+        a.bias[i] = _vp(g["layer"].b)
+        a.out[i] = _vp(g["out"])
+    a.fea_item = _item_stride([g["fea"] for g in groups], "dcn_sep fea")
+    a.in_item = _item_stride([g["inp"] for g in groups], "dcn_sep in")
+    a.out_item = _item_stride([g["out"] for g in groups], "dcn_sep out")
+    a.ngroups, a.nitems, a.H, a.W, a.epi = len(groups), nitems, H, W, epi
+    a.flags = L.CONV_F16X3
+    a.status = _vp(status)
+    tr = TRACE
+    if tr is not None:
+        px = H * W * nitems * len(groups)
+        # algorithmic: the offset/mask conv (216 x 576 MACs) + the deformable conv (64 x 576) per pixel;
+        # HBM bytes: the offset feature, the DCN input and the output read / written once (768 B / px)
+        tr.begin(("dcnsep", epi), 2.0 * (216 + 64) * 576 * px, 4.0 * 3 * 64 * px)
+    L.check(L.lib().stif_dcn_sep_nhwc(C.byref(a), _stream()), "stif_dcn_sep_nhwc")
+    if tr is not None:
+        tr.end()
+
+
 def dcn_v2_forward(input, weight, bias, offset, mask, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w,
                    dilation_h, dilation_w, deformable_group):
     """Drop-in for ``_ext.dcn_v2_forward`` (DCNv2/src/dcn_v2.h:9-23): NCHW in, new NCHW tensor out."""

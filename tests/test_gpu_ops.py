@@ -432,3 +432,89 @@ def test_dcn_v2_forward_dropin_stif_shape_fused(ops, hw):
     T = lambda a: torch.from_numpy(a).cuda()
     out = ops.dcn_v2_forward(T(x), T(w), T(b), T(off), T(mask), 3, 3, 1, 1, 1, 1, 1, 1, 8)
     assert relmax(out, ref) < RTOL
+
+
+def _dcnsep_weights(seed, oscale, boundary=False, H=0):
+    """conv_offset_mask / DCN weights whose offsets have std ~ oscale px on N(0,1) features; with
+    `boundary`, a few offset channels get zero weights and a bias that lands samples exactly on the
+    `> -1` / `< H` gates (tap 0: dy = -1 -> h_im = oy - 2, exactly -1 at row 1; tap 4 of group 3: dx = -1.5;
+    tap 8 of group 7: dy = H -> h_im >= H everywhere)."""
+    w_om = rnd(216, 64, 3, 3, seed=seed, scale=oscale / 24.0)
+    b_om = rnd(216, seed=seed + 1, scale=0.5)
+    if boundary:
+        for ch, v in ((0, -1.0), (3 * 18 + 2 * 4 + 1, -1.5), (7 * 18 + 2 * 8, float(H)), (144 + 5 * 9 + 2, 40.0)):
+            w_om[ch] = 0.0
+            b_om[ch] = v
+    w = rnd(64, 64, 3, 3, seed=seed + 2, scale=0.05)
+    b = rnd(64, seed=seed + 3)
+    return {"x.conv_offset_mask.weight": w_om, "x.conv_offset_mask.bias": b_om, "x.weight": w, "x.bias": b}
+
+
+def _dcnsep_layers(ops, L, sdx):
+    om = ops.pack_conv(sdx["x.conv_offset_mask.weight"], sdx["x.conv_offset_mask.bias"], L.PACK_DCNSEP | L.PACK_F16X3,
+                       range_fallback=False)
+    core = ops.pack_conv(sdx["x.weight"], sdx["x.bias"], L.PACK_PLAIN | L.PACK_F16X3)
+    return om, core
+
+
+@pytest.mark.parametrize("epi", ["none", "lrelu"])
+@pytest.mark.parametrize("hw", [(9, 11), (8, 32), (16, 40), (21, 70), (70, 37)])
+@pytest.mark.parametrize("oscale", [0.7, 2.0, 7.0])   # 7.0: many samples leave the staged margin
+def test_dcn_sep_fused_matches_oracle(ops, L, epi, hw, oscale):
+    """k_dcn_sep (stif_dcn_sep_nhwc): conv_offset_mask + chunk/cat/sigmoid + the deformable conv in one
+    launch == DCN_sep.forward (dcn_v2.py:127-140) restated by the oracle; partial tiles (9x11, 21x70,
+    70x37), exact tiles (8x32), samples beyond the staged margin, two items."""
+    H, W = hw
+    B = 2
+    sdx = _dcnsep_weights(40, oscale)
+    x = rnd(B, 64, H, W, seed=41)
+    fea = rnd(B, 64, H, W, seed=42)
+    ref = O.dcn_sep(x, fea, sdx, "x")
+    if epi == "lrelu":
+        ref = O.lrelu(ref)
+    om, core = _dcnsep_layers(ops, L, sdx)
+    out = torch.full((B, H, W, 64), float("nan"), device="cuda")
+    st = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ops.dcn_sep([dict(om_layer=om, layer=core, fea=nhwc(fea), inp=nhwc(x), out=out)],
+                epi=L.EPI_LRELU if epi == "lrelu" else L.EPI_NONE, status=st)
+    assert int(st.item()) == 0
+    assert relmax(to_nchw(out), ref) < RTOL
+
+
+def test_dcn_sep_fused_gates_and_groups(ops, L):
+    """Offsets exactly on the sampling gates (bias-only offset channels), and a launch of 3 weight sets
+    over strided items (a [3, n, H, W, 64] buffer's sub-tensors), each against its own oracle."""
+    H, W = 19, 45
+    B = 3
+    xs = torch.from_numpy(np.ascontiguousarray(np.stack([rnd(B, H, W, 64, seed=50 + i) for i in range(3)]))).cuda()
+    fs = torch.from_numpy(np.ascontiguousarray(np.stack([rnd(B, H, W, 64, seed=60 + i) for i in range(3)]))).cuda()
+    out = torch.full((3, B, H, W, 64), float("nan"), device="cuda")
+    sds = [_dcnsep_weights(70 + 10 * i, 2.0 + i, boundary=True, H=H) for i in range(3)]
+    groups = []
+    for i, sdx in enumerate(sds):
+        om, core = _dcnsep_layers(ops, L, sdx)
+        groups.append(dict(om_layer=om, layer=core, fea=fs[i], inp=xs[i], out=out[i]))
+    ops.dcn_sep(groups, epi=L.EPI_NONE)
+    for i, sdx in enumerate(sds):
+        x = xs[i].cpu().numpy().transpose(0, 3, 1, 2)
+        f = fs[i].cpu().numpy().transpose(0, 3, 1, 2)
+        assert relmax(to_nchw(out[i]), O.dcn_sep(x, f, sdx, "x")) < RTOL, i
+
+
+def test_dcn_sep_fused_equals_two_kernel_path(ops, L):
+    """The fused kernel and the two-launch path it replaces (k_wino_om -> 216-channel map -> k_dcn, both
+    f16x3) agree to the parity bar on the STIF shape."""
+    H, W = 32, 48
+    sdx = _dcnsep_weights(80, 3.0)
+    x, fea = rnd(2, 64, H, W, seed=81), rnd(2, 64, H, W, seed=82)
+    om, core = _dcnsep_layers(ops, L, sdx)
+    a = torch.empty(2, H, W, 64, device="cuda")
+    ops.dcn_sep([dict(om_layer=om, layer=core, fea=nhwc(fea), inp=nhwc(x), out=a)])
+    omw = ops.pack_conv(sdx["x.conv_offset_mask.weight"], sdx["x.conv_offset_mask.bias"],
+                        L.PACK_WINO_OFFMASK | L.PACK_F16X3)
+    omap = torch.empty(2, H, W, 216, device="cuda")
+    ops.conv2d([dict(layer=omw, in0=nhwc(fea), out=omap)], epi=L.EPI_OFFMASK)
+    b = torch.empty(2, H, W, 64, device="cuda")
+    ops.dcn([dict(layer=core, inp=nhwc(x), offmask=omap, out=b)])
+    ref = O.dcn_sep(x, fea, sdx, "x")
+    assert relmax(to_nchw(a), ref) < RTOL and relmax(to_nchw(b), ref) < RTOL

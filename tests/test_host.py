@@ -221,3 +221,44 @@ def test_pack_wino_f16x3_layout(stif):
     with pytest.raises(Exception):
         L.check(lib.stif_pack_conv_weight(w.ctypes.data, b.ctypes.data, cout, cin, 3, L.PACK_OFFMASK | L.PACK_F16X3,
                                           wd.ctypes.data, bd.ctypes.data), "pack")
+
+
+def test_pack_dcnsep_layout(stif):
+    """STIF_PACK_DCNSEP | F16X3 (the fused DCN_sep's offset/mask conv, include/stif.h): packed row i of a
+    group's 32-row block = component r % 3 of tap 2 (r / 3) + ((i >> 2) & 1), r = (i & 3) + 4 (i >> 3),
+    which is the MFMA accumulator register r of the lane half that samples that tap; the f16 h + l
+    planes carry the weight to ~22 bits; the bias follows the rows; rows 15 / tap 9 are zero."""
+    L = stif._lib
+    lib = L.lib()
+    rng = np.random.default_rng(0)
+    w = (rng.standard_normal((216, 64, 3, 3)) * 0.1).astype(np.float32)
+    b = rng.standard_normal(216).astype(np.float32)
+    mode = L.PACK_DCNSEP | L.PACK_F16X3
+    wd = np.empty(lib.stif_conv_weight_floats(216, 64, 3, mode), np.float32)
+    bd = np.empty(lib.stif_conv_bias_floats(216, mode), np.float32)
+    L.check(lib.stif_pack_conv_weight(w.ctypes.data, b.ctypes.data, 216, 64, 3, mode, wd.ctypes.data,
+                                      bd.ctypes.data), "pack")
+    h = wd.view(np.float16).reshape(36, 8, 2, 64, 8).astype(np.float64)
+    val = (h[:, :, 0] + h[:, :, 1]) / 1024.0                    # [k][group][lane][e]
+    seen = set()
+    for q in range(8):
+        for i in range(32):
+            hh, r = (i >> 2) & 1, (i & 3) + 4 * (i >> 3)
+            tap = 2 * (r // 3) + hh
+            if r >= 15 or tap > 8:
+                assert bd[q * 32 + i] == 0 and not val[:, q, i].any() and not val[:, q, i + 32].any()
+                continue
+            comp = r % 3
+            src = (q * 18 + 2 * tap + comp) if comp < 2 else 144 + q * 9 + tap
+            seen.add(src)
+            assert bd[q * 32 + i] == b[src]
+            for k in range(36):
+                c, t = divmod(k, 9)
+                for lane in (i, i + 32):
+                    ci = 16 * c + 8 * (lane >> 5) + np.arange(8)
+                    assert np.abs(val[k, q, lane] - w[src, ci, t // 3, t % 3]).max() <= 2e-7 * np.abs(w).max()
+    assert seen == set(range(216))
+    # the mode exists for split-fp16 operands only
+    with pytest.raises(L.StifError):
+        L.check(lib.stif_pack_conv_weight(w.ctypes.data, b.ctypes.data, 216, 64, 3, L.PACK_DCNSEP, wd.ctypes.data,
+                                          bd.ctypes.data), "pack")

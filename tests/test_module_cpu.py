@@ -72,7 +72,8 @@ def test_model_packs_out_of_range_layers_in_fp32(stif, sd):
     L = stif._lib
     sd2 = dict(sd)
     sd2["recon_trunk.7.conv2.weight"] = sd["recon_trunk.7.conv2.weight"] * 3000.0
-    sd2["encode_imnet.net.3.linear.weight"] = sd["encode_imnet.net.3.linear.weight"] * 1000.0   # x30: > 64
+    # x 30 / (2 pi) (the f16x3 packing's sine scale, in revolutions): > 64
+    sd2["encode_imnet.net.3.linear.weight"] = sd["encode_imnet.net.3.linear.weight"] * 10000.0
     m = stif.LunaTokis(64, 6, 8, 5, 40, device="cpu")
     m.load_state_dict(sd2)
     lay = m._build_layers(m._pk, m._meta)
