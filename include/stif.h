@@ -128,7 +128,7 @@ int stif_dcn_nhwc(const stif_dcn_args* args, void* stream);
  * sigmoid + the modulated deformable conv (64 -> 64, 3x3, 8 groups) -- the offset/mask map never leaves
  * the registers (split-fp16 MFMA only, flags = STIF_CONV_F16X3).  fea: the offset branch's feature
  * (NHWC 64 ch); in: the deformable conv's input (NHWC 64 ch); w_om / b_om: conv_offset_mask packed
- * with STIF_PACK_DCNSEP | STIF_PACK_F16X3; w / bias: the DCN weight packed STIF_PACK_PLAIN |
+ * with STIF_PACK_DCNSEP | STIF_PACK_F16X3; w / bias: the DCN weight packed STIF_PACK_DCNPAIR |
  * STIF_PACK_F16X3.  Replaces the pair conv (STIF_EPI_OFFMASK) -> stif_dcn_nhwc. */
 typedef struct {
   const float* fea[STIF_MAX_GROUPS];
@@ -266,7 +266,7 @@ int stif_frames_to_u8(const float* nchw, unsigned char* hwc, int n, int H, int W
 
 /* ---- host-side weight packing (pure CPU, callable without a GPU) ---- */
 enum { STIF_PACK_PLAIN = 0, STIF_PACK_OFFMASK = 1, STIF_PACK_LSTM = 2, STIF_PACK_WINO = 3, STIF_PACK_WINO_OFFMASK = 4,
-       STIF_PACK_WINO_LSTM = 5, STIF_PACK_DCNSEP = 6 };
+       STIF_PACK_WINO_LSTM = 5, STIF_PACK_DCNSEP = 6, STIF_PACK_DCNPAIR = 7 };
 /* OR'ed into a STIF_PACK_WINO* mode: the f16x3 split packing for stif_conv3x3_wino with
  * flags = STIF_CONV_F16X3 (same size in bytes) */
 #define STIF_PACK_F16X3 16
@@ -294,11 +294,14 @@ size_t stif_conv_bias_floats(int cout, int mode);
  * stride-2 convs of stif_conv2d_nhwc, with flags = STIF_CONV_F16X3): [group 8][tap pair 5][nt 2][plane h|l][lane 64][8 halves], element e
  * of lane l holding tap 2p + (l >> 5) (tap 9 = 0), input channel 8 group + e.
  * STIF_PACK_DCNSEP | STIF_PACK_F16X3 (conv_offset_mask 64 -> 216, 3x3, for stif_dcn_sep_nhwc): the MFMA
- * A operands [k 36][group 8][plane h|l][lane 64][8 halves] of W * 2^10, step k = 9 c + tap, lane l
- * holding packed row i = l & 31 of the group and input channel 16 c + 8 (l >> 5) + e; row i is
- * component r % 3 (dy, dx, mask) of tap 2 (r / 3) + ((i >> 2) & 1) with r = (i & 3) + 4 (i >> 3)
- * (zero for r = 15 and tap 9) -- the accumulator register r of the lane half that samples that tap.
- * Bias: [group 8][32] in the same row order. */
+ * A operands [k 36][M-tile m 7][plane h|l][lane 64][8 halves] of W * 2^10, step k = 9 c + tap, lane l
+ * holding row i = l & 31 of M-tile m and input channel 16 c + 8 (l >> 5) + e.  Row i is accumulator
+ * register r = (i & 3) + 4 (i >> 3) of lane half h = (i >> 2) & 1; half h owns the deformable groups
+ * h, h + 2, h + 4, h + 6 and its slot s = 16 m + r < 108 holds component s % 3 (dy, dx, mask) of tap
+ * (s % 27) / 3 of group 2 (s / 27) + h (slots 108..111 zero).  Bias: [8][32] in the same row order.
+ * STIF_PACK_DCNPAIR | STIF_PACK_F16X3 (the 64 -> 64 3x3 DCN weight of stif_dcn_sep_nhwc): [group pair
+ * a 4][tap 9][nt 2][plane h|l][lane 64][8 halves], element e of lane l holding input channel
+ * 8 (2 a + (l >> 5)) + e, cout nt * 32 + (l & 31). */
 int stif_pack_conv_weight(const float* w_oihw, const float* b, int cout, int cin, int ks, int mode,
                           float* w_dst, float* b_dst);
 

@@ -7,24 +7,25 @@
 // dmcn_im2col_bilinear (dcn_v2_im2col_cuda.cu:25-54,125-195).
 //
 // Workgroup = 8 waves, tile = 8 output rows x 32 columns, wave w = output row w (lane & 31 = column).
+// Lane half h works on the deformable groups h, h + 2, h + 4, h + 6 throughout.
 //
 // Phase 1, the offset/mask conv as a direct implicit GEMM with the WEIGHTS as the MFMA A operand:
 // D[om row][pixel] += W[om row][k] X[k][pixel] on split-fp16 v_mfma_f32_32x32x16_f16 (f16x3, fp32
-// accumulation).  Each deformable group's 27 offset/mask channels are one 32-row block whose rows
-// are permuted at packing time (stif_pack_conv_weight, STIF_PACK_DCNSEP) so that the accumulator
-// registers of lane (pixel p, half h) hold exactly the (dy, dx, mask) of the taps h, h + 2, ..., h + 8
-// that lane half samples in phase 2 -- the offsets go from the MFMA accumulators straight into the
-// bilinear sampling, with no exchange, no LDS round trip and no HBM traffic.  K = 36 steps
-// (16-channel chunk c, tap t); per step a wave reads its pixels' 8 channels of the staged input
-// halo (two ds_read_b128), splits them once and runs 3 MFMAs for each of the 8 groups (24 MFMAs per
-// step; 128 accumulator VGPRs).  The input halo (10 x 34 pixels, one 16-channel chunk, 80-B pixel
-// pitch: conflict-free reads) and the packed weights of each step (16 KB, a 3-slot ring) arrive by
-// LDS-DMA ahead of use; one barrier per step.
+// accumulation), 216 rows in 7 M-tiles.  The rows are permuted at packing time (stif_pack_conv_weight,
+// STIF_PACK_DCNSEP) so that the accumulator registers of lane (pixel p, half h) hold exactly the
+// (dy, dx, mask) of every tap of its four groups -- the offsets go from the MFMA accumulators
+// straight into the bilinear sampling, with no exchange, no LDS round trip and no HBM traffic.
+// K = 36 steps (16-channel chunk c, tap t); per step a wave reads its pixels' 8 channels of the staged
+// input halo (two ds_read_b128), splits them once and runs 3 MFMAs per M-tile (21 MFMAs per step;
+// 112 accumulator VGPRs).  The input halo (10 x 34 pixels, one 16-channel chunk, 80-B pixel pitch:
+// conflict-free reads) and the packed weights of each step (a 3-slot ring) arrive by LDS-DMA ahead of
+// use; one barrier per step.
 //
-// Phase 2, k_dcn's sampling + contraction with 8 waves x 1 row: per deformable group the input
-// tile with a 2-px margin and the group's weight fragments are LDS-DMA'd one group ahead (group 0
-// during phase 1), each lane samples its tap of every tap pair for the group's 8 channels (global
-// fallback outside the margin) and runs 3 MFMAs per 32-cout half; epilogue through LDS as k_dcn.
+// Phase 2, the deformable conv, two groups per K step: per group pair (2a, 2a + 1) the 16-channel input
+// tile with a 2-px margin and the pair's weight fragments are LDS-DMA'd one pair ahead (pair 0 during
+// phase 1); for every tap t lane half h samples group 2a + h's 8 channels at its pixel (global fallback
+// outside the margin) -- the 16 K values of one 32x32x16 MFMA -- and runs 3 MFMAs per 32-cout half:
+// 9 K steps per pair instead of 10 for two single groups (tap pairs); epilogue through LDS as k_dcn.
 #include "abi_util.h"
 #include "stif.h"
 #include "stif_common.h"
@@ -34,37 +35,39 @@ namespace {
 constexpr int NW = 8;                         // waves = output rows per tile
 constexpr int TW = 32;                        // output columns per tile
 // phase 1
+constexpr int MT = 7;                         // offset/mask M-tiles (224 rows >= 216)
 constexpr int HC1 = TW + 2;                   // halo columns (10 halo rows)
 constexpr int PX_F = 20;                      // floats per staged halo pixel: 16 channels + 4 pad
 constexpr int D_SLOTS = (NW + 2) * HC1 * 5;   // 16-B slots per data chunk (1700)
 constexpr int D_INS = 32;                     // DMA instructions per data chunk (4 per wave; 27 carry data)
 constexpr int D_F = D_INS * 256;              // floats per data buffer
 constexpr int KSTEPS = 36;                    // k = 9 c + t: 16-channel chunk c, tap t
-constexpr int WK_F = 8 * 2 * 256;             // packed weights of one step: [group][plane][lane][8 halves]
+constexpr int WK_F = MT * 2 * 256;            // packed weights of one step: [M-tile][plane][lane][8 halves]
+constexpr int WK_INS = 16;                    // DMA instructions per step (2 per wave; 14 carry data)
 constexpr int RING = 3;
-// phase 2 (k_dcn geometry, MR = 1)
+// phase 2
 constexpr int M = 2;                          // staged margin around the 3x3 footprint
 constexpr int TR = NW + 2 + 2 * M, TC = TW + 2 + 2 * M, TP = TC;
-constexpr int T_EL = TR * 2 * TP;             // 16-B elements of the staged tile
-constexpr int T_INST = (T_EL + 63) / 64;      // 17
-constexpr int T_F = T_INST * 256;
-constexpr int W_F = 5 * 2 * 2 * 256;          // packed B fragments of one group
-constexpr int G_INS = 40;                     // DMA instructions per group stage (17 tile + 20 weights + 3 pad)
-constexpr int G_F = G_INS * 256;
-static_assert(T_INST + W_F / 256 <= G_INS && G_INS % NW == 0 && D_INS % NW == 0 && 16 % NW == 0, "stage sizes");
-static_assert(D_SLOTS <= D_INS * 64, "data chunk");
-// LDS map (floats): [data 0][data 1][weight ring][phase-2 buffer 0]; phase-2 buffer 1 reuses the data
-// buffers, the epilogue blocks the ring
-constexpr int OFF_D = 0, OFF_W = 2 * D_F, OFF_G0 = OFF_W + RING * WK_F, OFF_G1 = 0;
-constexpr int LDS_F = OFF_G0 + G_F;
-static_assert(G_F <= 2 * D_F && NW * 1024 <= RING * WK_F && LDS_F * 4 <= 160 * 1024, "LDS map");
-constexpr int DCN0_STEP = 28;
+constexpr int T_EL = TR * 4 * TP;             // 16-B elements of the staged tile: [row][channel quad][col]
+constexpr int T_INST = (T_EL + 63) / 64;      // 34
+constexpr int WP_F = 9 * 2 * 2 * 256;         // packed B fragments of one group pair (36 KB)
+constexpr int P_INS = 72;                     // DMA instructions per pair stage (34 tile + 36 weights + 2 pad)
+static_assert(T_INST + WP_F / 256 <= P_INS && P_INS % NW == 0 && D_INS % NW == 0 && WK_INS % NW == 0,
+              "stage sizes");
+static_assert(D_SLOTS <= D_INS * 64 && MT * 2 <= WK_INS, "phase-1 stages");
+// LDS map (floats).  Phase 1: data chunks D0, D1 and the weight ring; the stage of group pair 0 (tile X,
+// weights XW) lands in D0 (free once chunk 2 is done) and above the ring.  Phase 2: pairs alternate
+// between X and Y (tile Y over D1, weights YW over the ring); the epilogue blocks reuse D0.
+constexpr int PW_PAD_F = (P_INS - T_INST) * 256;    // pair weight region incl. the pad instructions
+constexpr int OFF_D0 = 0, OFF_D1 = T_INST * 256, OFF_W = OFF_D1 + D_F;
+constexpr int OFF_XT = 0, OFF_XW = OFF_W + RING * 4096;
+constexpr int OFF_YT = T_INST * 256, OFF_YW = OFF_YT + T_INST * 256;
+constexpr int LDS_F = OFF_XW + PW_PAD_F;
+static_assert(D_F <= OFF_D1 && OFF_YW + PW_PAD_F <= OFF_XW && WK_F <= 4096 &&
+              NW * 1024 <= D_F && LDS_F * 4 <= 160 * 1024, "LDS map");
 #ifndef DCNSEP_EXP
 #define DCNSEP_EXP 0    // timing probes (wrong results): 1 no phase 1, 3 no phase 2, 4 no fallback loads
 #endif
-#ifndef DCNSEP_ROLL
-#define DCNSEP_ROLL 0   // 1: phase 2 as a runtime loop over the groups (offsets rotated through registers)
-#endif                 // phase-1 step that DMAs phase 2's first group
 
 // vmcnt waits with an immediate operand (the counts are wave-uniform)
 STIF_DEV void wait_vm(int n) {
@@ -72,16 +75,9 @@ STIF_DEV void wait_vm(int n) {
     case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
     case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
     case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
-}
-// side DMA instructions a wave issues at step s after that step's weight DMA: the next data chunk
-// (4) at steps 1, 10, 19 and phase 2's first group (5) at DCN0_STEP
-STIF_DEV int side_dma(int s) {
-  if (s < 0) return 0;
-  if (s == DCN0_STEP) return G_INS / NW;
-  return (s % 9 == 1 && s / 9 < 3) ? D_INS / NW : 0;
 }
 
 template <int EPI>
@@ -99,7 +95,6 @@ __global__ __launch_bounds__(64 * NW) void k_dcn_sep(stif_dcn_sep_args a) {
   const int g = z / a.nitems, n = z - g * a.nitems;
   const float* fea = a.fea[g] + (size_t)n * a.fea_item;
   const float* in = a.in[g] + (size_t)n * a.in_item;
-  const float* wom = a.w_om[g];
   const float* wt = a.w[g];
   const int oy0 = ty * NW, ox0 = tx * TW;
   const int oy = oy0 + wv, ox = ox0 + l32;
@@ -107,8 +102,10 @@ __global__ __launch_bounds__(64 * NW) void k_dcn_sep(stif_dcn_sep_args a) {
   const unsigned img_bytes = (unsigned)((size_t)H * W * 64 * 4);
   const __amdgpu_buffer_rsrc_t rfea = __builtin_amdgcn_make_buffer_rsrc((void*)fea, (short)0, (int)img_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc((void*)in, (short)0, (int)img_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rwom =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.w_om[g], (short)0, KSTEPS * WK_F * 4, 0x00020000);
 
-  // ---------------------------------------------------------------- phase 1: offset/mask conv
+  // ---------------------------------------------------------------- stages (LDS-DMA)
   // data chunk c (channels 16c..16c+15) of the 10 x 34 halo: slot s = pixel * 5 + sub (sub 4 = pad)
   auto stage_data = [&](int c, float* dst) {
 #pragma unroll
@@ -123,87 +120,130 @@ __global__ __launch_bounds__(64 * NW) void k_dcn_sep(stif_dcn_sep_args a) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rfea, dst + i * 256, 16, voff, 0, 0, 0);
     }
   };
+  // the packed weights of step k (the instructions past the step's 14 KB load zeros)
   auto stage_w = [&](int k, int slot) {
-    const float* src = wom + (size_t)k * WK_F;
-    float* dst = smem + OFF_W + slot * WK_F;
+    float* dst = smem + OFF_W + slot * 4096;
 #pragma unroll
-    for (int j = 0; j < 16 / NW; ++j) {
+    for (int j = 0; j < WK_INS / NW; ++j) {
       const int i = wv + j * NW;
-      __builtin_amdgcn_global_load_lds(src + (i * 64 + lane) * 4, dst + i * 256, 16, 0, 0);
+      const unsigned voff = i < MT * 2 ? (unsigned)((k * WK_F + i * 256) * 4 + lane * 16) : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rwom, dst + i * 256, 16, voff, 0, 0, 0);
     }
   };
-  // phase 2 stage of deformable group dg: [row][channel half][col][4] tile + the group's B fragments
-  auto stage_group = [&](int dg, float* st) {
-    const int ty0 = oy0 - 1 - M, tx0 = ox0 - 1 - M;
-    const float* wc = wt + (size_t)dg * W_F;
-#pragma unroll
-    for (int j = 0; j < G_INS / NW; ++j) {
+  // phase-2 stage of group pair pa: the [row][channel quad][col][4] tile of channels 16 pa .. 16 pa + 15
+  // and the pair's B fragments (instructions 0..33 tile, 34..69 weights, 70..71 pad)
+  const int ty0 = oy0 - 1 - M, tx0 = ox0 - 1 - M;
+  auto stage_pair = [&](int pa, float* st, float* sw) {
+    const float* wc = wt + (size_t)pa * WP_F;
+#pragma unroll 1
+    for (int j = 0; j < P_INS / NW; ++j) {
       const int i = wv + j * NW;   // wave-uniform
-      if (i >= T_INST && i < T_INST + W_F / 256) {
-        __builtin_amdgcn_global_load_lds(wc + ((i - T_INST) * 64 + lane) * 4, st + i * 256, 16, 0, 0);
+      if (i >= T_INST && i < T_INST + WP_F / 256) {
+        __builtin_amdgcn_global_load_lds(wc + ((i - T_INST) * 64 + lane) * 4, sw + (i - T_INST) * 256, 16, 0, 0);
       } else {
         const int e = i * 64 + lane;
-        const int col = e % TP, rh = e / TP, h = rh & 1, row = rh >> 1;
+        const int col = e % TP, rq = e / TP, q = rq & 3, row = rq >> 2;
         const int y = ty0 + row, x = tx0 + col;
         const bool ok = (i < T_INST) & (e < T_EL) & ((unsigned)y < (unsigned)H) & ((unsigned)x < (unsigned)W);
-        const unsigned voff = ok ? (unsigned)((((size_t)y * W + x) * 64 + dg * 8 + h * 4) * 4) : 0x80000000u;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, st + i * 256, 16, voff, 0, 0, 0);
+        const unsigned voff = ok ? (unsigned)((((size_t)y * W + x) * 64 + pa * 16 + q * 4) * 4) : 0x80000000u;
+        float* dst = i < T_INST ? st + i * 256 : sw + (i - T_INST) * 256;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, dst, 16, voff, 0, 0, 0);
       }
     }
   };
 
-  f32x16 om[8];
+  // ---------------------------------------------------------------- phase 1: offset/mask conv
+  f32x16 om[MT];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) om[q] = f32x16{0};
+  for (int q = 0; q < MT; ++q) om[q] = f32x16{0};
 #if DCNSEP_EXP == 1   // timing probe: no phase 1 (offsets = biases)
   if (false)
 #endif
   {
-  stage_data(0, smem + OFF_D);
+  stage_data(0, smem + OFF_D0);
   stage_w(0, 0);
   stage_w(1, 1);
+  // chunk loop at run time, taps unrolled: tap offsets, ring slots ((9 c + t) % 3 = t % 3) and the waits
+  // are compile-time; the next tap's data fragment is read and split while this tap's MFMAs run, each
+  // M-tile's weight fragments one M-tile ahead (scheduling barriers pin that order: the compiler would
+  // sink each read next to its MFMAs and wait for it there)
+  f16x8 dh, dl;
 #pragma unroll 1
-  for (int k = 0; k < KSTEPS; ++k) {
-    // this step's weights (and, at a chunk start, its data) landed in every wave: the DMA issued in the
-    // last two steps may stay in flight
-    wait_vm((k + 1 < KSTEPS ? 2 : 0) + side_dma(k - 1) + side_dma(k - 2));
-    __syncthreads();
-    if (k + 2 < KSTEPS) stage_w(k + 2, (k + 2) % RING);
-    if (k % 9 == 1 && k / 9 < 3) stage_data(k / 9 + 1, smem + OFF_D + ((k / 9 + 1) & 1) * D_F);
-    if (k == DCN0_STEP) stage_group(0, smem + OFF_G0);
-    const int c = k / 9, t = k - 9 * c, ky = t / 3, kx = t - 3 * ky;
-    const float* db = smem + OFF_D + (c & 1) * D_F + ((wv + ky) * HC1 + l32 + kx) * PX_F + hf * 8;
-    f16x8 dh, dl;
-    split_f16x3(ld4(db), ld4(db + 4), dh, dl);
-    const float* wb = smem + OFF_W + (k % RING) * WK_F + lane * 4;
+  for (int c = 0; c < KSTEPS / 9; ++c) {
+    const float* dbuf = smem + ((c & 1) ? OFF_D1 : OFF_D0) + (wv * HC1 + l32) * PX_F + hf * 8;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const f16x8 wh = ldh8(wb + (2 * q) * 256), wl = ldh8(wb + (2 * q + 1) * 256);
-      om[q] = mfma16h(wh, dh, om[q]);
-      om[q] = mfma16h(wh, dl, om[q]);
-      om[q] = mfma16h(wl, dh, om[q]);
+    for (int t = 0; t < 9; ++t) {
+      const int k = 9 * c + t;
+      // this step's weights (and, at a chunk start, its data) landed in every wave; the DMA issued in the
+      // last two steps (weights of k + 1, the side stage of tap 1) may stay in flight
+      if (t == 2 || t == 3) wait_vm(c < 3 ? 2 + D_INS / NW : 2 + P_INS / NW);
+      else if (t == 8 && c == 3) wait_vm(0);
+      else wait_vm(2);
+      // a bare s_barrier: __syncthreads()'s workgroup fence would wait for vmcnt(0), i.e. for the DMA of
+      // the next two steps too.  Every LDS read of the step that frees a ring slot has returned (its
+      // MFMAs consumed it), and LDS-DMA visibility is the vmcnt wait above.
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      // the first weight fragments right after the barrier; this step's data fragment was read and split
+      // during the previous step (a chunk's first tap: read now), so the MFMAs start at once, and the
+      // next steps' LDS-DMA is issued behind the first M-tile's MFMAs
+      const float* wb = smem + OFF_W + (t % RING) * 4096 + lane * 4;
+      f16x8 wh[2], wl[2];
+      wh[0] = ldh8(wb);
+      wl[0] = ldh8(wb + 256);
+      if (t == 0) {
+        split_f16x3(ld4(dbuf), ld4(dbuf + 4), dh, dl);
+      }
+      f32x4 x0, x1;
+#pragma unroll
+      for (int q = 0; q < MT; ++q) {
+        if (q + 1 < MT) {
+          wh[(q + 1) & 1] = ldh8(wb + (2 * q + 2) * 256);
+          wl[(q + 1) & 1] = ldh8(wb + (2 * q + 3) * 256);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        om[q] = mfma16h(wh[q & 1], dh, om[q]);
+        om[q] = mfma16h(wh[q & 1], dl, om[q]);
+        om[q] = mfma16h(wl[q & 1], dh, om[q]);
+        if (q == 0) {
+          if (t < 7 || c < 3) stage_w(k + 2, (t + 2) % RING);
+          if (t == 1) {
+            if (c < 3) stage_data(c + 1, smem + (((c + 1) & 1) ? OFF_D1 : OFF_D0));
+            else stage_pair(0, smem + OFF_XT, smem + OFF_XW);   // D0 is free: chunk 2 is done
+          }
+        }
+        if (q == 1 && t < 8) {   // the next tap of the same chunk: its buffer is stable until the chunk ends
+          const float* nb = dbuf + (((t + 1) / 3) * HC1 + (t + 1) % 3) * PX_F;
+          x0 = ld4(nb);
+          x1 = ld4(nb + 4);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (t < 8) split_f16x3(x0, x1, dh, dl);   // the next step's B operand
     }
   }
   }
 #if DCNSEP_EXP == 1
-  stage_group(0, smem + OFF_G0);
+  stage_pair(0, smem + OFF_XT, smem + OFF_XW);
 #endif
-  // om[q][r] of lane (p, h): packed row (r & 3) + 8 (r >> 2) + 4 h of group q = component r % 3 (dy, dx,
-  // mask) of tap 2 (r / 3) + h (r < 15); bias, unscale, sigmoid(mask) (dcn_v2.py:134-138)
+  // slot s = 16 m + r of lane half h = component s % 3 (dy, dx, mask) of tap (s % 27) / 3 of group
+  // 2 (s / 27) + h, packed row (r & 3) + 8 (r >> 2) + 4 h of M-tile m; bias, unscale, sigmoid(mask)
+  // (dcn_v2.py:134-138)
   bool bad = false;
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
+  for (int m = 0; m < MT; ++m) {
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      const f32x4 bq = ld4(a.b_om[g] + q * 32 + 8 * v + 4 * hf);
+      const f32x4 bq = ld4(a.b_om[g] + m * 32 + 8 * v + 4 * hf);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int r = 4 * v + e;
-        if (r < 15) {
-          float x = om[q][r] * F16X3_UNSCALE + bq[e];
+        const int s = 16 * m + 4 * v + e;
+        if (s < 108) {
+          float x = om[m][4 * v + e] * F16X3_UNSCALE + bq[e];
           bad |= not_finite(x);
-          if (r % 3 == 2) x = sigmoid_fast(x);
-          om[q][r] = x;
+          if (s % 3 == 2) x = sigmoid_fast(x);
+          om[m][4 * v + e] = x;
         }
       }
     }
@@ -211,14 +251,14 @@ __global__ __launch_bounds__(64 * NW) void k_dcn_sep(stif_dcn_sep_args a) {
   report_range(a.status, bad);
 
   // ---------------------------------------------------------------- phase 2: deformable conv
-  const int ty0 = oy0 - 1 - M, tx0 = ox0 - 1 - M;
-  // bilinear sample of the group's 8 channels (a0: 0-3, a1: 4-7) at tap `tap` with offset (dy, dx) and
-  // modulation m folded into the corner weights; `> -1` / `< H` gate; global fallback outside the tile
-  auto sample = [&](const float* st, int dg, int tap, float dy, float dx, float mk, f32x4& a0, f32x4& a1) {
+  // bilinear sample of this lane half's group (channels 16 pa + 8 h .. + 7: a0 = quad 2h, a1 = quad 2h + 1)
+  // at tap `tap` with offset (dy, dx) and modulation m folded into the corner weights; `> -1` / `< H`
+  // gate; global fallback outside the tile
+  auto sample = [&](const float* st, int pa, int tap, float dy, float dx, float mk, f32x4& a0, f32x4& a1) {
     const int ky = tap / 3, kx = tap - 3 * ky;
     const float h_im = (float)(oy - 1 + ky) + dy;
     const float w_im = (float)(ox - 1 + kx) + dx;
-    const bool valid = pix_ok & (tap < 9) & (h_im > -1.f) & (w_im > -1.f) & (h_im < (float)H) & (w_im < (float)W);
+    const bool valid = pix_ok & (h_im > -1.f) & (w_im > -1.f) & (h_im < (float)H) & (w_im < (float)W);
     const float fh = floorf(h_im), fw = floorf(w_im);
     const float lh = h_im - fh, lw = w_im - fw, hh = 1.f - lh, hw = 1.f - lw;
     const int h_low = (int)fh, w_low = (int)fw;
@@ -227,8 +267,8 @@ __global__ __launch_bounds__(64 * NW) void k_dcn_sep(stif_dcn_sep_args a) {
     const float m = valid ? mk : 0.f;
     const float hm = hh * m, lm = lh * m;
     const float w1 = hm * hw, w2 = hm * lw, w3 = lm * hw, w4 = lm * lw;
-    const float* p0 = st + (((in_tile ? r0 : 0) * 2) * TP + (in_tile ? c0 : 0)) * 4;
-    const float* p1 = p0 + 2 * TP * 4;
+    const float* p0 = st + (((in_tile ? r0 : 0) * 4 + 2 * hf) * TP + (in_tile ? c0 : 0)) * 4;
+    const float* p1 = p0 + 4 * TP * 4;   // next row
     a0 = w1 * ld4(p0) + w2 * ld4(p0 + 4) + w3 * ld4(p1) + w4 * ld4(p1 + 4);
     a1 = w1 * ld4(p0 + TP * 4) + w2 * ld4(p0 + TP * 4 + 4) + w3 * ld4(p1 + TP * 4) + w4 * ld4(p1 + TP * 4 + 4);
 #if DCNSEP_EXP == 4   // timing probe: no global fallback outside the staged tile
@@ -238,7 +278,7 @@ __global__ __launch_bounds__(64 * NW) void k_dcn_sep(stif_dcn_sep_args a) {
 #endif
     if (__builtin_amdgcn_ballot_w64(fb)) {
       if (fb) {
-        const int h_high = h_low + 1, w_high = w_low + 1, co = dg * 8;
+        const int h_high = h_low + 1, w_high = w_low + 1, co = pa * 16 + hf * 8;
         const bool b1 = h_low >= 0 && w_low >= 0, b2 = h_low >= 0 && w_high <= W - 1;
         const bool b3 = h_high <= H - 1 && w_low >= 0, b4 = h_high <= H - 1 && w_high <= W - 1;
         const float* q1 = in + ((size_t)h_low * W + w_low) * 64 + co;
@@ -254,22 +294,27 @@ __global__ __launch_bounds__(64 * NW) void k_dcn_sep(stif_dcn_sep_args a) {
   };
 
   f32x16 acc0 = f32x16{0}, acc1 = f32x16{0};
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // group 0 staged (and the om biases loaded)
-  __syncthreads();                                    // phase-1 buffers free for group 1
-  auto dcn_group = [&](int dg, const f32x16& o) {
-#if DCNSEP_EXP == 3   // timing probe: no phase 2 work
-    return;
-#endif
-    if (dg + 1 < 8) stage_group(dg + 1, smem + (((dg + 1) & 1) ? OFF_G1 : OFF_G0));
-    const float* st = smem + ((dg & 1) ? OFF_G1 : OFF_G0);
-    const float* sw = st + T_F;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // pair 0 staged (and the om biases loaded)
+  __syncthreads();                                    // phase-1 buffers free
 #pragma unroll
-    for (int pp = 0; pp < 5; ++pp) {
+  for (int pa = 0; pa < 4; ++pa) {
+#if DCNSEP_EXP == 3   // timing probe: no phase 2 work
+    break;
+#endif
+    if (pa + 1 < 4) {
+      if ((pa + 1) & 1) stage_pair(pa + 1, smem + OFF_YT, smem + OFF_YW);
+      else stage_pair(pa + 1, smem + OFF_XT, smem + OFF_XW);
+    }
+    const float* st = smem + ((pa & 1) ? OFF_YT : OFF_XT);
+    const float* sw = smem + ((pa & 1) ? OFF_YW : OFF_XW);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int s = 27 * pa + 3 * t;   // this lane half's group 2 pa + h, tap t: slots s .. s + 2
       f32x4 a0, a1;
-      sample(st, dg, 2 * pp + hf, o[3 * pp], o[3 * pp + 1], o[3 * pp + 2], a0, a1);
+      sample(st, pa, t, om[s / 16][s % 16], om[(s + 1) / 16][(s + 1) % 16], om[(s + 2) / 16][(s + 2) % 16], a0, a1);
       f16x8 ah, al;
       split_f16x3(a0, a1, ah, al);
-      const float* wp = sw + pp * 1024 + lane * 4;   // [pair][nt][plane][lane][8 halves]
+      const float* wp = sw + t * 1024 + lane * 4;   // [tap][nt][plane][lane][8 halves]
       const f16x8 bh0 = ldh8(wp), bl0 = ldh8(wp + 256), bh1 = ldh8(wp + 512), bl1 = ldh8(wp + 768);
       acc0 = mfma16h(ah, bh0, acc0);
       acc1 = mfma16h(ah, bh1, acc1);
@@ -277,25 +322,14 @@ __global__ __launch_bounds__(64 * NW) void k_dcn_sep(stif_dcn_sep_args a) {
       acc1 = mfma16h(ah, bl1, acc1);
       acc0 = mfma16h(al, bh0, acc0);
       acc1 = mfma16h(al, bh1, acc1);
+      __builtin_amdgcn_sched_barrier(0);   // one tap's operands live at a time (VGPR budget)
     }
     lds_dma_barrier();
-  };
-#if DCNSEP_ROLL
-  // one loop body (smaller code): the next group's offsets rotate into om[0]
-#pragma unroll 1
-  for (int dg = 0; dg < 8; ++dg) {
-    dcn_group(dg, om[0]);
-#pragma unroll
-    for (int q = 0; q < 7; ++q) om[q] = om[q + 1];
   }
-#else
-#pragma unroll
-  for (int dg = 0; dg < 8; ++dg) dcn_group(dg, om[dg]);
-#endif
   // epilogue through a per-wave LDS block -> coalesced 16-B stores (k_dcn's)
   float* out = a.out[g] + (size_t)n * a.out_item;
   const float* bias = a.bias[g];
-  float* blk = smem + OFF_W + wv * 1024;
+  float* blk = smem + OFF_D0 + wv * 1024;
   const int rpx = lane >> 3, c4 = lane & 7;
   bool bad2 = false;
 #pragma unroll

@@ -101,7 +101,8 @@ std::vector<float> omega(const float* src, size_t n, bool rev) {
 
 extern "C" size_t stif_conv_weight_floats(int cout, int cin, int ks, int mode) {
   // DCNSEP | F16X3 (the fused DCN_sep's offset/mask conv): 36 steps x 8 groups x 2 planes x 1 KB
-  if (mode == (STIF_PACK_DCNSEP | STIF_PACK_F16X3)) return (size_t)36 * 8 * 2 * 256;
+  if (mode == (STIF_PACK_DCNSEP | STIF_PACK_F16X3)) return (size_t)36 * 7 * 2 * 256;
+  if (mode == (STIF_PACK_DCNPAIR | STIF_PACK_F16X3)) return (size_t)4 * 9 * 2 * 2 * 256;
   // PLAIN | F16X3 (the DCN core, 64 -> 64 3x3): 5 tap pairs x 2 nt x 2 planes x 1 KB per 8-channel group
   if (mode == (STIF_PACK_PLAIN | STIF_PACK_F16X3) && ks == 3) return (size_t)(cin / 8) * 5 * 2 * 2 * 256;
   // PLAIN | F16X3 1x1 (k_conv1x1): 2 nt x 2 planes x 1 KB per (64-cout slice, 16-channel chunk)
@@ -114,6 +115,7 @@ extern "C" size_t stif_conv_weight_floats(int cout, int cin, int ks, int mode) {
 
 extern "C" size_t stif_conv_bias_floats(int cout, int mode) {
   if (mode == (STIF_PACK_DCNSEP | STIF_PACK_F16X3)) return 256;
+  if (mode == (STIF_PACK_DCNPAIR | STIF_PACK_F16X3)) return 64;
   mode &= ~STIF_PACK_F16X3;
   return (mode == STIF_PACK_WINO || mode == STIF_PACK_WINO_OFFMASK || mode == STIF_PACK_WINO_LSTM)
              ? (size_t)round64(cout)
@@ -253,16 +255,17 @@ int pack_1x1_f16x3(const float* w, const float* b, int cout, int cin, float* w_d
   return STIF_OK;
 }
 // DCNSEP | F16X3: conv_offset_mask (216 x 64 x 3 x 3) as the A operands of k_dcn_sep's phase 1,
-// [k = 9 c + tap][group][plane][lane][8 halves]; packed row i of a group's 32-row block is component
-// r % 3 of tap 2 (r / 3) + ((i >> 2) & 1), r = (i & 3) + 4 (i >> 3) -- the MFMA accumulator register r
-// of lane half (i >> 2) & 1 -- with the reference channel of (group q, tap k): offset dy q*18 + 2k,
-// dx q*18 + 2k + 1, mask 144 + q*9 + k (dcn_v2.py:134-138, dcn_v2_im2col_cuda.cu:160-167)
-int dcnsep_src_row(int q, int i) {
-  const int hh = (i >> 2) & 1, r = (i & 3) + 4 * (i >> 3);
-  if (r >= 15) return -1;
-  const int tap = 2 * (r / 3) + hh, comp = r % 3;
-  if (tap > 8) return -1;
-  return comp == 0 ? q * 18 + 2 * tap : (comp == 1 ? q * 18 + 2 * tap + 1 : 144 + q * 9 + tap);
+// [k = 9 c + tap][M-tile m 7][plane][lane][8 halves].  Row i of M-tile m lands in accumulator register
+// r = (i & 3) + 4 (i >> 3) of lane half h = (i >> 2) & 1; lane half h owns the deformable groups
+// h, h + 2, h + 4, h + 6 (the groups it samples in phase 2) and its slot s = 16 m + r holds value
+// v = 27 a + 3 tap + comp of group 2 a + h (slots 108..111 zero): the reference channel of (group g,
+// tap k) is offset dy g*18 + 2k, dx g*18 + 2k + 1, mask 144 + g*9 + k (dcn_v2.py:134-138,
+// dcn_v2_im2col_cuda.cu:160-167).  216 rows in 7 M-tiles (224).
+int dcnsep_src_row(int m, int i) {
+  const int hh = (i >> 2) & 1, r = (i & 3) + 4 * (i >> 3), v = 16 * m + r;
+  if (v >= 108) return -1;
+  const int g = 2 * (v / 27) + hh, tap = (v % 27) / 3, comp = v % 3;
+  return comp == 0 ? g * 18 + 2 * tap : (comp == 1 ? g * 18 + 2 * tap + 1 : 144 + g * 9 + tap);
 }
 int pack_dcnsep_f16x3(const float* w, const float* b, int cout, int cin, int ks, float* w_dst, float* b_dst) {
   if (cout != 216 || cin != 64 || ks != 3)
@@ -271,22 +274,44 @@ int pack_dcnsep_f16x3(const float* w, const float* b, int cout, int cin, int ks,
     if (!f16x3_ok(w[i])) return range_fail("stif_pack_conv_weight: a weight is outside the f16x3 range (|w| < 64); pack it without STIF_PACK_F16X3");
   _Float16* dst = reinterpret_cast<_Float16*>(w_dst);
   for (int k = 0; k < 36; ++k)
-    for (int q = 0; q < 8; ++q)
+    for (int m = 0; m < 7; ++m)
       for (int l = 0; l < 64; ++l) {
-        const int src = dcnsep_src_row(q, l & 31), c = k / 9, t = k % 9;
+        const int src = dcnsep_src_row(m, l & 31), c = k / 9, t = k % 9;
         for (int e = 0; e < 8; ++e) {
           const int ci = 16 * c + 8 * (l >> 5) + e;
           const double x = src >= 0 ? (double)w[((size_t)src * cin + ci) * 9 + t] : 0.0;
-          const size_t o = (((size_t)k * 8 + q) * 2) * 512 + l * 8 + e;
+          const size_t o = (((size_t)k * 7 + m) * 2) * 512 + l * 8 + e;
           split_f16x3_host(x, dst + o, dst + o + 512);
         }
       }
   if (b_dst)
-    for (int q = 0; q < 8; ++q)
+    for (int m = 0; m < 8; ++m)
       for (int i = 0; i < 32; ++i) {
-        const int src = dcnsep_src_row(q, i);
-        b_dst[q * 32 + i] = (src >= 0 && b) ? b[src] : 0.f;
+        const int src = m < 7 ? dcnsep_src_row(m, i) : -1;
+        b_dst[m * 32 + i] = (src >= 0 && b) ? b[src] : 0.f;
       }
+  return STIF_OK;
+}
+// DCNPAIR | F16X3: the DCN weight (64 x 64 x 3 x 3) for k_dcn_sep's phase 2, which contracts two
+// deformable groups per K step: [group pair a 4][tap 9][nt 2][plane][lane][8 halves], element e of lane l
+// holding input channel 8 (2 a + (l >> 5)) + e at `tap`, cout nt * 32 + (l & 31)
+int pack_dcnpair_f16x3(const float* w, const float* b, int cout, int cin, int ks, float* w_dst, float* b_dst) {
+  if (cout != 64 || cin != 64 || ks != 3)
+    return stif_fail(STIF_E_INVALID, "STIF_PACK_DCNPAIR packing needs a 64 -> 64 3x3 weight");
+  for (size_t i = 0; i < (size_t)cout * cin * 9; ++i)
+    if (!f16x3_ok(w[i])) return range_fail("stif_pack_conv_weight: a weight is outside the f16x3 range (|w| < 64); pack it without STIF_PACK_F16X3");
+  _Float16* dst = reinterpret_cast<_Float16*>(w_dst);
+  for (int a = 0; a < 4; ++a)
+    for (int t = 0; t < 9; ++t)
+      for (int nt = 0; nt < 2; ++nt)
+        for (int l = 0; l < 64; ++l)
+          for (int e = 0; e < 8; ++e) {
+            const int ci = 8 * (2 * a + (l >> 5)) + e, co = nt * 32 + (l & 31);
+            const size_t o = ((((size_t)a * 9 + t) * 2 + nt) * 2) * 512 + l * 8 + e;
+            split_f16x3_host((double)w[((size_t)co * cin + ci) * 9 + t], dst + o, dst + o + 512);
+          }
+  if (b_dst)
+    for (int j = 0; j < cout; ++j) b_dst[j] = b ? b[j] : 0.f;
   return STIF_OK;
 }
 }  // namespace
@@ -300,6 +325,10 @@ extern "C" int stif_pack_conv_weight(const float* w, const float* b, int cout, i
   if (mode == STIF_PACK_DCNSEP) {
     if (!f16x3) return stif_fail(STIF_E_INVALID, "STIF_PACK_DCNSEP exists for split-fp16 operands only (| STIF_PACK_F16X3)");
     return pack_dcnsep_f16x3(w, b, cout, cin, ks, w_dst, b_dst);
+  }
+  if (mode == STIF_PACK_DCNPAIR) {
+    if (!f16x3) return stif_fail(STIF_E_INVALID, "STIF_PACK_DCNPAIR exists for split-fp16 operands only (| STIF_PACK_F16X3)");
+    return pack_dcnpair_f16x3(w, b, cout, cin, ks, w_dst, b_dst);
   }
   if ((mode == STIF_PACK_OFFMASK || mode == STIF_PACK_WINO_OFFMASK) && cout != 216)
     return stif_fail(STIF_E_INVALID, "offmask pack needs cout=216");

@@ -213,17 +213,21 @@ class LunaTokis(nn.Module):
                 for ln, cin, _ in W._PCD_LAYERS:
                     n = f"{prefix}{ln}_{d}"
                     if cin is None:
-                        conv(n, L.PACK_PLAIN | f16)     # the DCN core (k_dcn)
                         om = n + ".conv_offset_mask"
                         if f16 and self.fused_dcn:
                             # the fused DCN_sep kernel (k_dcn_sep); out of the split range -> the two-kernel path
                             try:
-                                put(om, ops.pack_conv(h[om + ".weight"], h[om + ".bias"],
-                                                      L.PACK_DCNSEP | L.PACK_F16X3, dev, range_fallback=False))
+                                pom = ops.pack_conv(h[om + ".weight"], h[om + ".bias"], L.PACK_DCNSEP | L.PACK_F16X3,
+                                                    dev, range_fallback=False)
+                                pcore = ops.pack_conv(h[n + ".weight"], h[n + ".bias"], L.PACK_DCNPAIR | L.PACK_F16X3,
+                                                      dev, range_fallback=False)
+                                put(n, pcore)
+                                put(om, pom)
                                 continue
                             except L.StifError as e:
                                 if e.code != L.E_RANGE:
                                     raise
+                        conv(n, L.PACK_PLAIN | f16)     # the DCN core (k_dcn)
                         conv(om, (L.PACK_WINO_OFFMASK | f16) if self.winograd else L.PACK_OFFMASK)
                     else:
                         conv(n, wino)

@@ -216,13 +216,13 @@ def dcn(groups, *, epi=L.EPI_NONE, status=None):
 
 def dcn_sep_fusable(om_layer: PackedConv, layer: PackedConv) -> bool:
     """Both layers of a DCN_sep packed for the fused kernel (stif_dcn_sep_nhwc)."""
-    return om_layer.mode == (L.PACK_DCNSEP | L.PACK_F16X3) and layer.mode == (L.PACK_PLAIN | L.PACK_F16X3)
+    return om_layer.mode == (L.PACK_DCNSEP | L.PACK_F16X3) and layer.mode == (L.PACK_DCNPAIR | L.PACK_F16X3)
 
 
 def dcn_sep(groups, *, epi=L.EPI_NONE, status=None):
     """Fused DCN_sep (dcn_v2.py:127-140): offset/mask conv + sigmoid + deformable conv in one launch.
     groups: list of {om_layer: PackedConv (STIF_PACK_DCNSEP | F16X3), layer: PackedConv (64->64 3x3,
-    PLAIN | F16X3), fea, inp, out} with NHWC [nitems, H, W, 64] tensors."""
+    STIF_PACK_DCNPAIR | F16X3), fea, inp, out} with NHWC [nitems, H, W, 64] tensors."""
     if not 1 <= len(groups) <= L.MAXG:
         raise ValueError("dcn_sep: 1..8 groups")
     g0 = groups[0]

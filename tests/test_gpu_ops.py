@@ -453,7 +453,7 @@ def _dcnsep_weights(seed, oscale, boundary=False, H=0):
 def _dcnsep_layers(ops, L, sdx):
     om = ops.pack_conv(sdx["x.conv_offset_mask.weight"], sdx["x.conv_offset_mask.bias"], L.PACK_DCNSEP | L.PACK_F16X3,
                        range_fallback=False)
-    core = ops.pack_conv(sdx["x.weight"], sdx["x.bias"], L.PACK_PLAIN | L.PACK_F16X3)
+    core = ops.pack_conv(sdx["x.weight"], sdx["x.bias"], L.PACK_DCNPAIR | L.PACK_F16X3, range_fallback=False)
     return om, core
 
 
@@ -515,6 +515,7 @@ def test_dcn_sep_fused_equals_two_kernel_path(ops, L):
     omap = torch.empty(2, H, W, 216, device="cuda")
     ops.conv2d([dict(layer=omw, in0=nhwc(fea), out=omap)], epi=L.EPI_OFFMASK)
     b = torch.empty(2, H, W, 64, device="cuda")
-    ops.dcn([dict(layer=core, inp=nhwc(x), offmask=omap, out=b)])
+    core2 = ops.pack_conv(sdx["x.weight"], sdx["x.bias"], L.PACK_PLAIN | L.PACK_F16X3)
+    ops.dcn([dict(layer=core2, inp=nhwc(x), offmask=omap, out=b)])
     ref = O.dcn_sep(x, fea, sdx, "x")
     assert relmax(to_nchw(a), ref) < RTOL and relmax(to_nchw(b), ref) < RTOL

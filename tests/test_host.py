@@ -224,10 +224,12 @@ def test_pack_wino_f16x3_layout(stif):
 
 
 def test_pack_dcnsep_layout(stif):
-    """STIF_PACK_DCNSEP | F16X3 (the fused DCN_sep's offset/mask conv, include/stif.h): packed row i of a
-    group's 32-row block = component r % 3 of tap 2 (r / 3) + ((i >> 2) & 1), r = (i & 3) + 4 (i >> 3),
-    which is the MFMA accumulator register r of the lane half that samples that tap; the f16 h + l
-    planes carry the weight to ~22 bits; the bias follows the rows; rows 15 / tap 9 are zero."""
+    """STIF_PACK_DCNSEP | F16X3 (the fused DCN_sep's offset/mask conv, include/stif.h): 7 M-tiles; row i of
+    M-tile m is accumulator register r = (i & 3) + 4 (i >> 3) of lane half h = (i >> 2) & 1, whose slot
+    s = 16 m + r < 108 holds component s % 3 of tap (s % 27) / 3 of group 2 (s / 27) + h -- the groups that
+    lane half samples; the f16 h + l planes carry the weight to ~22 bits; the bias follows the rows.
+    STIF_PACK_DCNPAIR | F16X3 (its DCN weight): [pair][tap][nt][plane][lane][8], input channel
+    8 (2 pair + (lane >> 5)) + e."""
     L = stif._lib
     lib = L.lib()
     rng = np.random.default_rng(0)
@@ -238,27 +240,44 @@ def test_pack_dcnsep_layout(stif):
     bd = np.empty(lib.stif_conv_bias_floats(216, mode), np.float32)
     L.check(lib.stif_pack_conv_weight(w.ctypes.data, b.ctypes.data, 216, 64, 3, mode, wd.ctypes.data,
                                       bd.ctypes.data), "pack")
-    h = wd.view(np.float16).reshape(36, 8, 2, 64, 8).astype(np.float64)
-    val = (h[:, :, 0] + h[:, :, 1]) / 1024.0                    # [k][group][lane][e]
+    h = wd.view(np.float16).reshape(36, 7, 2, 64, 8).astype(np.float64)
+    val = (h[:, :, 0] + h[:, :, 1]) / 1024.0                    # [k][M-tile][lane][e]
     seen = set()
-    for q in range(8):
+    for m in range(7):
         for i in range(32):
             hh, r = (i >> 2) & 1, (i & 3) + 4 * (i >> 3)
-            tap = 2 * (r // 3) + hh
-            if r >= 15 or tap > 8:
-                assert bd[q * 32 + i] == 0 and not val[:, q, i].any() and not val[:, q, i + 32].any()
+            s_ = 16 * m + r
+            if s_ >= 108:
+                assert bd[m * 32 + i] == 0 and not val[:, m, i].any() and not val[:, m, i + 32].any()
                 continue
-            comp = r % 3
-            src = (q * 18 + 2 * tap + comp) if comp < 2 else 144 + q * 9 + tap
+            g, tap, comp = 2 * (s_ // 27) + hh, (s_ % 27) // 3, s_ % 3
+            src = (g * 18 + 2 * tap + comp) if comp < 2 else 144 + g * 9 + tap
             seen.add(src)
-            assert bd[q * 32 + i] == b[src]
+            assert bd[m * 32 + i] == b[src]
             for k in range(36):
                 c, t = divmod(k, 9)
                 for lane in (i, i + 32):
                     ci = 16 * c + 8 * (lane >> 5) + np.arange(8)
-                    assert np.abs(val[k, q, lane] - w[src, ci, t // 3, t % 3]).max() <= 2e-7 * np.abs(w).max()
+                    assert np.abs(val[k, m, lane] - w[src, ci, t // 3, t % 3]).max() <= 2e-7 * np.abs(w).max()
     assert seen == set(range(216))
-    # the mode exists for split-fp16 operands only
-    with pytest.raises(L.StifError):
-        L.check(lib.stif_pack_conv_weight(w.ctypes.data, b.ctypes.data, 216, 64, 3, L.PACK_DCNSEP, wd.ctypes.data,
-                                          bd.ctypes.data), "pack")
+    # the DCN weight for the fused kernel: two deformable groups per K step
+    wc = (rng.standard_normal((64, 64, 3, 3)) * 0.1).astype(np.float32)
+    mode2 = L.PACK_DCNPAIR | L.PACK_F16X3
+    wd2 = np.empty(lib.stif_conv_weight_floats(64, 64, 3, mode2), np.float32)
+    bd2 = np.empty(lib.stif_conv_bias_floats(64, mode2), np.float32)
+    L.check(lib.stif_pack_conv_weight(wc.ctypes.data, b.ctypes.data, 64, 64, 3, mode2, wd2.ctypes.data,
+                                      bd2.ctypes.data), "pack")
+    h2 = wd2.view(np.float16).reshape(4, 9, 2, 2, 64, 8).astype(np.float64)
+    v2 = (h2[:, :, :, 0] + h2[:, :, :, 1]) / 1024.0             # [pair][tap][nt][lane][e]
+    for pa in range(4):
+        for t in range(9):
+            for nt in range(2):
+                for lane in (0, 5, 31, 32, 47, 63):
+                    ci = 8 * (2 * pa + (lane >> 5)) + np.arange(8)
+                    assert np.abs(v2[pa, t, nt, lane] - wc[nt * 32 + (lane & 31), ci, t // 3, t % 3]).max() <= 2e-7 * np.abs(wc).max()
+    assert (bd2 == b[:64]).all()
+    # both modes exist for split-fp16 operands only
+    for md in (L.PACK_DCNSEP, L.PACK_DCNPAIR):
+        with pytest.raises(L.StifError):
+            L.check(lib.stif_pack_conv_weight(w.ctypes.data, b.ctypes.data, 216 if md == L.PACK_DCNSEP else 64, 64, 3,
+                                              md, wd.ctypes.data, bd.ctypes.data), "pack")
