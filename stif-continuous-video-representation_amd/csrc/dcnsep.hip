@@ -32,39 +32,45 @@
 
 namespace {
 
-constexpr int NW = 8;                         // waves = output rows per tile
+#ifndef DCNSEP_NW
+#define DCNSEP_NW 4
+#endif
+// NW = 4: 4 output rows per tile, two 80-KB workgroups per CU -- one's MFMA-dense phase 1 runs beside the
+// other's sampling-bound phase 2; NW = 8: one 152-KB workgroup per CU with the next phase staged ahead
+constexpr int NW = DCNSEP_NW;                 // waves = output rows per tile
 constexpr int TW = 32;                        // output columns per tile
 // phase 1
 constexpr int MT = 7;                         // offset/mask M-tiles (224 rows >= 216)
-constexpr int HC1 = TW + 2;                   // halo columns (10 halo rows)
+constexpr int HC1 = TW + 2;                   // halo columns (NW + 2 halo rows)
 constexpr int PX_F = 20;                      // floats per staged halo pixel: 16 channels + 4 pad
-constexpr int D_SLOTS = (NW + 2) * HC1 * 5;   // 16-B slots per data chunk (1700)
-constexpr int D_INS = 32;                     // DMA instructions per data chunk (4 per wave; 27 carry data)
+constexpr int D_SLOTS = (NW + 2) * HC1 * 5;   // 16-B slots per data chunk
+constexpr int D_INS = NW == 8 ? 32 : 16;      // DMA instructions per data chunk (the last ones partly pad)
 constexpr int D_F = D_INS * 256;              // floats per data buffer
 constexpr int KSTEPS = 36;                    // k = 9 c + t: 16-channel chunk c, tap t
 constexpr int WK_F = MT * 2 * 256;            // packed weights of one step: [M-tile][plane][lane][8 halves]
-constexpr int WK_INS = 16;                    // DMA instructions per step (2 per wave; 14 carry data)
+constexpr int WK_INS = 16;                    // DMA instructions per step (14 carry data)
 constexpr int RING = 3;
 // phase 2
 constexpr int M = 2;                          // staged margin around the 3x3 footprint
 constexpr int TR = NW + 2 + 2 * M, TC = TW + 2 + 2 * M, TP = TC;
 constexpr int T_EL = TR * 4 * TP;             // 16-B elements of the staged tile: [row][channel quad][col]
-constexpr int T_INST = (T_EL + 63) / 64;      // 34
+constexpr int T_INST = (T_EL + 63) / 64;      // 34 (NW 8), 24 (NW 4)
 constexpr int WP_F = 9 * 2 * 2 * 256;         // packed B fragments of one group pair (36 KB)
-constexpr int P_INS = 72;                     // DMA instructions per pair stage (34 tile + 36 weights + 2 pad)
-static_assert(T_INST + WP_F / 256 <= P_INS && P_INS % NW == 0 && D_INS % NW == 0 && WK_INS % NW == 0,
-              "stage sizes");
+constexpr int P_INS = ((T_INST + WP_F / 256 + NW - 1) / NW) * NW;   // pair stage (tile + weights + pad)
+constexpr bool PAIR_AHEAD = NW == 8;          // phase 2 double-buffered (pair 0 staged during phase 1)
+static_assert(P_INS % NW == 0 && D_INS % NW == 0 && WK_INS % NW == 0, "stage sizes");
 static_assert(D_SLOTS <= D_INS * 64 && MT * 2 <= WK_INS, "phase-1 stages");
-// LDS map (floats).  Phase 1: data chunks D0, D1 and the weight ring; the stage of group pair 0 (tile X,
-// weights XW) lands in D0 (free once chunk 2 is done) and above the ring.  Phase 2: pairs alternate
-// between X and Y (tile Y over D1, weights YW over the ring); the epilogue blocks reuse D0.
+// LDS map (floats).  NW 8 -- phase 1: data chunks D0, D1 and the weight ring; the stage of group pair 0
+// (tile X, weights XW) lands in D0 (free once chunk 2 is done) and above the ring; phase 2: pairs
+// alternate between X and Y (tile Y over D1, weights YW over the ring).  NW 4 -- phase 1: D0, D1, ring
+// (80 KB); phase 2: one pair buffer X over them.  The epilogue blocks reuse D0.
 constexpr int PW_PAD_F = (P_INS - T_INST) * 256;    // pair weight region incl. the pad instructions
-constexpr int OFF_D0 = 0, OFF_D1 = T_INST * 256, OFF_W = OFF_D1 + D_F;
-constexpr int OFF_XT = 0, OFF_XW = OFF_W + RING * 4096;
+constexpr int OFF_D0 = 0, OFF_D1 = PAIR_AHEAD ? T_INST * 256 : D_F, OFF_W = OFF_D1 + D_F;
+constexpr int OFF_XT = 0, OFF_XW = PAIR_AHEAD ? OFF_W + RING * 4096 : T_INST * 256;
 constexpr int OFF_YT = T_INST * 256, OFF_YW = OFF_YT + T_INST * 256;
-constexpr int LDS_F = OFF_XW + PW_PAD_F;
-static_assert(D_F <= OFF_D1 && OFF_YW + PW_PAD_F <= OFF_XW && WK_F <= 4096 &&
-              NW * 1024 <= D_F && LDS_F * 4 <= 160 * 1024, "LDS map");
+constexpr int LDS_F = PAIR_AHEAD ? OFF_XW + PW_PAD_F : OFF_W + RING * 4096;
+static_assert(D_F <= OFF_D1 && WK_F <= 4096 && NW * 1024 <= D_F && LDS_F * 4 <= (NW == 8 ? 160 : 80) * 1024 &&
+              (PAIR_AHEAD ? OFF_YW + PW_PAD_F <= OFF_XW : OFF_XW + PW_PAD_F <= LDS_F), "LDS map");
 #ifndef DCNSEP_EXP
 #define DCNSEP_EXP 0    // timing probes (wrong results): 1 no phase 1, 3 no phase 2, 4 no fallback loads
 #endif
@@ -74,6 +80,8 @@ STIF_DEV void wait_vm(int n) {
   switch (n) {
     case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
     case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
     case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
     case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
@@ -81,7 +89,7 @@ STIF_DEV void wait_vm(int n) {
 }
 
 template <int EPI>
-__global__ __launch_bounds__(64 * NW) void k_dcn_sep(stif_dcn_sep_args a) {
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) void k_dcn_sep(stif_dcn_sep_args a) {
   __shared__ __attribute__((aligned(16))) float smem[LDS_F];
   const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, hf = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -176,9 +184,10 @@ __global__ __launch_bounds__(64 * NW) void k_dcn_sep(stif_dcn_sep_args a) {
       const int k = 9 * c + t;
       // this step's weights (and, at a chunk start, its data) landed in every wave; the DMA issued in the
       // last two steps (weights of k + 1, the side stage of tap 1) may stay in flight
-      if (t == 2 || t == 3) wait_vm(c < 3 ? 2 + D_INS / NW : 2 + P_INS / NW);
+      constexpr int WQ = WK_INS / NW;   // weight DMA instructions per wave and step
+      if (t == 2 || t == 3) wait_vm(c < 3 ? WQ + D_INS / NW : (PAIR_AHEAD ? WQ + P_INS / NW : WQ));
       else if (t == 8 && c == 3) wait_vm(0);
-      else wait_vm(2);
+      else wait_vm(WQ);
       // a bare s_barrier: __syncthreads()'s workgroup fence would wait for vmcnt(0), i.e. for the DMA of
       // the next two steps too.  Every LDS read of the step that frees a ring slot has returned (its
       // MFMAs consumed it), and LDS-DMA visibility is the vmcnt wait above.
@@ -210,7 +219,7 @@ __global__ __launch_bounds__(64 * NW) void k_dcn_sep(stif_dcn_sep_args a) {
           if (t < 7 || c < 3) stage_w(k + 2, (t + 2) % RING);
           if (t == 1) {
             if (c < 3) stage_data(c + 1, smem + (((c + 1) & 1) ? OFF_D1 : OFF_D0));
-            else stage_pair(0, smem + OFF_XT, smem + OFF_XW);   // D0 is free: chunk 2 is done
+            else if (PAIR_AHEAD) stage_pair(0, smem + OFF_XT, smem + OFF_XW);   // D0 is free: chunk 2 is done
           }
         }
         if (q == 1 && t < 8) {   // the next tap of the same chunk: its buffer is stable until the chunk ends
@@ -225,7 +234,7 @@ __global__ __launch_bounds__(64 * NW) void k_dcn_sep(stif_dcn_sep_args a) {
   }
   }
 #if DCNSEP_EXP == 1
-  stage_pair(0, smem + OFF_XT, smem + OFF_XW);
+  if (PAIR_AHEAD) stage_pair(0, smem + OFF_XT, smem + OFF_XW);
 #endif
   // slot s = 16 m + r of lane half h = component s % 3 (dy, dx, mask) of tap (s % 27) / 3 of group
   // 2 (s / 27) + h, packed row (r & 3) + 8 (r >> 2) + 4 h of M-tile m; bias, unscale, sigmoid(mask)
@@ -254,31 +263,53 @@ __global__ __launch_bounds__(64 * NW) void k_dcn_sep(stif_dcn_sep_args a) {
   // bilinear sample of this lane half's group (channels 16 pa + 8 h .. + 7: a0 = quad 2h, a1 = quad 2h + 1)
   // at tap `tap` with offset (dy, dx) and modulation m folded into the corner weights; `> -1` / `< H`
   // gate; global fallback outside the tile
-  auto sample = [&](const float* st, int pa, int tap, float dy, float dx, float mk, f32x4& a0, f32x4& a1) {
+  // split in two so that tap t + 1's eight corner reads are in flight while tap t blends and multiplies:
+  // prep() = coordinates, corner weights and the LDS reads; finish() = the blend (and the fallback)
+  struct Samp {
+    f32x4 v[8];
+    float w1, w2, w3, w4;
+    int h_low, w_low;
+    bool fb;
+  };
+  auto prep = [&](const float* st, int tap, float dy, float dx, float mk, Samp& o) {
     const int ky = tap / 3, kx = tap - 3 * ky;
     const float h_im = (float)(oy - 1 + ky) + dy;
     const float w_im = (float)(ox - 1 + kx) + dx;
     const bool valid = pix_ok & (h_im > -1.f) & (w_im > -1.f) & (h_im < (float)H) & (w_im < (float)W);
     const float fh = floorf(h_im), fw = floorf(w_im);
     const float lh = h_im - fh, lw = w_im - fw, hh = 1.f - lh, hw = 1.f - lw;
-    const int h_low = (int)fh, w_low = (int)fw;
-    const int r0 = h_low - ty0, c0 = w_low - tx0;
+    o.h_low = (int)fh;
+    o.w_low = (int)fw;
+    const int r0 = o.h_low - ty0, c0 = o.w_low - tx0;
     const bool in_tile = ((unsigned)r0 < (unsigned)(TR - 1)) & ((unsigned)c0 < (unsigned)(TC - 1));
     const float m = valid ? mk : 0.f;
     const float hm = hh * m, lm = lh * m;
-    const float w1 = hm * hw, w2 = hm * lw, w3 = lm * hw, w4 = lm * lw;
+    o.w1 = hm * hw;
+    o.w2 = hm * lw;
+    o.w3 = lm * hw;
+    o.w4 = lm * lw;
+#if DCNSEP_EXP == 4   // timing probe: no global fallback outside the staged tile
+    o.fb = false;
+#else
+    o.fb = valid & !in_tile;
+#endif
     const float* p0 = st + (((in_tile ? r0 : 0) * 4 + 2 * hf) * TP + (in_tile ? c0 : 0)) * 4;
     const float* p1 = p0 + 4 * TP * 4;   // next row
-    a0 = w1 * ld4(p0) + w2 * ld4(p0 + 4) + w3 * ld4(p1) + w4 * ld4(p1 + 4);
-    a1 = w1 * ld4(p0 + TP * 4) + w2 * ld4(p0 + TP * 4 + 4) + w3 * ld4(p1 + TP * 4) + w4 * ld4(p1 + TP * 4 + 4);
-#if DCNSEP_EXP == 4   // timing probe: no global fallback outside the staged tile
-    const bool fb = false;
-#else
-    const bool fb = valid & !in_tile;
-#endif
-    if (__builtin_amdgcn_ballot_w64(fb)) {
-      if (fb) {
-        const int h_high = h_low + 1, w_high = w_low + 1, co = pa * 16 + hf * 8;
+    o.v[0] = ld4(p0);
+    o.v[1] = ld4(p0 + 4);
+    o.v[2] = ld4(p1);
+    o.v[3] = ld4(p1 + 4);
+    o.v[4] = ld4(p0 + TP * 4);
+    o.v[5] = ld4(p0 + TP * 4 + 4);
+    o.v[6] = ld4(p1 + TP * 4);
+    o.v[7] = ld4(p1 + TP * 4 + 4);
+  };
+  auto finish = [&](const Samp& o, int pa, f32x4& a0, f32x4& a1) {
+    a0 = o.w1 * o.v[0] + o.w2 * o.v[1] + o.w3 * o.v[2] + o.w4 * o.v[3];
+    a1 = o.w1 * o.v[4] + o.w2 * o.v[5] + o.w3 * o.v[6] + o.w4 * o.v[7];
+    if (__builtin_amdgcn_ballot_w64(o.fb)) {
+      if (o.fb) {
+        const int h_low = o.h_low, w_low = o.w_low, h_high = h_low + 1, w_high = w_low + 1, co = pa * 16 + hf * 8;
         const bool b1 = h_low >= 0 && w_low >= 0, b2 = h_low >= 0 && w_high <= W - 1;
         const bool b3 = h_high <= H - 1 && w_low >= 0, b4 = h_high <= H - 1 && w_high <= W - 1;
         const float* q1 = in + ((size_t)h_low * W + w_low) * 64 + co;
@@ -286,46 +317,67 @@ __global__ __launch_bounds__(64 * NW) void k_dcn_sep(stif_dcn_sep_args a) {
         const float* q3 = in + ((size_t)h_high * W + w_low) * 64 + co;
         const float* q4 = in + ((size_t)h_high * W + w_high) * 64 + co;
         const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
-        a0 = w1 * (b1 ? ld4(q1) : z) + w2 * (b2 ? ld4(q2) : z) + w3 * (b3 ? ld4(q3) : z) + w4 * (b4 ? ld4(q4) : z);
-        a1 = w1 * (b1 ? ld4(q1 + 4) : z) + w2 * (b2 ? ld4(q2 + 4) : z) + w3 * (b3 ? ld4(q3 + 4) : z) +
-             w4 * (b4 ? ld4(q4 + 4) : z);
+        a0 = o.w1 * (b1 ? ld4(q1) : z) + o.w2 * (b2 ? ld4(q2) : z) + o.w3 * (b3 ? ld4(q3) : z) +
+             o.w4 * (b4 ? ld4(q4) : z);
+        a1 = o.w1 * (b1 ? ld4(q1 + 4) : z) + o.w2 * (b2 ? ld4(q2 + 4) : z) + o.w3 * (b3 ? ld4(q3 + 4) : z) +
+             o.w4 * (b4 ? ld4(q4 + 4) : z);
       }
     }
   };
 
   f32x16 acc0 = f32x16{0}, acc1 = f32x16{0};
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // pair 0 staged (and the om biases loaded)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // pair 0 staged (NW 8) and the om biases loaded
   __syncthreads();                                    // phase-1 buffers free
 #pragma unroll
   for (int pa = 0; pa < 4; ++pa) {
 #if DCNSEP_EXP == 3   // timing probe: no phase 2 work
     break;
 #endif
-    if (pa + 1 < 4) {
-      if ((pa + 1) & 1) stage_pair(pa + 1, smem + OFF_YT, smem + OFF_YW);
-      else stage_pair(pa + 1, smem + OFF_XT, smem + OFF_XW);
+    if (PAIR_AHEAD) {
+      if (pa + 1 < 4) {
+        if ((pa + 1) & 1) stage_pair(pa + 1, smem + OFF_YT, smem + OFF_YW);
+        else stage_pair(pa + 1, smem + OFF_XT, smem + OFF_XW);
+      }
+    } else {
+      // one buffer: this pair's stage lands while the other workgroup on the CU computes
+      if (pa) __syncthreads();   // every wave is done with the previous pair's buffer
+      stage_pair(pa, smem + OFF_XT, smem + OFF_XW);
+      lds_dma_barrier();
     }
-    const float* st = smem + ((pa & 1) ? OFF_YT : OFF_XT);
-    const float* sw = smem + ((pa & 1) ? OFF_YW : OFF_XW);
+    const float* st = smem + ((PAIR_AHEAD && (pa & 1)) ? OFF_YT : OFF_XT);
+    const float* sw = smem + ((PAIR_AHEAD && (pa & 1)) ? OFF_YW : OFF_XW);
+    // tap software pipeline: tap t + 1's corner reads are issued (after tap t's B fragments, so the
+    // in-order LDS counter lets the MFMAs start before they return) ahead of tap t's blend
+    Samp cur, nxt;
+    {
+      const int s = 27 * pa;
+      prep(st, 0, om[s / 16][s % 16], om[(s + 1) / 16][(s + 1) % 16], om[(s + 2) / 16][(s + 2) % 16], cur);
+    }
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
-      const int s = 27 * pa + 3 * t;   // this lane half's group 2 pa + h, tap t: slots s .. s + 2
-      f32x4 a0, a1;
-      sample(st, pa, t, om[s / 16][s % 16], om[(s + 1) / 16][(s + 1) % 16], om[(s + 2) / 16][(s + 2) % 16], a0, a1);
-      f16x8 ah, al;
-      split_f16x3(a0, a1, ah, al);
       const float* wp = sw + t * 1024 + lane * 4;   // [tap][nt][plane][lane][8 halves]
       const f16x8 bh0 = ldh8(wp), bl0 = ldh8(wp + 256), bh1 = ldh8(wp + 512), bl1 = ldh8(wp + 768);
+      if (t < 8) {
+        const int s = 27 * pa + 3 * (t + 1);   // this lane half's group 2 pa + h, tap t + 1: slots s .. s + 2
+        prep(st, t + 1, om[s / 16][s % 16], om[(s + 1) / 16][(s + 1) % 16], om[(s + 2) / 16][(s + 2) % 16], nxt);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      f32x4 a0, a1;
+      finish(cur, pa, a0, a1);
+      f16x8 ah, al;
+      split_f16x3(a0, a1, ah, al);
       acc0 = mfma16h(ah, bh0, acc0);
       acc1 = mfma16h(ah, bh1, acc1);
       acc0 = mfma16h(ah, bl0, acc0);
       acc1 = mfma16h(ah, bl1, acc1);
       acc0 = mfma16h(al, bh0, acc0);
       acc1 = mfma16h(al, bh1, acc1);
-      __builtin_amdgcn_sched_barrier(0);   // one tap's operands live at a time (VGPR budget)
+      __builtin_amdgcn_sched_barrier(0);   // two taps' operands live at a time (VGPR budget)
+      if (t < 8) cur = nxt;
     }
-    lds_dma_barrier();
+    if (PAIR_AHEAD) lds_dma_barrier();
   }
+  if (!PAIR_AHEAD) __syncthreads();   // the epilogue blocks overwrite the pair buffer
   // epilogue through a per-wave LDS block -> coalesced 16-B stores (k_dcn's)
   float* out = a.out[g] + (size_t)n * a.out_item;
   const float* bias = a.bias[g];

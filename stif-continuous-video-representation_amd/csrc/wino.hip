@@ -45,6 +45,9 @@ constexpr int OM_RP = 320;                     // 16-B chunks per staged halo ro
 constexpr int EX_F = 2 * 2 * 2 * 1024;         // epilogue exchange: [wave 1|2][nt][b][32 tiles][32 co]
 constexpr int BUF_F = EX_F;                    // floats per buffer (32 KB)
 constexpr int WG_PER_CU = 2;
+#ifndef WINO_EXP
+#define WINO_EXP 0   // k_wino f16x3 timing probes (wrong results): 1 no LDS-DMA after the first phase, 2 no B refills, 3 no output exchange
+#endif
 static_assert(HR * OM_RP * 4 <= BUF_F && OM_RP % 8 == 0 && 35 * PITCH <= OM_RP, "staging image");
 
 // slot of halo column c in its (row, chunk, half) run: even columns first, then odd
@@ -277,8 +280,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         // the phase's first LDS reads go out before the next phase's LDS-DMA is issued, so the DMA
         // issue (~1K cycles per wave) overlaps their latency instead of preceding it
         xread(buf, 0, rd);
-        if (p + 1 < NP) stage(cur, p + 1, (gp + 1) & 1);
-        else if (has_next) stage(nxt, 0, (gp + 1) & 1);
+        if (WINO_EXP != 1) {
+          if (p + 1 < NP) stage(cur, p + 1, (gp + 1) & 1);
+          else if (has_next) stage(nxt, 0, (gp + 1) & 1);
+        }
 #pragma unroll
         for (int sp = 0; sp < PSUB / 2; ++sp) {
           // chunk pair (2 sp, 2 sp + 1): lane half h holds channels 4h..4h+3 of both, i.e. the 8
@@ -305,7 +310,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
             // refill the slot with block j + 2: (pair q, j + 2) or (pair q + 1, j - 2)
             const float* wn = j < 2 ? wq + (j + 2) * 1024 : wq1 + (j - 2) * 1024;
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
+            for (int u = 0; u < 2 && WINO_EXP != 2; ++u) {
               bh[j & 1][u] = ldh8(wn + (u * 2) * 256);
               bl[j & 1][u] = ldh8(wn + (u * 2 + 1) * 256);
             }
@@ -368,6 +373,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     // pixel's 128 B).  Row swizzle R ^ (bit2(tile) ^ b) keeps both the b32 writes (lane halves 4
     // tiles apart) and the b128 reads (16-lane groups = b 0/1 of one tile) conflict-free.
     float* ex = smem + ((gp - 1) & 1) * BUF_F;
+    if (WINO_EXP == 3) {
+      f32x16 sm = f32x16{0};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sm += acc[j][0] + acc[j][1];
+      float tot = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) tot += sm[r];
+      a.out[cur.g][(size_t)cur.n * a.out_item + ((size_t)(cur.oy0 * a.Wo + cur.ox0) * a.cout) + tid] = tot;
+      if (!has_next) break;
+      T = Tn;
+      cur = nxt;
+      wsl = wnx;
+      continue;
+    }
     f32x16 yv[2][2];   // [local half][b]
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
