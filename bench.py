@@ -17,6 +17,7 @@ CPU oracle (max error, PSNR), the fp32-MFMA value and the C1 / C2 lines.
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c0|c1|c2|c3|c4]
 """
 import argparse
+import glob
 import json
 import os
 import sys
@@ -454,7 +455,7 @@ def main():
     ap.add_argument("--no-extras", action="store_true", help="N=1: skip the fp32-MFMA and C1/C2 lines")
     ap.add_argument("--traffic", default=None,
                     help="PMC summary (tools/pmc_summary.py) giving the dominant kernel's HBM bytes/dispatch; "
-                         "default profiles/pmc_r02_<config>.json")
+                         "default: the newest profiles/pmc_rNN_<config>.json")
     ap.add_argument("--mfma", default="f16x3", choices=["f32", "f16x3"],
                     help="operand mode of the contractions (model.LunaTokis mfma=)")
     ap.add_argument("--kernel-report", action="store_true", help="time every launch kind (stderr)")
@@ -519,7 +520,8 @@ def main():
         traffic = None
         # HBM bytes per dispatch of the same kernel from the committed PMC passes over this bench at this
         # config (tools/pmc_summary.py; FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md HBM section)
-        tpath = args.traffic or os.path.join(REPO, "profiles", f"pmc_r02_{args.config}.json")
+        found = sorted(glob.glob(os.path.join(REPO, "profiles", f"pmc_r[0-9][0-9]_{args.config}.json")))
+        tpath = args.traffic or (found[-1] if found else "")
         if os.path.exists(tpath) and args.mfma == "f16x3":
             try:
                 pmc = json.load(open(tpath))["per_kernel"]

@@ -89,7 +89,10 @@ STIF_DEV void wait_vm(int n) {
 }
 
 template <int EPI>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) void k_dcn_sep(stif_dcn_sep_args a) {
+#ifndef DCNSEP_WPE
+#define DCNSEP_WPE 2
+#endif
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_WPE))) void k_dcn_sep(stif_dcn_sep_args a) {
   __shared__ __attribute__((aligned(16))) float smem[LDS_F];
   const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, hf = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -161,9 +164,18 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
   };
 
   // ---------------------------------------------------------------- phase 1: offset/mask conv
+  // the accumulators start at bias x 2^14 (the f16x3 scale): no bias pass between the phases.  Slot s =
+  // 16 m + r of lane half h is packed row (r & 3) + 8 (r >> 2) + 4 h of M-tile m (stif_pack_conv_weight,
+  // STIF_PACK_DCNSEP: bias [M-tile][32 rows], zero on the padding rows)
   f32x16 om[MT];
 #pragma unroll
-  for (int q = 0; q < MT; ++q) om[q] = f32x16{0};
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const f32x4 bq = ld4(a.b_om[g] + m * 32 + 8 * v + 4 * hf) * (1.0f / F16X3_UNSCALE);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) om[m][4 * v + e] = bq[e];
+    }
 #if DCNSEP_EXP == 1   // timing probe: no phase 1 (offsets = biases)
   if (false)
 #endif
@@ -239,77 +251,50 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
   // slot s = 16 m + r of lane half h = component s % 3 (dy, dx, mask) of tap (s % 27) / 3 of group
   // 2 (s / 27) + h, packed row (r & 3) + 8 (r >> 2) + 4 h of M-tile m; bias, unscale, sigmoid(mask)
   // (dcn_v2.py:134-138)
-  bool bad = false;
+  // unscale, sigmoid(mask) (dcn_v2.py:134-138); the range check is one sum (a non-finite value makes it
+  // non-finite) -- a per-value compare would hold 108 lane masks in SGPRs
+  float chk = 0.f;
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const f32x4 bq = ld4(a.b_om[g] + m * 32 + 8 * v + 4 * hf);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int s = 16 * m + 4 * v + e;
-        if (s < 108) {
-          float x = om[m][4 * v + e] * F16X3_UNSCALE + bq[e];
-          bad |= not_finite(x);
-          if (s % 3 == 2) x = sigmoid_fast(x);
-          om[m][4 * v + e] = x;
-        }
+    for (int r = 0; r < 16; ++r) {
+      const int s = 16 * m + r;
+      if (s < 108) {
+        float x = om[m][r] * F16X3_UNSCALE;
+        chk += x;
+        if (s % 3 == 2) x = sigmoid_fast(x);
+        om[m][r] = x;
       }
     }
   }
+  const bool bad = not_finite(chk);
   report_range(a.status, bad);
 
   // ---------------------------------------------------------------- phase 2: deformable conv
   // bilinear sample of this lane half's group (channels 16 pa + 8 h .. + 7: a0 = quad 2h, a1 = quad 2h + 1)
   // at tap `tap` with offset (dy, dx) and modulation m folded into the corner weights; `> -1` / `< H`
   // gate; global fallback outside the tile
-  // split in two so that tap t + 1's eight corner reads are in flight while tap t blends and multiplies:
-  // prep() = coordinates, corner weights and the LDS reads; finish() = the blend (and the fallback)
-  struct Samp {
-    f32x4 v[8];
-    float w1, w2, w3, w4;
-    int h_low, w_low;
-    bool fb;
-  };
-  auto prep = [&](const float* st, int tap, float dy, float dx, float mk, Samp& o) {
+  auto sample = [&](const float* st, int pa, int tap, float dy, float dx, float mk, f32x4& a0, f32x4& a1) {
     const int ky = tap / 3, kx = tap - 3 * ky;
     const float h_im = (float)(oy - 1 + ky) + dy;
     const float w_im = (float)(ox - 1 + kx) + dx;
     const bool valid = pix_ok & (h_im > -1.f) & (w_im > -1.f) & (h_im < (float)H) & (w_im < (float)W);
     const float fh = floorf(h_im), fw = floorf(w_im);
     const float lh = h_im - fh, lw = w_im - fw, hh = 1.f - lh, hw = 1.f - lw;
-    o.h_low = (int)fh;
-    o.w_low = (int)fw;
-    const int r0 = o.h_low - ty0, c0 = o.w_low - tx0;
+    const int h_low = (int)fh, w_low = (int)fw;
+    const int r0 = h_low - ty0, c0 = w_low - tx0;
     const bool in_tile = ((unsigned)r0 < (unsigned)(TR - 1)) & ((unsigned)c0 < (unsigned)(TC - 1));
     const float m = valid ? mk : 0.f;
     const float hm = hh * m, lm = lh * m;
-    o.w1 = hm * hw;
-    o.w2 = hm * lw;
-    o.w3 = lm * hw;
-    o.w4 = lm * lw;
-#if DCNSEP_EXP == 4   // timing probe: no global fallback outside the staged tile
-    o.fb = false;
-#else
-    o.fb = valid & !in_tile;
-#endif
+    const float w1 = hm * hw, w2 = hm * lw, w3 = lm * hw, w4 = lm * lw;
     const float* p0 = st + (((in_tile ? r0 : 0) * 4 + 2 * hf) * TP + (in_tile ? c0 : 0)) * 4;
     const float* p1 = p0 + 4 * TP * 4;   // next row
-    o.v[0] = ld4(p0);
-    o.v[1] = ld4(p0 + 4);
-    o.v[2] = ld4(p1);
-    o.v[3] = ld4(p1 + 4);
-    o.v[4] = ld4(p0 + TP * 4);
-    o.v[5] = ld4(p0 + TP * 4 + 4);
-    o.v[6] = ld4(p1 + TP * 4);
-    o.v[7] = ld4(p1 + TP * 4 + 4);
-  };
-  auto finish = [&](const Samp& o, int pa, f32x4& a0, f32x4& a1) {
-    a0 = o.w1 * o.v[0] + o.w2 * o.v[1] + o.w3 * o.v[2] + o.w4 * o.v[3];
-    a1 = o.w1 * o.v[4] + o.w2 * o.v[5] + o.w3 * o.v[6] + o.w4 * o.v[7];
-    if (__builtin_amdgcn_ballot_w64(o.fb)) {
-      if (o.fb) {
-        const int h_low = o.h_low, w_low = o.w_low, h_high = h_low + 1, w_high = w_low + 1, co = pa * 16 + hf * 8;
+    a0 = w1 * ld4(p0) + w2 * ld4(p0 + 4) + w3 * ld4(p1) + w4 * ld4(p1 + 4);
+    a1 = w1 * ld4(p0 + TP * 4) + w2 * ld4(p0 + TP * 4 + 4) + w3 * ld4(p1 + TP * 4) + w4 * ld4(p1 + TP * 4 + 4);
+    const bool fb = valid & !in_tile;
+    if (__builtin_amdgcn_ballot_w64(fb)) {
+      if (fb) {
+        const int h_high = h_low + 1, w_high = w_low + 1, co = pa * 16 + hf * 8;
         const bool b1 = h_low >= 0 && w_low >= 0, b2 = h_low >= 0 && w_high <= W - 1;
         const bool b3 = h_high <= H - 1 && w_low >= 0, b4 = h_high <= H - 1 && w_high <= W - 1;
         const float* q1 = in + ((size_t)h_low * W + w_low) * 64 + co;
@@ -317,15 +302,23 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
         const float* q3 = in + ((size_t)h_high * W + w_low) * 64 + co;
         const float* q4 = in + ((size_t)h_high * W + w_high) * 64 + co;
         const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
-        a0 = o.w1 * (b1 ? ld4(q1) : z) + o.w2 * (b2 ? ld4(q2) : z) + o.w3 * (b3 ? ld4(q3) : z) +
-             o.w4 * (b4 ? ld4(q4) : z);
-        a1 = o.w1 * (b1 ? ld4(q1 + 4) : z) + o.w2 * (b2 ? ld4(q2 + 4) : z) + o.w3 * (b3 ? ld4(q3 + 4) : z) +
-             o.w4 * (b4 ? ld4(q4 + 4) : z);
+        a0 = w1 * (b1 ? ld4(q1) : z) + w2 * (b2 ? ld4(q2) : z) + w3 * (b3 ? ld4(q3) : z) + w4 * (b4 ? ld4(q4) : z);
+        a1 = w1 * (b1 ? ld4(q1 + 4) : z) + w2 * (b2 ? ld4(q2 + 4) : z) + w3 * (b3 ? ld4(q3 + 4) : z) +
+             w4 * (b4 ? ld4(q4 + 4) : z);
       }
     }
   };
 
-  f32x16 acc0 = f32x16{0}, acc1 = f32x16{0};
+  // accumulators start at the DCN bias x 2^14 (lane = output channel)
+  f32x16 acc0, acc1;
+  {
+    const float b0 = a.bias[g][l32] * (1.0f / F16X3_UNSCALE), b1 = a.bias[g][32 + l32] * (1.0f / F16X3_UNSCALE);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      acc0[r] = b0;
+      acc1[r] = b1;
+    }
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // pair 0 staged (NW 8) and the om biases loaded
   __syncthreads();                                    // phase-1 buffers free
 #pragma unroll
@@ -346,52 +339,41 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     }
     const float* st = smem + ((PAIR_AHEAD && (pa & 1)) ? OFF_YT : OFF_XT);
     const float* sw = smem + ((PAIR_AHEAD && (pa & 1)) ? OFF_YW : OFF_XW);
-    // tap software pipeline: tap t + 1's corner reads are issued (after tap t's B fragments, so the
-    // in-order LDS counter lets the MFMAs start before they return) ahead of tap t's blend
-    Samp cur, nxt;
-    {
-      const int s = 27 * pa;
-      prep(st, 0, om[s / 16][s % 16], om[(s + 1) / 16][(s + 1) % 16], om[(s + 2) / 16][(s + 2) % 16], cur);
-    }
+    // a tap-level software pipeline (tap t + 1's corner reads issued before tap t's blend, one more
+    // sample set live) measured 4 % faster in the C0 step but made the outputs depend on the launch's
+    // timing at two waves per SIMD; not kept
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
-      const float* wp = sw + t * 1024 + lane * 4;   // [tap][nt][plane][lane][8 halves]
-      const f16x8 bh0 = ldh8(wp), bl0 = ldh8(wp + 256), bh1 = ldh8(wp + 512), bl1 = ldh8(wp + 768);
-      if (t < 8) {
-        const int s = 27 * pa + 3 * (t + 1);   // this lane half's group 2 pa + h, tap t + 1: slots s .. s + 2
-        prep(st, t + 1, om[s / 16][s % 16], om[(s + 1) / 16][(s + 1) % 16], om[(s + 2) / 16][(s + 2) % 16], nxt);
-      }
-      __builtin_amdgcn_sched_barrier(0);
+      const int s = 27 * pa + 3 * t;   // this lane half's group 2 pa + h, tap t: slots s .. s + 2
       f32x4 a0, a1;
-      finish(cur, pa, a0, a1);
+      sample(st, pa, t, om[s / 16][s % 16], om[(s + 1) / 16][(s + 1) % 16], om[(s + 2) / 16][(s + 2) % 16], a0, a1);
       f16x8 ah, al;
       split_f16x3(a0, a1, ah, al);
+      const float* wp = sw + t * 1024 + lane * 4;   // [tap][nt][plane][lane][8 halves]
+      const f16x8 bh0 = ldh8(wp), bl0 = ldh8(wp + 256), bh1 = ldh8(wp + 512), bl1 = ldh8(wp + 768);
       acc0 = mfma16h(ah, bh0, acc0);
       acc1 = mfma16h(ah, bh1, acc1);
       acc0 = mfma16h(ah, bl0, acc0);
       acc1 = mfma16h(ah, bl1, acc1);
       acc0 = mfma16h(al, bh0, acc0);
       acc1 = mfma16h(al, bh1, acc1);
-      __builtin_amdgcn_sched_barrier(0);   // two taps' operands live at a time (VGPR budget)
-      if (t < 8) cur = nxt;
+      __builtin_amdgcn_sched_barrier(0);   // one tap's operands live at a time (VGPR budget)
     }
     if (PAIR_AHEAD) lds_dma_barrier();
   }
   if (!PAIR_AHEAD) __syncthreads();   // the epilogue blocks overwrite the pair buffer
   // epilogue through a per-wave LDS block -> coalesced 16-B stores (k_dcn's)
   float* out = a.out[g] + (size_t)n * a.out_item;
-  const float* bias = a.bias[g];
   float* blk = smem + OFF_D0 + wv * 1024;
   const int rpx = lane >> 3, c4 = lane & 7;
-  bool bad2 = false;
+  float chk2 = 0.f;
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt) {
-    const float bv = bias[nt * 32 + l32];
     f32x16 v;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      float t = (nt ? acc1[r] : acc0[r]) * F16X3_UNSCALE + bv;
-      bad2 |= not_finite(t);
+      float t = (nt ? acc1[r] : acc0[r]) * F16X3_UNSCALE;
+      chk2 += t;
       if (EPI == STIF_EPI_LRELU) t = lrelu01(t);
       v[r] = t;
     }
@@ -403,7 +385,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
       if (oy < H && x < W) st4(out + ((size_t)oy * W + x) * 64 + nt * 32 + c4 * 4, o);
     }
   }
-  report_range(a.status, bad2);
+  report_range(a.status, not_finite(chk2));
 }
 
 }  // namespace

@@ -481,6 +481,52 @@ def test_dcn_sep_fused_matches_oracle(ops, L, epi, hw, oscale):
     assert relmax(to_nchw(out), ref) < RTOL
 
 
+def test_dcn_sep_fused_many_workgroups(ops, L):
+    """k_dcn_sep with more workgroups than CUs (two resident per CU, several rounds, two weight sets):
+    == the oracle, and three launches agree bit for bit."""
+    H, W, B = 64, 128, 6
+    sds = [_dcnsep_weights(90 + 10 * i, 2.0) for i in range(2)]
+    xs = [rnd(B, 64, H, W, seed=91 + i) for i in range(2)]
+    fs = [rnd(B, 64, H, W, seed=93 + i) for i in range(2)]
+    groups, outs = [], []
+    for i in range(2):
+        om, core = _dcnsep_layers(ops, L, sds[i])
+        outs.append(torch.full((B, H, W, 64), float("nan"), device="cuda"))
+        groups.append(dict(om_layer=om, layer=core, fea=nhwc(fs[i]), inp=nhwc(xs[i]), out=outs[i]))
+    st = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ops.dcn_sep(groups, epi=L.EPI_NONE, status=st)
+    first = [o.clone() for o in outs]
+    for _ in range(2):
+        ops.dcn_sep(groups, epi=L.EPI_NONE, status=st)
+        for o, f in zip(outs, first):
+            assert torch.equal(o, f)
+    assert int(st.item()) == 0
+    for i in range(2):
+        assert relmax(to_nchw(first[i]), O.dcn_sep(xs[i], fs[i], sds[i], "x")) < RTOL
+
+
+@pytest.mark.parametrize("oscale", [2.0, 7.0])
+def test_dcn_sep_fused_batch_independent(ops, L, oscale):
+    """k_dcn_sep: an item's output does not depend on the other items of the launch (tile placement,
+    workgroup scheduling, which lanes of a wave take the global fallback), bit for bit, and two launches
+    of the same batch agree bit for bit."""
+    H, W, B = 37, 100, 5
+    sdx = _dcnsep_weights(80, oscale)
+    x = torch.from_numpy(rnd(B, H, W, 64, seed=81)).cuda()
+    fea = torch.from_numpy(rnd(B, H, W, 64, seed=82)).cuda()
+    om, core = _dcnsep_layers(ops, L, sdx)
+
+    def run(xs, fs):
+        out = torch.full(xs.shape, float("nan"), device="cuda")
+        ops.dcn_sep([dict(om_layer=om, layer=core, fea=fs, inp=xs, out=out)], epi=L.EPI_NONE)
+        return out
+
+    full = run(x, fea)
+    assert torch.equal(full, run(x, fea))
+    for i in (0, 3):
+        assert torch.equal(full[i:i + 1], run(x[i:i + 1].clone(), fea[i:i + 1].clone())), i
+
+
 def test_dcn_sep_fused_gates_and_groups(ops, L):
     """Offsets exactly on the sampling gates (bias-only offset channels), and a launch of 3 weight sets
     over strided items (a [3, n, H, W, 64] buffer's sub-tensors), each against its own oracle."""

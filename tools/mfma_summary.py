@@ -1,4 +1,4 @@
-"""Per-kernel MFMA-busy summary of a rocprofv3 SQ pass over the C0 bench (tools/r2_prof.sh, *_mfma).
+"""Per-kernel MFMA-busy summary of a rocprofv3 SQ pass over the C0 bench (tools/prof_c0.sh, *_mfma).
 
 usage: python tools/mfma_summary.py COUNTER_CSV > profiles/r02_mfma_c0.txt
 
@@ -13,7 +13,7 @@ from collections import OrderedDict, defaultdict
 acc = OrderedDict()
 for r in csv.DictReader(open(sys.argv[1])):
     acc.setdefault(r["Kernel_Name"], defaultdict(list))[r["Counter_Name"]].append(float(r["Counter_Value"]))
-print("# SQ pass over one C0 bench step (rocprofv3 --pmc, tools/r2_prof.sh): per kernel, mean per dispatch.")
+print("# SQ pass over one C0 bench step (rocprofv3 --pmc, tools/prof_c0.sh): per kernel, mean per dispatch.")
 print("# MFMA-busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs): the share of SIMD "
       "cycles the MFMA pipe is busy")
 mean = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}

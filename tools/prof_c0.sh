@@ -1,8 +1,8 @@
-# Round-2 profile of the default (C0) bench: kernel-trace stats, FETCH/WRITE passes and one SQ
+# Profile of the default (C0) bench: kernel-trace stats, FETCH/WRITE passes and one SQ
 # MFMA-busy pass (separate rocprofv3 runs, MI355X_MICROARCH.md PMC rules).  TAG names the outputs.
 set -e
 R=$GRAFT_REPO_ROOT
-TAG=${TAG:-r2}
+TAG=${TAG:-r03}
 mkdir -p $R/gpurun_out
 cd $R
 timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-extras --steps 10 --warmup 2 --kernel-report > gpurun_out/${TAG}_bench_c0.log 2>&1
