@@ -103,23 +103,36 @@ def test_training_step_through_ext_shim_matches_oracle(sd):
             "conv_offset_mask.bias": sd[p + ".conv_offset_mask.bias"]}
     inp = rng.standard_normal((B, 64, H, W)).astype(np.float32)
     fea = rng.standard_normal((B, 64, H, W)).astype(np.float32)
-    gt = rng.standard_normal((B, 64, H, W)).astype(np.float32)
-    res = {}
-    for name, backend, dt, dev in (("gpu", _ext(), torch.float32, "cuda"), ("oracle", _OracleBackend, torch.float64, "cpu")):
+
+    def make(backend, dt, dev):
         net = DcnSep(make_dcn_conv(backend), dt, dev)
         with torch.no_grad():
             for k, v in net.named_parameters():
                 v.copy_(torch.from_numpy(np.asarray(init[k])))
+        return net
+
+    # the target sits 1-2 away from the output everywhere: the Charbonnier gradient d / sqrt(d^2 + 1e-6)
+    # is then ~sign(d) and well conditioned (near d = 0 it amplifies a 1e-6 forward difference ~350x,
+    # which would test the loss's conditioning, not the DCN op)
+    with torch.no_grad():
+        out0 = make(_OracleBackend, torch.float64, "cpu")(torch.from_numpy(inp).double(),
+                                                          torch.from_numpy(fea).double()).numpy()
+    gt = (out0 + np.where(rng.random(out0.shape) < 0.5, -1.0, 1.0) * (1.0 + rng.random(out0.shape))).astype(np.float32)
+    res = {}
+    for name, backend, dt, dev in (("gpu", _ext(), torch.float32, "cuda"), ("oracle", _OracleBackend, torch.float64, "cpu")):
+        net = make(backend, dt, dev)
         T = lambda a: torch.from_numpy(a).to(dev, dt)
         res[name] = _step(net, T(inp), T(fea), T(gt))
     (lg, gg, pg), (lo, go, po) = res["gpu"], res["oracle"]
-    assert abs(lg - lo) <= 1e-5 * abs(lo)
+    assert abs(lg - lo) <= 1e-5 * abs(lo), (lg, lo)
     for k in go:
         g, r = gg[k].double().cpu(), go[k]
-        assert float((g - r).abs().max()) <= 2e-5 * float(r.abs().max()), k
+        err, tol = float((g - r).abs().max()), 2e-5 * float(r.abs().max())
+        assert err <= tol, (k, err, tol)
         # Adam's first step moves each parameter by ~lr * sign(grad): equal wherever the gradient's sign
         # is not decided by rounding
         d = (pg[k].double().cpu() - po[k]).abs()
         firm = r.abs() > 1e-3 * r.abs().max()
-        assert float(d[firm].max()) <= 1e-6, k
-        assert float(d.max()) <= 2 * 2e-5 + 1e-6, k
+        e_firm, e_all = float(d[firm].max()), float(d.max())
+        assert e_firm <= 1e-6, (k, e_firm)
+        assert e_all <= 2 * 2e-5 + 1e-6, (k, e_all)
