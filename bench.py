@@ -254,7 +254,7 @@ def cpu_model():
     return "unknown"
 
 
-CPU_SAMPLE = 64   # LR crop of the CPU-baseline sample (FLOP per output pixel does not depend on it)
+CPU_SAMPLE = 128  # LR crop of the CPU-baseline sample (FLOP per output pixel does not depend on it)
 
 
 def _oracle_timed(threads=None):

@@ -6,8 +6,9 @@
 // (src/cuda/dcn_v2_cuda.cu:42-172) with the sampling of modulated_deformable_im2col_gpu_kernel /
 // dmcn_im2col_bilinear (dcn_v2_im2col_cuda.cu:25-54,125-195).
 //
-// Workgroup = 8 waves, tile = 8 output rows x 32 columns, wave w = output row w (lane & 31 = column).
-// Lane half h works on the deformable groups h, h + 2, h + 4, h + 6 throughout.
+// Workgroup = NW waves (default 4: two 80-KB workgroups per CU), tile = NW output rows x 32 columns,
+// wave w = output row w (lane & 31 = column).  Lane half h works on the deformable groups h, h + 2,
+// h + 4, h + 6 throughout.
 //
 // Phase 1, the offset/mask conv as a direct implicit GEMM with the WEIGHTS as the MFMA A operand:
 // D[om row][pixel] += W[om row][k] X[k][pixel] on split-fp16 v_mfma_f32_32x32x16_f16 (f16x3, fp32
@@ -17,14 +18,15 @@
 // straight into the bilinear sampling, with no exchange, no LDS round trip and no HBM traffic.
 // K = 36 steps (16-channel chunk c, tap t); per step a wave reads its pixels' 8 channels of the staged
 // input halo (two ds_read_b128), splits them once and runs 3 MFMAs per M-tile (21 MFMAs per step;
-// 112 accumulator VGPRs).  The input halo (10 x 34 pixels, one 16-channel chunk, 80-B pixel pitch:
+// 112 accumulator VGPRs).  The input halo ((NW + 2) x 34 pixels, one 16-channel chunk, 80-B pixel pitch:
 // conflict-free reads) and the packed weights of each step (a 3-slot ring) arrive by LDS-DMA ahead of
 // use; one barrier per step.
 //
 // Phase 2, the deformable conv, two groups per K step: per group pair (2a, 2a + 1) the 16-channel input
-// tile with a 2-px margin and the pair's weight fragments are LDS-DMA'd one pair ahead (pair 0 during
-// phase 1); for every tap t lane half h samples group 2a + h's 8 channels at its pixel (global fallback
-// outside the margin) -- the 16 K values of one 32x32x16 MFMA -- and runs 3 MFMAs per 32-cout half:
+// tile with a 2-px margin and the pair's weight fragments are LDS-DMA'd (NW 8: one pair ahead, pair 0
+// during phase 1; NW 4: into one buffer while the CU's other workgroup computes); for every tap t lane
+// half h samples group 2a + h's 8 channels at its pixel (global fallback outside the margin) -- the 16
+// K values of one 32x32x16 MFMA -- and runs 3 MFMAs per 32-cout half:
 // 9 K steps per pair instead of 10 for two single groups (tap pairs); epilogue through LDS as k_dcn.
 #include "abi_util.h"
 #include "stif.h"

@@ -75,6 +75,32 @@ def test_c0_window_pairs_equal_single_pairs(models):
             assert torch.equal(win[p:p + 1], one), p
 
 
+def test_c0_window_dcn_sep_launches_deterministic(stif, models):
+    """Every fused DCN_sep launch of the C0 window (k_dcn_sep: the L3 / L2 / L1 alignments of the PCD and
+    the three Bi-ConvLSTM steps, launch groups of up to 8 weight sets at two waves per SIMD), re-run into
+    fresh buffers, reproduces its output bit for bit (a kernel whose result depended on wave timing --
+    the removed tap-pipelined form -- fails here)."""
+    fr = synth(0, 7, 128, 128)
+    ops = stif.ops
+    orig = ops.dcn_sep
+    seen = []
+
+    def traced(groups, epi=0, status=None):
+        orig(groups, epi=epi, status=status)
+        ref = [g["out"].clone() for g in groups]
+        for _ in range(2):
+            g2 = [dict(g, out=torch.full_like(g["out"], float("nan"))) for g in groups]
+            orig(g2, epi=epi, status=None)
+            seen.append(all(torch.equal(a["out"], b) for a, b in zip(g2, ref)))
+    ops.dcn_sep = traced
+    try:
+        with torch.no_grad():
+            models["f16x3"].gen_feat_window(fr)
+    finally:
+        ops.dcn_sep = orig
+    assert len(seen) >= 2 * 12 and all(seen), seen
+
+
 CONFIG_CASES = {
     # BASELINE configs[1..4] at their full per-GPU sizes: (frames, H, W, output size or None, times)
     "C1": (7, 256, 256, None, [0.5]),
