@@ -13,6 +13,7 @@
 //    runs k_dcn between NCHW <-> NHWC transposes (weights packed on the device); any other shape
 //    an im2col kernel into a caller workspace + an fp32-MFMA GEMM with fused bias, per sample.
 #include "stif_common.h"
+#include "tuning.h"
 #include "stif.h"
 #include "abi_util.h"
 
@@ -54,20 +55,7 @@ STIF_DEV f32x4 dcn_sample4(const float* __restrict__ img, int H, int W, float h,
 // MR = 1, where the halved grid would leave CUs idle.  The kernel is latency-bound (waves parked on
 // memory waits and group barriers 43 % of their cycles, profiles/r02_dcn_sq_c0l1.txt), so two
 // independent 4-wave workgroups per CU beat one 8-wave workgroup.
-#ifndef DCN_TH
-// 4 waves per workgroup: with two rows per wave an 8-row tile, two workgroups per CU (74 KB of LDS each)
-// whose group barriers and memory waits overlap -- C0 L1 DCN 240 -> 223 us against 8 waves (one
-// 16-row workgroup per CU), same-box A/B (profiles/r02_dcn_th_ab.log); round 1's one-row kernel was
-// faster with 8 (C1 L1 438.7 -> 414.9 us against 4)
-#define DCN_TH 4
-#endif
 constexpr int DCN_ROWS = DCN_TH;   // waves per workgroup
-#ifndef DCN_M
-// staged margin (pixels) around the 3x3 footprint; samples beyond it use the global-load fallback.
-// C0 L1 (same-box A/B over the full bench): margin 2 / 3 / 4 / 6 / 8 -> 248 / 250 / 257 / 266 / 289 us --
-// staging a wider tile costs more than the fallbacks it saves
-#define DCN_M 2
-#endif
 
 // MR: output rows per wave (2 only with F16; the launcher picks it by grid size, see stif_dcn_nhwc)
 template <int EPI, int F16, int MR = 1>
@@ -589,9 +577,6 @@ extern "C" int stif_dcn_nhwc(const stif_dcn_args* pa, void* stream) {
   const bool f16 = a.flags & STIF_CONV_F16X3;
   // two rows per wave (8-row workgroups, two per CU) when that still gives >= 4 workgroups per CU
   const long long wg2 = (long long)((a.W + 31) / 32) * ((a.H + 2 * DCN_ROWS - 1) / (2 * DCN_ROWS)) * a.ngroups * a.nitems;
-#ifndef DCN_MR2_MIN
-#define DCN_MR2_MIN 1024   // 512 (two-row kernel also at the C0 L2 maps) measured no faster
-#endif
   const bool mr2 = f16 && wg2 >= DCN_MR2_MIN;
   const int th = DCN_ROWS * (mr2 ? 2 : 1);   // output rows per workgroup
   dim3 grid(((a.W + 31) / 32) * ((a.H + th - 1) / th), 1, a.ngroups * a.nitems);

@@ -31,14 +31,12 @@
 #include "abi_util.h"
 #include "stif.h"
 #include "stif_common.h"
+#include "tuning.h"
 
 namespace {
 
-#ifndef DCNSEP_NW
-#define DCNSEP_NW 4
-#endif
-// NW = 4: 4 output rows per tile, two 80-KB workgroups per CU -- one's MFMA-dense phase 1 runs beside the
-// other's sampling-bound phase 2; NW = 8: one 152-KB workgroup per CU with the next phase staged ahead
+// NW = 4 (tuning.h): 4 output rows per tile, two 80-KB workgroups per CU; NW = 8: one 152-KB workgroup per
+// CU with the next group pair staged ahead (slower)
 constexpr int NW = DCNSEP_NW;                 // waves = output rows per tile
 constexpr int TW = 32;                        // output columns per tile
 // phase 1
@@ -73,9 +71,6 @@ constexpr int OFF_YT = T_INST * 256, OFF_YW = OFF_YT + T_INST * 256;
 constexpr int LDS_F = PAIR_AHEAD ? OFF_XW + PW_PAD_F : OFF_W + RING * 4096;
 static_assert(D_F <= OFF_D1 && WK_F <= 4096 && NW * 1024 <= D_F && LDS_F * 4 <= (NW == 8 ? 160 : 80) * 1024 &&
               (PAIR_AHEAD ? OFF_YW + PW_PAD_F <= OFF_XW : OFF_XW + PW_PAD_F <= LDS_F), "LDS map");
-#ifndef DCNSEP_EXP
-#define DCNSEP_EXP 0    // timing probes (wrong results): 1 no phase 1, 3 no phase 2, 4 no fallback loads
-#endif
 
 // vmcnt waits with an immediate operand (the counts are wave-uniform)
 STIF_DEV void wait_vm(int n) {
@@ -91,9 +86,6 @@ STIF_DEV void wait_vm(int n) {
 }
 
 template <int EPI>
-#ifndef DCNSEP_WPE
-#define DCNSEP_WPE 2
-#endif
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_WPE))) void k_dcn_sep(stif_dcn_sep_args a) {
   __shared__ __attribute__((aligned(16))) float smem[LDS_F];
   const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, hf = lane >> 5;

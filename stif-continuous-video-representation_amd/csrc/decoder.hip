@@ -17,6 +17,7 @@
 // accumulator registers (layout in dec_layout.h), sin(30 z) applied in registers.
 #include "dec_layout.h"
 #include "stif_common.h"
+#include "tuning.h"
 #include "stif.h"
 #include "abi_util.h"
 
@@ -173,17 +174,11 @@ STIF_DEV f32x4 img_sample(const float* __restrict__ I, const Bilin& b, int hf) {
 // (a few 4-KB tiles: one layer, or one output tile's K-tiles) is LDS-DMA'd while the previous one
 // is being consumed (double-buffered, one barrier per segment), and every wave reads its A
 // operands from LDS -- one tile feeds 16 MFMAs in each wave of the workgroup.
-#ifndef DEC1_NW
-#define DEC1_NW 4
-#endif
 // waves per workgroup of k_dec1 (~240 VGPRs: 2 waves/SIMD).  4-wave workgroups, 2 per CU (80 KB LDS
 // each): the two waves sharing a SIMD come from different workgroups, so one's segment barrier or
 // sin stretch overlaps the other's MFMAs
 constexpr int DEC_NW = DEC1_NW;
 constexpr int DEC2_NW = 4;   // k_dec2: 8 layer-3 accumulator tiles (128 VGPRs) live
-#ifndef DEC2_WPE
-#define DEC2_WPE 2           // waves per SIMD k_dec2 is register-budgeted for (2 workgroups/CU, 80 KB LDS each)
-#endif
 constexpr int SEG = 10;      // max tiles per segment (k_dec2)
 constexpr int SEG1 = 8;      // max tiles per segment (k_dec1)
 

@@ -1,0 +1,57 @@
+// Compile-time tuning knobs of the gfx950 kernels, in one place.  Each default is the measured optimum
+// of a same-box A/B (DESIGN.md sections 3-5, logs under profiles/); tools/build_obj_variants.sh builds a
+// one-object library with any of them overridden (-DNAME=value) for such an A/B.  The *_EXP switches are
+// timing probes that skip work and give wrong results; they are never set in a product build.
+#pragma once
+
+// ---- k_wino / k_wino_om (wino.hip)
+#ifndef WINO_OM
+#define WINO_OM 1          // offset/mask conv (f16x3) by k_wino_om; 0 = the per-slice k_wino
+#endif
+#ifndef WINO_OM_RING
+#define WINO_OM_RING 2     // k_wino_om B-operand blocks in flight (4: 158 -> 170-177 us, r02_wino_om_ring_ab.log)
+#endif
+#ifndef WINO_OM_SCHED
+#define WINO_OM_SCHED 1    // a scheduling barrier after every k_wino_om B block (keeps the B loads early)
+#endif
+#ifndef WINO_EXP
+#define WINO_EXP 0         // probes: 1 no LDS-DMA after the first phase, 2 no B refills, 3 no output exchange
+#endif
+
+// ---- k_dcn (dcn.hip): the DCN core of the two-kernel path and the _ext drop-in at the STIF shape
+#ifndef DCN_TH
+// waves per workgroup: 4 (8-row two-row tiles, two workgroups per CU whose barriers and memory waits
+// overlap): C0 L1 DCN 240 -> 223 us against 8 (r02_dcn_th_ab.log)
+#define DCN_TH 4
+#endif
+#ifndef DCN_M
+// staged margin (px) around the 3x3 footprint; samples beyond it use the global-load fallback.
+// C0 L1: margin 2 / 3 / 4 / 6 / 8 -> 248 / 250 / 257 / 266 / 289 us (r02_dcn_margin_ab.log)
+#define DCN_M 2
+#endif
+#ifndef DCN_MR2_MIN
+#define DCN_MR2_MIN 1024   // two-row kernel from this many workgroups (512 measured no faster)
+#endif
+
+// ---- k_dcn_sep (dcnsep.hip): the fused DCN_sep
+#ifndef DCNSEP_NW
+// waves (= output rows) per tile: 4 -> two 80-KB workgroups per CU; 8 -> one 152-KB workgroup staging the
+// next group pair ahead (slower)
+#define DCNSEP_NW 4
+#endif
+#ifndef DCNSEP_WPE
+#define DCNSEP_WPE 2       // waves per SIMD the kernel is register-budgeted for
+#endif
+#ifndef DCNSEP_EXP
+#define DCNSEP_EXP 0       // probes: 1 no phase 1, 3 no phase 2, 4 no fallback loads (r03_dcnsep_phase_probes.log)
+#endif
+
+// ---- k_dec1 / k_dec2 (decoder.hip)
+#ifndef DEC1_NW
+// waves per k_dec1 workgroup (~240 VGPRs: 2 waves/SIMD); 4-wave workgroups, 2 per CU (80 KB LDS each):
+// the two waves sharing a SIMD come from different workgroups (4 vs 8 within noise, r01_knob_sweep.log)
+#define DEC1_NW 4
+#endif
+#ifndef DEC2_WPE
+#define DEC2_WPE 2         // waves per SIMD k_dec2 is register-budgeted for (2 workgroups/CU, 80 KB LDS each)
+#endif

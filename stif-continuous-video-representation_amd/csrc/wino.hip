@@ -25,6 +25,7 @@
 #include "abi_util.h"
 #include "stif.h"
 #include "stif_common.h"
+#include "tuning.h"
 
 #include <algorithm>
 
@@ -45,9 +46,6 @@ constexpr int OM_RP = 320;                     // 16-B chunks per staged halo ro
 constexpr int EX_F = 2 * 2 * 2 * 1024;         // epilogue exchange: [wave 1|2][nt][b][32 tiles][32 co]
 constexpr int BUF_F = EX_F;                    // floats per buffer (32 KB)
 constexpr int WG_PER_CU = 2;
-#ifndef WINO_EXP
-#define WINO_EXP 0   // k_wino f16x3 timing probes (wrong results): 1 no LDS-DMA after the first phase, 2 no B refills, 3 no output exchange
-#endif
 static_assert(HR * OM_RP * 4 <= BUF_F && OM_RP % 8 == 0 && 35 * PITCH <= OM_RP, "staging image");
 
 // slot of halo column c in its (row, chunk, half) run: even columns first, then odd
@@ -499,12 +497,6 @@ template <int EPI>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_wino_om(stif_conv_args a,
                                                                                         int ntiles) {
   constexpr int SLICE_F = 8 * 8192;             // packed floats per 64-cout slice (8 chunks of 8 channels)
-#ifndef WINO_OM_RING
-#define WINO_OM_RING 2
-#endif
-#ifndef WINO_OM_SCHED
-#define WINO_OM_SCHED 1   // a scheduling barrier after every B block (keeps the B loads early)
-#endif
   constexpr int RING = WINO_OM_RING;            // B blocks in flight
   __shared__ __attribute__((aligned(16))) float smem[2 * BUF_F];
   float* const ex = smem + BUF_F;               // exchange image (buffer 1 once the A operands are built)
@@ -721,9 +713,6 @@ int num_cus() {
   return n;
 }
 
-#ifndef WINO_OM
-#define WINO_OM 1   // offset/mask conv (f16x3) by k_wino_om; 0 = the per-slice k_wino
-#endif
 
 template <int IN1, int EPI>
 int launch(const stif_conv_args& a, hipStream_t st) {
