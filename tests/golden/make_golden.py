@@ -25,6 +25,7 @@ Usage:  python tests/golden/make_golden.py             (model, window and per-op
         python tests/golden/make_golden.py single      (custom_video_test's single_forward, 11x13 pair)
         python tests/golden/make_golden.py c0          (BASELINE config C0: one full 128x128 pair, t=0.5)
         python tests/golden/make_golden.py gratings    (C0-sized moving-grating pair, analytic ground truth)
+        python tests/golden/make_golden.py c1          (BASELINE config C1: one full 256x256 pair, pinned pixels)
 """
 import json
 import os
@@ -369,6 +370,47 @@ def c0():
     print("c0 pair:", tuple(out.shape), float(out.min()), float(out.max()))
 
 
+def c1_pins(H=256, W=256, seed=7):
+    """(latent (y, x) positions, HR output (y, x) positions) pinned by c1(): the rows and columns where the
+    engine's tiles meet (Winograd: 4-row x 32-column tiles; DCN: 4 x 32; decoder: 32-pixel blocks) and
+    the frame's edges, plus random positions"""
+    rng = np.random.default_rng(seed)
+    ly = [0, 1, 3, 4, 127, 128, H - 2, H - 1]
+    lx = [0, 31, 32, 33, W - 1]
+    fy = np.concatenate([np.repeat(ly, W), np.tile(np.arange(H), len(lx)), rng.integers(0, H, 1024)])
+    fx = np.concatenate([np.tile(np.arange(W), len(ly)), np.repeat(lx, H), rng.integers(0, W, 1024)])
+    HH, WW = 4 * H, 4 * W
+    hy = [0, 1, 2, 3, 4, 511, 512, HH - 1]
+    hx = [0, 31, 32, 127, 128, WW - 1]
+    k = 256
+    oy = np.concatenate([np.repeat(hy, k), rng.integers(0, HH, len(hx) * k), rng.integers(0, HH, 4096)])
+    ox = np.concatenate([rng.integers(0, WW, len(hy) * k), np.repeat(hx, k), rng.integers(0, WW, 4096)])
+    return fy.astype(np.int64), fx.astype(np.int64), oy.astype(np.int64), ox.astype(np.int64)
+
+
+def c1():
+    """BASELINE.json configs[1] (C1) at full size: one 256x256 pair of bench.py's synthetic window (frames
+    0 and 1, torch.Generator seeds 1234 / 1235), 4x, t = 0.5, through the reference model; the latent
+    (reference ``self.feat``) and the 1024x1024 output are kept at the positions c1_pins() picks ->
+    c1_pair_pins.npz (the full tensors would be 50 MB + 12 MB)."""
+    if not os.path.isdir(REF):
+        print("reference absent; nothing to do")
+        return
+    model = _reference_model()
+    fr = []
+    for i in range(2):
+        g = torch.Generator().manual_seed(1234 + i)
+        fr.append(torch.rand(3, 256, 256, generator=g))
+    x = torch.stack(fr)[None]
+    with torch.no_grad():
+        out = model(x, [torch.tensor([[0.5]])])[0][0]
+    feat = model.feat[0]                        # [3, 64, 256, 256]
+    fy, fx, oy, ox = c1_pins()
+    np.savez_compressed(os.path.join(HERE, "c1_pair_pins.npz"), x=f32(x), feat_y=fy, feat_x=fx,
+                        feat=f32(feat[:, :, fy, fx]), out_y=oy, out_x=ox, out=f32(out[:, oy, ox]))
+    print("c1 pair:", tuple(out.shape), tuple(feat.shape), len(fy), len(oy))
+
+
 def gratings_c0():
     """The moving-grating pair of bench.py (frames 0 and 1 of bench.gratings at 128 x 128, SURVEY.md
     section 8d input (ii)) through the reference model, 4x, t = 0.5 -> gratings_128.npz; bench.py
@@ -395,6 +437,9 @@ if __name__ == "__main__":
         sys.exit(0)
     if sys.argv[1:] == ["c0"]:
         c0()
+        sys.exit(0)
+    if sys.argv[1:] == ["c1"]:
+        c1()
         sys.exit(0)
     if sys.argv[1:] == ["decoders"]:
         decoders()

@@ -63,6 +63,26 @@ def test_c0_full_pair_matches_reference(models, mf):
     assert abs(psnr(out.cpu().numpy()) - psnr(g["out"])) < 1e-3
 
 
+@pytest.mark.parametrize("mf", ["f16x3", "f32"])
+def test_c1_full_pair_matches_reference_at_pins(models, mf):
+    """BASELINE config C1 at full size: one 256x256 pair (bench.py's frames 0-1), 4x, t = 0.5, against the
+    reference model's own latent and 1024x1024 output (tests/golden/make_golden.py c1) at the positions
+    make_golden.c1_pins keeps: the rows / columns where the engine's conv, DCN and decoder tiles meet,
+    the frame edges, and random pixels -- elementwise |a - b| <= 1e-4 |b| + 1e-6."""
+    g = np.load(os.path.join(GOLD, "c1_pair_pins.npz"))
+    m = models[mf]
+    with torch.no_grad():
+        out = m(torch.from_numpy(g["x"]).cuda(), [torch.tensor([[0.5]])])[0][0]
+        feat = m.feat[0]                                       # [3, 64, 256, 256] (view of the NHWC latent)
+        fy, fx = torch.from_numpy(g["feat_y"]).cuda(), torch.from_numpy(g["feat_x"]).cuda()
+        oy, ox = torch.from_numpy(g["out_y"]).cuda(), torch.from_numpy(g["out_x"]).cuda()
+        ok, worst, dmax = elementwise_ok(feat[:, :, fy, fx], g["feat"])
+        assert ok, ("latent", worst, dmax)
+        assert tuple(out.shape) == (3, 1024, 1024)
+        ok, worst, dmax = elementwise_ok(out[:, oy, ox], g["out"])
+        assert ok, ("output", worst, dmax)
+
+
 def test_c0_window_pairs_equal_single_pairs(models):
     """The C0 7-frame window (bench's workload) batched = every pair run alone, bit for bit."""
     fr = synth(0, 7, 128, 128)
