@@ -178,6 +178,23 @@ def roofline(kname, kdesc, dom, peak_tflops, achieved_tflops, avg_ms, avg_flops,
     return rec
 
 
+def kernel_table(probe, mfma, top=4):
+    """The `top` launch kinds of one step by total time (HIP events on the launch stream, one untimed
+    step): launches, avg us, share of the step's kernel time, and each kind's roofline fraction on the
+    bound its intensity picks (roofline())."""
+    agg = probe.per_kind()
+    tot = sum(v[1] for v in agg.values()) or 1.0
+    out = []
+    for k, (nl, ms, fl, nb) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]:
+        kname, kdesc, peak = kernel_desc(k, mfma)
+        tf = fl / (ms * 1e-3) / 1e12 if ms else 0.0
+        r = roofline(kname, kdesc, k, peak, tf, ms / nl, fl / nl, nb / nl, nl, None)
+        out.append({"kind": list(k), "kernel": kname, "launches": nl, "avg_us": round(ms / nl * 1e3, 1),
+                    "share": round(ms / tot, 3), "bound": r["bound"], "frac": r["frac"],
+                    "hbm_frac": r["hbm_view"]["frac"], "mfma_frac": r["mfma_view"]["frac"]})
+    return out
+
+
 def hot_path_kernels(probe, mfma):
     """The north star's DCNv2 + implicit-decoder kernels, from the last warm-up step (HIP events on
     the launch stream): per kind avg time and TFLOP/s; for the DCN core also its algorithmic HBM
@@ -254,7 +271,7 @@ def cpu_model():
     return "unknown"
 
 
-CPU_SAMPLE = 128  # LR crop of the CPU-baseline sample (FLOP per output pixel does not depend on it)
+CPU_SAMPLE = 96   # LR crop of the CPU-baseline sample (FLOP per output pixel does not depend on it)
 
 
 def _oracle_timed(threads=None):
@@ -575,10 +592,21 @@ def main():
             a2.range_check = rc
             del model
             torch.cuda.empty_cache()
-            el, _, _, model, _, _, px = run_config(stif, sd, cfg, a2, 1, 0, device, None, mf, trace_dom=False)
+            el, _, _, model, fr2, tq2, px = run_config(stif, sd, cfg, a2, 1, 0, device, None, mf, trace_dom=False)
             key = f"{cfg}_{mf}" + ("_range_check_off" if rc == "off" else "")
             extras[key] = {"value": round(px * a2.steps / el / 1e6, 4), "unit": "Mpix/s",
                            "ms_per_step": round(el / a2.steps * 1e3, 3), "steps": a2.steps}
+            if cfg in ("c1", "c2") and mf == "f16x3":
+                # the config's own top kernels and their roofline fractions (one more, untimed step)
+                probe2 = KernelTimer(None)
+                with torch.no_grad():
+                    stif.ops.TRACE = probe2
+                    model.gen_feat_window(fr2)
+                    model.decoding(tq2)
+                    torch.cuda.synchronize()
+                    stif.ops.TRACE = None
+                extras[key]["top_kernels"] = kernel_table(probe2, mf)
+                del fr2
             if cfg in ("c3", "c4"):
                 extras[key]["workload"] = (f"{CONFIGS[cfg][0]}-frame {CONFIGS[cfg][1]}x{CONFIGS[cfg][2]} sequence "
                                            f"({CONFIGS[cfg][0] - 1} pairs), {CONFIGS[cfg][3]}x, t={CONFIGS[cfg][4]}, "
