@@ -327,9 +327,16 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_
       }
     } else {
       // one buffer: this pair's stage lands while the other workgroup on the CU computes
+#if DCNSEP_EXP == 5   // timing probe: pair 0's stage reused for every pair (no restaging)
+      if (pa == 0) {
+        stage_pair(pa, smem + OFF_XT, smem + OFF_XW);
+        lds_dma_barrier();
+      }
+#else
       if (pa) __syncthreads();   // every wave is done with the previous pair's buffer
       stage_pair(pa, smem + OFF_XT, smem + OFF_XW);
       lds_dma_barrier();
+#endif
     }
     const float* st = smem + ((PAIR_AHEAD && (pa & 1)) ? OFF_YT : OFF_XT);
     const float* sw = smem + ((PAIR_AHEAD && (pa & 1)) ? OFF_YW : OFF_XW);

@@ -43,7 +43,7 @@
 #define DCNSEP_WPE 2       // waves per SIMD the kernel is register-budgeted for
 #endif
 #ifndef DCNSEP_EXP
-#define DCNSEP_EXP 0       // probes: 1 no phase 1, 3 no phase 2, 4 no fallback loads (r03_dcnsep_phase_probes.log)
+#define DCNSEP_EXP 0       // probes: 1 no phase 1, 3 no phase 2, 4 no fallback loads, 5 no per-pair restaging
 #endif
 
 // ---- k_dec1 / k_dec2 (decoder.hip)
