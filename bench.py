@@ -575,6 +575,9 @@ def main():
             "roofline": roofline(kname, kdesc, dom, peak, achieved, avg_ms, avg_flops, avg_bytes, timer.seen,
                                  traffic, n_timed=n_launch),
             "hot_path_kernels": hot,
+            # every kernel kind's share of the last warm-up step and its roofline fraction (the headline
+            # `roofline` above is the dominant kind's, timed over the whole timed region)
+            "top_kernels": kernel_table(probe, args.mfma, top=6) if probe.rec else [],
         }
     if world == 1 and not args.no_extras:
         # the same workload with every contraction on fp32 MFMA and without the per-call f16x3 range sync,
