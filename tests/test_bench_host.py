@@ -1,0 +1,61 @@
+"""bench.py's host-side record logic on CPU (no GPU): the roofline record picks its bound by the kernel's
+arithmetic intensity against the ridge of the pipe it runs on, reports both views, and the per-kind
+table orders kinds by time; the moving-grating ground truth is the analytic pattern."""
+import importlib.util
+import os
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def bench():
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+class FakeTimer:
+    """per_kind() as KernelTimer returns it: kind -> [launches, total ms, total FLOP, total bytes]"""
+
+    def __init__(self, agg):
+        self.agg = agg
+        self.rec = [None]
+
+    def per_kind(self):
+        return self.agg
+
+
+def test_roofline_bound_follows_intensity(bench):
+    peak = bench.F16X3_PEAK_TFLOPS
+    # 96 FLOP/B (the trunk conv): below the f16x3 ridge (104 FLOP/B) -> HBM-bound, achieved = GB/s
+    r = bench.roofline("k", "d", ("wino",), peak, 300.0, 0.05, 96.0 * 1e9, 1e9, 45, None)
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s"
+    assert abs(r["achieved"] - 1e9 / 0.05e-3 / 1e9) < 1e-6 and abs(r["frac"] - r["hbm_view"]["frac"]) < 1e-9
+    # 420 FLOP/B (the fused DCN_sep): above the ridge -> MFMA-bound, achieved = TFLOP/s
+    r = bench.roofline("k", "d", ("dcnsep", 0), peak, 314.0, 0.36, 420.0 * 2.7e8, 2.7e8, 8, 291e6)
+    assert r["bound"] == "mfma" and r["unit"] == "TFLOP/s" and abs(r["frac"] - 314.0 / peak) < 1e-4
+    assert r["traffic"] == 291e6 and r["ridge_flop_per_byte"] == round(peak * 1e12 / 8e12, 1)
+
+
+def test_kernel_table_orders_by_time(bench):
+    agg = {("wino", 3, 1, 3, 0, 64): [45, 2.5, 45 * 21.7e9, 45 * 226e6],
+           ("dcnsep", 0): [8, 2.9, 8 * 113e9, 8 * 269e6],
+           ("dec2",): [1, 1.1, 3.0e14 * 1.1e-3, 0.0]}
+    t = bench.kernel_table(FakeTimer(agg), "f16x3", top=2)
+    assert [e["kind"] for e in t] == [["dcnsep", 0], ["wino", 3, 1, 3, 0, 64]]
+    assert abs(sum(e["share"] for e in bench.kernel_table(FakeTimer(agg), "f16x3")) - 1.0) < 1e-2
+    assert t[0]["bound"] == "mfma" and t[1]["bound"] == "hbm"
+    assert t[1]["frac"] == t[1]["hbm_frac"] and t[0]["frac"] == t[0]["mfma_frac"]
+
+
+def test_gratings_ground_truth_is_the_pattern(bench):
+    fr = bench.gratings(3, 2, 16, 24)                       # frames 3 and 4
+    assert fr.shape == (2, 3, 16, 24) and fr.dtype == np.float32
+    # at an integer time and the LR pixel grid (scale 1) the ground truth is the frame itself
+    gt = bench.gratings_gt(3, 1.0, 16, 24, 16, 24)
+    assert np.allclose(gt, fr[1], atol=1e-6)
+    assert 0.0 <= fr.min() and fr.max() <= 1.0
