@@ -207,3 +207,24 @@ def test_decoding_at_pixels_equals_full_decode(golden, sd, size):
         assert relmax(full[0][0], g["out"][2]) < 1e-5                    # t = 0.5
     else:
         assert relmax(full[0], g["out_scale_40x50"]) < 1e-5
+
+
+def test_c1_pin_fixture_is_consistent():
+    """c1_pair_pins.npz (make_golden.py c1: the reference's own 256x256 pair) keeps exactly the positions
+    make_golden.c1_pins() names -- tile seams, frame edges, random pixels -- with finite values, and its
+    input is bench.py's frames 0-1 (seeds 1234 / 1235)."""
+    import importlib.util
+    import torch
+    here = os.path.dirname(os.path.abspath(__file__))
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(here, "golden", "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    g = np.load(os.path.join(here, "golden", "c1_pair_pins.npz"))
+    fy, fx, oy, ox = mg.c1_pins()
+    for k, v in (("feat_y", fy), ("feat_x", fx), ("out_y", oy), ("out_x", ox)):
+        assert np.array_equal(g[k], v), k
+    assert g["feat"].shape == (3, 64, len(fy)) and g["out"].shape == (3, len(oy))
+    assert np.isfinite(g["feat"]).all() and np.isfinite(g["out"]).all()
+    for i in range(2):
+        fr = torch.rand(3, 256, 256, generator=torch.Generator().manual_seed(1234 + i)).numpy()
+        assert np.array_equal(g["x"][0, i], fr)
