@@ -396,9 +396,10 @@ def run_config(stif, sd, cfg, args, world, rank, device, dist, mfma, trace_dom=T
     exchange = args.halo == "exchange"
 
     def step():
+        # every rank calls gen_feat_shard (an empty shard only joins its first-call barrier)
+        P.gen_feat_shard(model, frames, rank, world, shards=shards, exchange=exchange)
         if frames is None:
             return None
-        P.gen_feat_shard(model, frames, rank, world, shards=shards, exchange=exchange)
         return model.decoding(tq, None if scale == 4.0 else (HH, WW))
 
     with torch.no_grad():
@@ -493,7 +494,9 @@ def main():
     td = None
     if args.backend == "gloo":
         local = local % max(1, torch.cuda.device_count())
-    if world > 1:
+    # a torchrun launch (MASTER_ADDR set) initialises the process group even at world size 1, so the
+    # N = 1 run of a scaling sweep goes through the same init / all_reduce / teardown as N > 1
+    if world > 1 or "MASTER_ADDR" in os.environ:
         import torch.distributed as td
         torch.cuda.set_device(local)
         if args.backend == "nccl":
@@ -579,7 +582,7 @@ def main():
             # `roofline` above is the dominant kind's, timed over the whole timed region)
             "top_kernels": kernel_table(probe, args.mfma, top=6) if probe.rec else [],
         }
-    if world == 1 and not args.no_extras:
+    if world == 1 and not args.no_extras and td is None:
         # the same workload with every contraction on fp32 MFMA and without the per-call f16x3 range sync,
         # then the other configs on this one GPU (C3 / C4: the whole sequence -- the 1-GPU denominators
         # of the strong-scaling runs), and the host-inclusive line (frames from host memory, outputs back)
@@ -618,7 +621,7 @@ def main():
         torch.cuda.empty_cache()
         extras[f"{args.config}_host_inclusive"] = host_inclusive(stif, sd, args.config, device, args.mfma)
         res["extra_lines"] = extras
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and td is None and not args.no_cpu_baseline:
         res["parity"], res["parity_gratings"] = parity_records(stif, sd, device, args.mfma)
         res["cpu_baseline"] = cpu_baseline()
     if rank == 0:

@@ -312,7 +312,8 @@ int stif_pack_dec_proj(const float* feat_w0, const float* feat_b0, const float* 
 /* lr_image bit 0 clear: P2..P4 without the image columns (decoding_test samples a high-resolution
  * image); lr_image | STIF_DEC_REVOLUTIONS: the sine-layer factor is omega_0 / (2 pi) instead of omega_0
  * (pre-activations in revolutions), as the decoder stages run with STIF_CONV_F16X3 expect -- set it iff
- * the mlp was packed with that flag; lr_image | STIF_PACK_F16X3: the PLAIN | F16X3 1x1 packing for stif_conv2d_nhwc with
+ * the mlp was packed with STIF_CONV_F16X3 (the stages cannot check the pairing: a mismatch gives wrong first-layer
+ * sines with no error, INTEGRATION.md "Decoder pairing rule"); lr_image | STIF_PACK_F16X3: the PLAIN | F16X3 1x1 packing for stif_conv2d_nhwc with
  * flags = STIF_CONV_F16X3 (split-fp16 k_conv1x1) */
 #define STIF_DEC_REVOLUTIONS 2
 int stif_pack_dec_proj_ex(const float* feat_w0, const float* feat_b0, const float* flow_w0,

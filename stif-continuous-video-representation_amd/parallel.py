@@ -38,6 +38,21 @@ def shard_for_rank(num_frames: int, world: int, rank: int) -> Tuple[int, int]:
     return pair_shards(num_frames, world)[rank]
 
 
+_WARM = set()
+
+
+def warm_group(group=None):
+    """One ``dist.barrier(group)`` per process group, the first time a shard step runs: every rank --
+    also one whose shard is empty and that never enters the exchange -- takes part, so a lazily
+    initialised NCCL communicator exists before the first ``batch_isend_irecv`` whatever the caller's
+    ``init_process_group`` did (no ``device_id`` needed)."""
+    key = id(group) if group is not None else None
+    if key in _WARM or not dist.is_initialized():
+        return
+    dist.barrier(group)
+    _WARM.add(key)
+
+
 def halo_exchange(first_frame_feats: Sequence[torch.Tensor], rank: int, world: int, group=None,
                   shards: Sequence[Tuple[int, int]] = None):
     """Send this rank's first-frame features to rank-1 and receive rank+1's (which is this rank's
@@ -49,10 +64,9 @@ def halo_exchange(first_frame_feats: Sequence[torch.Tensor], rank: int, world: i
 
     With the gloo backend device tensors are staged through host memory (gloo's send/recv move CPU
     tensors), so several ranks can share one GPU (the multi-rank GPU test).  With nccl the group's
-    communicator must exist before the first exchange -- ``init_process_group(..., device_id=...)``
-    (eager init, as bench.py does) or any collective run beforehand: ranks with an empty shard (or no
-    neighbour) never enter ``batch_isend_irecv``, and a lazily created NCCL communicator needs every
-    rank of the group in its first collective."""
+    communicator must exist before the first exchange: ranks with an empty shard (or no neighbour)
+    never enter ``batch_isend_irecv``, and a lazily created NCCL communicator needs every rank of the
+    group in its first collective -- ``gen_feat_shard`` calls ``warm_group`` (one barrier) first."""
     def has(r):
         return 0 <= r < world and (shards is None or shards[r][1] > shards[r][0])
 
@@ -75,13 +89,19 @@ def halo_exchange(first_frame_feats: Sequence[torch.Tensor], rank: int, world: i
     return recv
 
 
-def gen_feat_shard(model, frames: torch.Tensor, rank: int, world: int, group=None, shards=None,
+def gen_feat_shard(model, frames, rank: int, world: int, group=None, shards=None,
                    exchange: bool = True):
     """Encoder of this rank's shard of one sequence.  ``frames``: the shard's frames [a, b) (its
-    pairs' frames, boundary frame included).  With ``exchange``, the boundary frame's per-frame
-    features (L1/L2/L3 of conv_first + feature_extraction + pyramid, 336 B per LR pixel) come from
-    rank r+1 by ``halo_exchange`` instead of being recomputed; ``exchange=False`` recomputes them.
-    Leaves the latents of the shard's pairs in ``model.feat``."""
+    pairs' frames, boundary frame included), or None for an empty shard (more ranks than pairs: the
+    rank only joins the first call's ``warm_group`` barrier).  With ``exchange``, the boundary frame's
+    per-frame features (L1/L2/L3 of conv_first + feature_extraction + pyramid, 336 B per LR pixel)
+    come from rank r+1 by ``halo_exchange`` instead of being recomputed; ``exchange=False`` recomputes
+    them.  Every rank of the group calls it (collectively, the first time).  Leaves the latents of the
+    shard's pairs in ``model.feat``."""
+    if exchange and world > 1:
+        warm_group(group)
+    if frames is None:
+        return
     if not exchange or world == 1:
         model.gen_feat_window(frames)
         return

@@ -26,6 +26,8 @@ Usage:  python tests/golden/make_golden.py             (model, window and per-op
         python tests/golden/make_golden.py c0          (BASELINE config C0: one full 128x128 pair, t=0.5)
         python tests/golden/make_golden.py gratings    (C0-sized moving-grating pair, analytic ground truth)
         python tests/golden/make_golden.py c1          (BASELINE config C1: one full 256x256 pair, pinned pixels)
+        python tests/golden/make_golden.py c2|c3|c4    (the encoder's latent of one full-size C2 / C3 / C4 pair, pinned)
+        python tests/golden/make_golden.py chunk-check (the row-chunked DCN shim == the unchunked one)
 """
 import json
 import os
@@ -411,6 +413,137 @@ def c1():
     print("c1 pair:", tuple(out.shape), tuple(feat.shape), len(fy), len(oy))
 
 
+LARGE = {
+    # BASELINE configs whose encoder runs at sizes no test can run the reference at: (H, W, pins seed)
+    "c2": (540, 960, 11),      # configs[2]: the Vimeo-septuplet shape
+    "c3": (720, 1280, 13),     # configs[3]: one 720p pair of the 64-frame sequence (a rank's window)
+    "c4": (1080, 1920, 17),    # configs[4]: one 1080p pair
+}
+
+
+def large_pins(H, W, seed):
+    """Latent (y, x) positions pinned by large(): where the engine's tiles meet at every pyramid level
+    (Winograd / DCN 4-row x 32-column tiles at L1, their L2 / L3 images at 2x / 4x -- at 960 / 1280 /
+    1920 the L3 width 240 / 320 / 480 leaves a partial last 32-column tile at 960 and 1920), the
+    frame edges and random pixels: 8 positions on each seam row / column, plus 1,536 random ones."""
+    rng = np.random.default_rng(seed)
+    seam_y = sorted({0, 1, 2, 3, 4, 7, 8, 15, 16, H // 2 - 1, H // 2, H - 8, H - 5, H - 4, H - 3, H - 2, H - 1})
+    l3w = W // 4
+    seam_x = sorted({0, 1, 31, 32, 63, 64, 127, 128, W // 2, 4 * (l3w // 32) * 32 - 1, 4 * (l3w // 32) * 32,
+                     W - 33, W - 32, W - 2, W - 1})
+    k = 8
+    fy = np.concatenate([np.repeat(seam_y, k), rng.integers(0, H, len(seam_x) * k), rng.integers(0, H, 1536)])
+    fx = np.concatenate([rng.integers(0, W, len(seam_y) * k), np.repeat(seam_x, k), rng.integers(0, W, 1536)])
+    return fy.astype(np.int64), fx.astype(np.int64)
+
+
+def large(cfg):
+    """The encoder (LunaTokis.gen_feat, Sakuya_arch_test.py:313-362) of the reference on one full-size pair
+    of bench.py's synthetic frames (frames 0 and 1: torch.Generator seeds 1234 / 1235, torch.rand(3, H, W))
+    at a large BASELINE config; the latent (``self.feat`` [1, 3, 64, H, W]) is kept at large_pins() ->
+    <cfg>_pair_feat_pins.npz.  The frames are not stored: the GPU test regenerates them from the seeds.
+    The DCN shim runs in row chunks (dcn_v2_forward_cpu_chunked) so its columns buffer stays bounded."""
+    if not os.path.isdir(REF):
+        print("reference absent; nothing to do")
+        return
+    import time
+    H, W, seed = LARGE[cfg]
+    model = _reference_model()
+    sys.modules["_ext"].dcn_v2_forward = dcn_v2_forward_cpu_chunked
+    fr = []
+    for i in range(2):
+        g = torch.Generator().manual_seed(1234 + i)
+        fr.append(torch.rand(3, H, W, generator=g))
+    x = torch.stack(fr)[None]
+    t0 = time.time()
+    with torch.no_grad():
+        model.gen_feat(x)
+    feat = model.feat[0]                        # [3, 64, H, W]
+    fy, fx = large_pins(H, W, seed)
+    np.savez_compressed(os.path.join(HERE, f"{cfg}_pair_feat_pins.npz"), H=np.int64(H), W=np.int64(W),
+                        frame_seeds=np.array([1234, 1235], np.int64), feat_y=fy, feat_x=fx,
+                        feat=f32(feat[:, :, fy, fx]))
+    print(f"{cfg} pair latent:", tuple(feat.shape), len(fy), f"{time.time() - t0:.0f} s")
+
+
+def dcn_v2_forward_cpu_chunked(input, weight, bias, offset, mask, kh, kw, sh, sw, ph, pw, dh, dw, dg, rows=64):
+    """dcn_v2_forward_cpu over blocks of output rows (an output row depends only on its own offsets and mask
+    and on the input), each block gathering from the window of input rows its samples can reach; bounds
+    the columns buffer at 1080p.  Coordinates stay the image's own (same fp32 expressions as
+    dcn_v2_forward_cpu), so the result is the unchunked one."""
+    B, C, H, W = input.shape
+    Ho = (H + 2 * ph - (dh * (kh - 1) + 1)) // sh + 1
+    Wo = (W + 2 * pw - (dw * (kw - 1) + 1)) // sw + 1
+    if Ho <= rows or (kh, kw, sh, ph, dh) != (3, 3, 1, 1, 1):
+        return dcn_v2_forward_cpu(input, weight, bias, offset, mask, kh, kw, sh, sw, ph, pw, dh, dw, dg)
+    M = 8                                              # row margin: |row offset| < M (checked)
+    cpg = C // dg
+    K = kh * kw
+    rep = lambda t: t.repeat_interleave(cpg, dim=1)
+    off_all = offset.view(B, dg, K, 2, Ho, Wo)
+    assert float(off_all[:, :, :, 0].abs().max()) < M, "chunked DCN shim: row offsets beyond the margin"
+    msk_all = mask.view(B, dg, K, Ho, Wo)
+    outs = []
+    for r0 in range(0, Ho, rows):
+        r1 = min(Ho, r0 + rows)
+        n = r1 - r0
+        lo = max(0, r0 - ph - M)                       # input rows the block can reach: lo .. hi - 1
+        hi = min(H, r1 - 1 - ph + dh * (kh - 1) + M + 2)
+        img = input[:, :, lo:hi].reshape(B, C, (hi - lo) * W)
+        cols = torch.zeros(B, C, K, n, Wo, dtype=torch.float32)
+        h_in = (torch.arange(r0, r1) * sh - ph).view(1, 1, n, 1)
+        w_in = (torch.arange(Wo) * sw - pw).view(1, 1, 1, Wo)
+        for i in range(kh):
+            for j in range(kw):
+                k = i * kw + j
+                h_im = (h_in + i * dh).float() + off_all[:, :, k, 0, r0:r1]
+                w_im = (w_in + j * dw).float() + off_all[:, :, k, 1, r0:r1]
+                inside = (h_im > -1) & (w_im > -1) & (h_im < H) & (w_im < W)
+                h_low = torch.floor(h_im)
+                w_low = torch.floor(w_im)
+                lh = h_im - h_low
+                lw = w_im - w_low
+                hh = 1 - lh
+                hw = 1 - lw
+                h_low = h_low.long()
+                w_low = w_low.long()
+                h_high = h_low + 1
+                w_high = w_low + 1
+
+                def corner(hc, wc, ok):
+                    idx = ((hc.clamp(0, H - 1) - lo).clamp(0, hi - lo - 1) * W + wc.clamp(0, W - 1))
+                    idx = idx.repeat_interleave(cpg, dim=1).view(B, C, n * Wo)
+                    v = torch.gather(img, 2, idx).view(B, C, n, Wo)
+                    return torch.where(rep(ok), v, torch.zeros((), dtype=v.dtype))
+
+                v1 = corner(h_low, w_low, (h_low >= 0) & (w_low >= 0))
+                v2 = corner(h_low, w_high, (h_low >= 0) & (w_high <= W - 1))
+                v3 = corner(h_high, w_low, (h_high <= H - 1) & (w_low >= 0))
+                v4 = corner(h_high, w_high, (h_high <= H - 1) & (w_high <= W - 1))
+                val = rep(hh * hw) * v1 + rep(hh * lw) * v2 + rep(lh * hw) * v3 + rep(lh * lw) * v4
+                val = torch.where(rep(inside), val, torch.zeros((), dtype=val.dtype))
+                cols[:, :, k] = val * rep(msk_all[:, :, k, r0:r1])
+        cols = cols.view(B, C * K, n * Wo)
+        o = torch.einsum("ok,bkn->bon", weight.reshape(weight.shape[0], C * K), cols) + bias.view(1, -1, 1)
+        outs.append(o.view(B, -1, n, Wo))
+    return torch.cat(outs, dim=2)
+
+
+def chunk_check():
+    """dcn_v2_forward_cpu_chunked reproduces dcn_v2_forward_cpu bit for bit (offsets up to 6 px, a map whose
+    rows span several blocks incl. a partial last one and the image edges)."""
+    g = torch.Generator().manual_seed(5)
+    B, C, H, W, dg = 1, 16, 150, 40, 2
+    inp = torch.randn(B, C, H, W, generator=g)
+    wt = torch.randn(8, C, 3, 3, generator=g)
+    bs = torch.randn(8, generator=g)
+    off = (torch.rand(B, 2 * dg * 9, H, W, generator=g) * 12 - 6)
+    m = torch.rand(B, dg * 9, H, W, generator=g)
+    a = dcn_v2_forward_cpu(inp, wt, bs, off, m, 3, 3, 1, 1, 1, 1, 1, 1, dg)
+    b = dcn_v2_forward_cpu_chunked(inp, wt, bs, off, m, 3, 3, 1, 1, 1, 1, 1, 1, dg, rows=32)
+    print("chunked shim max |diff|:", float((a - b).abs().max()), "equal:", bool(torch.equal(a, b)))
+
+
 def gratings_c0():
     """The moving-grating pair of bench.py (frames 0 and 1 of bench.gratings at 128 x 128, SURVEY.md
     section 8d input (ii)) through the reference model, 4x, t = 0.5 -> gratings_128.npz; bench.py
@@ -440,6 +573,12 @@ if __name__ == "__main__":
         sys.exit(0)
     if sys.argv[1:] == ["c1"]:
         c1()
+        sys.exit(0)
+    if len(sys.argv) == 2 and sys.argv[1] in LARGE:
+        large(sys.argv[1])
+        sys.exit(0)
+    if sys.argv[1:] == ["chunk-check"]:
+        chunk_check()
         sys.exit(0)
     if sys.argv[1:] == ["decoders"]:
         decoders()

@@ -320,3 +320,45 @@ def test_single_forward_matches_reference_harness(stif, models):
         assert tuple(o.shape) == (1, 3, 48, 64)
         ok, worst, dmax = elementwise_ok(o[0], g["out"][i])
         assert ok, (i, worst, dmax)
+
+
+def test_f16x3_dcn_sep_range_flag_triggers_rerun(stif, sd, golden):
+    """The model's range guard through k_dcn_sep's own flag (advisor finding, round 3): only the first
+    fused DCN_sep launch sees a poisoned offset feature (one value of 5000, outside the split range);
+    that launch itself sets the status word, the call is re-run in fp32 (range_reruns + 1), and the
+    result equals an fp32-MFMA model's on the clean input."""
+    ops = stif.ops
+    orig = ops.dcn_sep
+    seen = []
+
+    def poisoned(groups, epi=0, status=None):
+        if not seen:
+            g0 = dict(groups[0])
+            f = g0["fea"].clone()
+            f.view(-1)[f.numel() // 3] = 5000.0
+            g0["fea"] = f
+            groups = [g0] + list(groups[1:])
+            if status is not None:
+                status.zero_()
+            orig(groups, epi=epi, status=status)
+            seen.append(None if status is None else int(status.item()))
+            return
+        orig(groups, epi=epi, status=status)
+
+    x = torch.from_numpy(golden["model_16x20"]["x"]).cuda()
+    m16 = stif.LunaTokis(64, 6, 8, 5, 40)
+    m32 = stif.LunaTokis(64, 6, 8, 5, 40, mfma="f32")
+    for m in (m16, m32):
+        m.load_state_dict(sd)
+    with torch.no_grad():
+        ref = m32(x, [0.5])[0]
+        ops.dcn_sep = poisoned
+        try:
+            with warnings.catch_warnings():
+                warnings.simplefilter("ignore")
+                out = m16(x, [0.5])[0]
+        finally:
+            ops.dcn_sep = orig
+    assert seen == [1], seen
+    assert m16.range_reruns == 1
+    assert torch.equal(out, ref)

@@ -565,3 +565,29 @@ def test_dcn_sep_fused_equals_two_kernel_path(ops, L):
     ops.dcn([dict(layer=core2, inp=nhwc(x), offmask=omap, out=b)])
     ref = O.dcn_sep(x, fea, sdx, "x")
     assert relmax(to_nchw(a), ref) < RTOL and relmax(to_nchw(b), ref) < RTOL
+
+
+@pytest.mark.parametrize("which", ["fea", "inp"])
+def test_dcn_sep_fused_reports_range(ops, L, which):
+    """k_dcn_sep's own range reporting (advisor finding, round 3): one offset-feature value (phase 1: the
+    offset/mask sums go non-finite, the `chk` sum) or one DCN-input value (phase 2: the output goes
+    non-finite, `chk2`) far outside the split-fp16 range sets the status word; the same call in range
+    leaves it 0."""
+    H, W, B = 20, 40, 2
+    sdx = _dcnsep_weights(40, 2.0)
+    x = rnd(B, 64, H, W, seed=41)
+    fea = rnd(B, 64, H, W, seed=42)
+    om, core = _dcnsep_layers(ops, L, sdx)
+    st = torch.zeros(1, dtype=torch.int32, device="cuda")
+    out = torch.empty(B, H, W, 64, device="cuda")
+    xi, fi = nhwc(x), nhwc(fea)
+    ops.dcn_sep([dict(om_layer=om, layer=core, fea=fi, inp=xi, out=out)], status=st)
+    assert int(st.item()) == 0
+    if which == "fea":
+        fi = fi.clone()
+        fi[1, 7, 13, 5] = 5000.0
+    else:
+        xi = xi.clone()
+        xi[0, 11, 30, 60] = 5000.0
+    ops.dcn_sep([dict(om_layer=om, layer=core, fea=fi, inp=xi, out=out)], status=st)
+    assert int(st.item()) == 1, which

@@ -103,3 +103,76 @@ def test_halo_exchange_neighbours(nframes, world):
             assert got[r] == [nxt[0] * 10 + lv for lv in range(3)], (r, got[r])
         else:
             assert got[r] == [-1.0], (r, got[r])
+
+
+@pytest.mark.parametrize("nframes,world", [(64, 8), (9, 8)], ids=["c3_plan", "c4_plan"])
+def test_halo_exchange_world8_plans(nframes, world):
+    """The exact shard plans of the 8-GPU configs (BASELINE configs[3] / [4]): C3 = 64 frames -> 63 pairs as
+    8,8,8,8,8,8,8,7; C4 = 9 frames -> one pair per rank.  Every rank receives its last frame's features
+    from its right neighbour (whose first frame it is), rank 7 receives nothing."""
+    import stif_pkg
+    P = stif_pkg.load().parallel
+    shards = P.pair_shards(nframes, world)
+    sizes = [b - a - 1 for a, b in shards]
+    assert sizes == ([8] * 7 + [7] if nframes == 64 else [1] * 8), sizes
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_halo_worker, args=(world, _free_port(), nframes, d), nprocs=world, join=True)
+        got = [np.load(os.path.join(d, f"h{r}.npy")).tolist() for r in range(world)]
+    for r in range(world - 1):
+        assert got[r] == [shards[r + 1][0] * 10 + lv for lv in range(3)], (r, got[r])
+        assert shards[r + 1][0] == shards[r][1] - 1
+    assert got[world - 1] == [-1.0]
+
+
+class _FakeModel:
+    """Stands in for LunaTokis in gen_feat_shard: per-frame 'features' tagged with the global frame index."""
+
+    def __init__(self, a):
+        self.a = a
+        self.window = None
+
+    def frame_features(self, frames):
+        idx = frames[:, 0, 0, 0]
+        return tuple(idx.view(-1, 1, 1, 1).repeat(1, 2, 2, 3) * 10 + lv for lv in range(3))
+
+    def gen_feat_window(self, frames, frame_feats=None):
+        self.window = (frames[:, 0, 0, 0].tolist(), None if frame_feats is None else
+                       [t[:, 0, 0, 0].tolist() for t in frame_feats])
+
+
+def _shard_worker(rank, world, port, nframes, outdir):
+    """gen_feat_shard on every rank, empty shards included (frames=None): the first call's warm_group
+    barrier is collective, then the halo exchange runs among the ranks with frames."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import stif_pkg
+    P = stif_pkg.load().parallel
+    shards = P.pair_shards(nframes, world)
+    a, b = shards[rank]
+    frames = torch.arange(a, b, dtype=torch.float32).view(-1, 1, 1, 1).repeat(1, 3, 2, 2) if b > a else None
+    m = _FakeModel(a)
+    for _ in range(2):                                   # the barrier runs once per group
+        P.gen_feat_shard(m, frames, rank, world, shards=shards, exchange=True)
+    np.save(os.path.join(outdir, f"s{rank}.npy"), np.array(m.window, dtype=object), allow_pickle=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("nframes,world", [(3, 4), (9, 8)], ids=["empty_shards", "c4_plan"])
+def test_gen_feat_shard_all_ranks(nframes, world):
+    """gen_feat_shard called by every rank (bench.py's step): ranks with frames get their window's
+    features with the boundary frame's from the right neighbour; empty-shard ranks return after the
+    one-time barrier and nobody hangs."""
+    import stif_pkg
+    P = stif_pkg.load().parallel
+    shards = P.pair_shards(nframes, world)
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_shard_worker, args=(world, _free_port(), nframes, d), nprocs=world, join=True)
+        got = [np.load(os.path.join(d, f"s{r}.npy"), allow_pickle=True) for r in range(world)]
+    for r, (a, b) in enumerate(shards):
+        if b <= a:
+            assert got[r].tolist() is None or got[r].size == 0 or got[r].tolist() == [None, None], got[r]
+            continue
+        frames_seen, feats = got[r].tolist()
+        assert frames_seen == list(range(a, b))
+        assert feats is not None and feats[0] == [10.0 * f for f in range(a, b)], (r, feats)

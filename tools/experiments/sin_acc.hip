@@ -1,6 +1,9 @@
 // Accuracy of sine evaluations on gfx950 vs a double-precision sin of the same fp32 argument:
 // the previous polynomial sine, the bare hardware v_sin_f32 (argument in revolutions), a 2-part
-// Cody-Waite / magic-rounding polynomial variant, and stif_sin (reduction by 2 pi, then v_sin_f32).  Max abs error per |x| band.
+// Cody-Waite / magic-rounding polynomial variant, and the two product sines of stif_common.h:
+// stif_sin_poly (the fp32-operand decoder: pi/2 Cody-Waite + Taylor) and stif_sin_rev (the f16x3
+// decoder: its argument is already in revolutions, omega / 2 pi folded into the packed weights, so it
+// is fed x / 2 pi here, rounded to fp32 as the packed weights round it).  Max abs error per |x| band.
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include <cstdio>
@@ -40,7 +43,8 @@ __global__ void k(const float* x, float* o, int n) {
   if (i < n) {
     const float v = x[i];
     o[i] = sin_poly(v);
-    o[3 * n + i] = stif_sin(v);
+    o[3 * n + i] = stif_sin_poly(v);
+    o[4 * n + i] = stif_sin_rev(v * 0.159154943091895335769f);
     o[n + i] = __builtin_amdgcn_sinf(v * 0.159154943091895335769f);
     o[2 * n + i] = sin_cw2(v);
   }
@@ -48,17 +52,17 @@ __global__ void k(const float* x, float* o, int n) {
 
 int main() {
   const int n = 1 << 24;
-  std::vector<float> x(n), o(4 * (size_t)n);
+  std::vector<float> x(n), o(5 * (size_t)n);
   for (int i = 0; i < n; ++i) x[i] = -3000.f + 6000.f * (float)((i * 2654435761u) % n) / n;
   float *dx, *dout;
   hipMalloc(&dx, n * 4);
-  hipMalloc(&dout, 4 * (size_t)n * 4);
+  hipMalloc(&dout, 5 * (size_t)n * 4);
   hipMemcpy(dx, x.data(), n * 4, hipMemcpyHostToDevice);
   k<<<(n + 255) / 256, 256>>>(dx, dout, n);
-  hipMemcpy(o.data(), dout, 4 * (size_t)n * 4, hipMemcpyDeviceToHost);
+  hipMemcpy(o.data(), dout, 5 * (size_t)n * 4, hipMemcpyDeviceToHost);
   const float bands[] = {1, 4, 16, 64, 256, 1000, 3000};
-  const char* names[] = {"poly", "v_sin_f32", "cw2_magic", "stif_sin"};
-  for (int m = 0; m < 4; ++m) {
+  const char* names[] = {"poly", "v_sin_f32", "cw2_magic", "sin_poly", "sin_rev"};
+  for (int m = 0; m < 5; ++m) {
     double e[7] = {0};
     for (int i = 0; i < n; ++i) {
       const double ref = std::sin((double)x[i]);
