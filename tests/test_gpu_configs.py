@@ -362,3 +362,43 @@ def test_f16x3_dcn_sep_range_flag_triggers_rerun(stif, sd, golden):
     assert seen == [1], seen
     assert m16.range_reruns == 1
     assert torch.equal(out, ref)
+
+
+LARGE_WINDOWS = {
+    # fixture: frames in the window (pairs chosen so chunk_px = 2^21 LR pixels splits the encoder's pairs:
+    # C2 5 pairs -> chunks of 3 + 2, C3 3 pairs -> 2 + 1, C4 2 pairs -> 1 + 1)
+    "c2": 6,
+    "c3": 4,
+    "c4": 3,
+}
+
+
+@pytest.mark.parametrize("mf", ["f16x3", "f32"])
+@pytest.mark.parametrize("cfg", sorted(LARGE_WINDOWS))
+def test_large_config_latent_matches_reference_at_pins(models, cfg, mf):
+    """BASELINE configs[2..4] at full size: the reference's own encoder (gen_feat, Sakuya_arch_test.py:313-362)
+    run on bench.py's frames 0-1 at 540x960 / 720x1280 / 1080x1920 (tests/golden/make_golden.py c2|c3|c4)
+    against pair 0 of a multi-pair window of this engine -- the window is long enough that chunk_px splits
+    its pairs into several encoder passes -- at the tile seams of every pyramid level (incl. the partial last
+    32-column L3 tile at 960 / 1920), the frame edges and random pixels, elementwise
+    |a - b| <= 1e-4 |b| + 1e-6."""
+    path = os.path.join(GOLD, f"{cfg}_pair_feat_pins.npz")
+    if not os.path.exists(path):
+        pytest.skip(f"{cfg} fixture not generated")
+    g = np.load(path)
+    H, W = int(g["H"]), int(g["W"])
+    m = models[mf]
+    n = LARGE_WINDOWS[cfg]
+    per = max(1, m.chunk_px // (H * W))
+    assert per < n - 1, "the window must span more than one encoder chunk"
+    fr = synth(0, n, H, W)
+    with torch.no_grad():
+        m.gen_feat_window(fr)
+        feat = m.feat[0]                                       # pair 0: [3, 64, H, W]
+        fy, fx = torch.from_numpy(g["feat_y"]).cuda(), torch.from_numpy(g["feat_x"]).cuda()
+        got = feat[:, :, fy, fx]
+        m._feat = None
+    ok, worst, dmax = elementwise_ok(got, g["feat"])
+    assert ok, (cfg, mf, worst, dmax)
+    del fr, feat, got
+    torch.cuda.empty_cache()
