@@ -57,10 +57,6 @@ def kernel_desc(kind, mfma="f32"):
             return ("k_wino_om<4>", f"3x3 64->{cout} conv, EPI_OFFMASK, Winograd F(2x2,3x3) on split-fp16 MFMA, all "
                     "couts per tile (3 fp16 products per fp32-class product); algorithmic = direct-conv FLOPs, peak = "
                     "fp16 MFMA dense peak / 3 x 36/16", F16X3_PEAK_TFLOPS * WINO_GAIN)
-        if f16 and not in1 and cout == 64 and epi <= 3:
-            return (f"k_wino_ws<{epi}>", f"3x3 64->64 conv, EPI_{EPI_NAMES[epi]}, weight-stationary Winograd F(2x2,3x3) "
-                    "on split-fp16 MFMA (3 fp16 products per fp32-class product); algorithmic = direct-conv FLOPs, "
-                    "peak = fp16 MFMA dense peak / 3 x 36/16", F16X3_PEAK_TFLOPS * WINO_GAIN)
         if f16:
             return (f"k_wino<{in1}, {epi}, 1>", f"3x3 {64 * (2 if in1 else 1)}->{cout} conv, EPI_{EPI_NAMES[epi]}, "
                     "Winograd F(2x2,3x3) on split-fp16 MFMA (3 fp16 products per fp32-class product); algorithmic = "

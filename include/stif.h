@@ -83,9 +83,6 @@ typedef struct {
  * outside it, and an activation outside it turns the outputs it feeds into NaN/inf, which the
  * kernels report through the `status` word (the host then re-runs the call in fp32). */
 #define STIF_CONV_F16X3 1
-/* stif_conv_args.flags (test / benchmark aid): keep stif_conv3x3_wino on the generic per-slice kernel for
- * the 64 -> 64 f16x3 convs it otherwise runs weight-stationary (k_wino_ws; bit-identical results). */
-#define STIF_CONV_GENERIC 2
 
 int stif_conv2d_nhwc(const stif_conv_args* args, void* stream);
 

@@ -16,7 +16,6 @@ EPI_NONE, EPI_LRELU, EPI_RELU, EPI_RES, EPI_OFFMASK, EPI_LSTM = range(6)
 PACK_PLAIN, PACK_OFFMASK, PACK_LSTM, PACK_WINO, PACK_WINO_OFFMASK, PACK_WINO_LSTM, PACK_DCNSEP, PACK_DCNPAIR = range(8)
 PACK_F16X3 = 16          # OR'ed into a PACK_WINO* mode (stif.h STIF_PACK_F16X3)
 CONV_F16X3 = 1           # stif_conv_args.flags
-CONV_GENERIC = 2         # stif_conv_args.flags: 64 -> 64 f16x3 Winograd on the generic kernel (test aid)
 DEC_REVOLUTIONS = 2      # stif_pack_dec_proj_ex lr_image bit (stif.h STIF_DEC_REVOLUTIONS)
 
 _P = C.c_void_p

@@ -14,9 +14,6 @@
 #ifndef WINO_OM_SCHED
 #define WINO_OM_SCHED 1    // a scheduling barrier after every k_wino_om B block (keeps the B loads early)
 #endif
-#ifndef WINO_WS
-#define WINO_WS 1          // 64 -> 64 f16x3 convs by the weight-stationary k_wino_ws (0: k_wino)
-#endif
 #ifndef WINO_EXP
 #define WINO_EXP 0         // probes: 1 no LDS-DMA after the first phase, 2 no B refills, 3 no output exchange
 #endif

@@ -45,10 +45,7 @@ constexpr int PITCH = 2 * PSUB + 1;
 constexpr int OM_RP = 320;                     // 16-B chunks per staged halo row (35 x PITCH + 5)
 constexpr int EX_F = 2 * 2 * 2 * 1024;         // epilogue exchange: [wave 1|2][nt][b][32 tiles][32 co]
 constexpr int BUF_F = EX_F;                    // floats per buffer (32 KB)
-#ifndef WINO_WGCU
-#define WINO_WGCU 2
-#endif
-constexpr int WG_PER_CU = WINO_WGCU;
+constexpr int WG_PER_CU = 2;
 static_assert(HR * OM_RP * 4 <= BUF_F && OM_RP % 8 == 0 && 35 * PITCH <= OM_RP, "staging image");
 
 // slot of halo column c in its (row, chunk, half) run: even columns first, then odd
@@ -706,220 +703,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// k_wino_ws: weight-stationary f16x3 Winograd for the 64 -> 64 convs (the recon_trunk ResidualBlock_noBN
-// pair, module_util.py:48-52; feature_extraction, the pyramid / PCD 64 -> 64 convs).  k_wino streams the
-// 256 KB of transformed, split weights of a 64-cout slice from L2 for every 4 x 32 tile (4 waves x 64 KB,
-// 2 KB per output pixel -- four times the activation bytes) and spends half its vector-memory
-// instructions on it.  Here the weights stay in registers for the whole persistent launch: 8 waves, wave
-// (i, u) = transform row i x cout half u holds U[i][j][32 couts of half u][64 cin] for all j as MFMA B
-// fragments (4 chunk pairs x 4 j x h / l planes = 128 VGPRs), and its accumulators cover one cout half (4 j
-// x 16 = 64 VGPRs).  A tile's per-wave work is then the input transform + split of row i (duplicated by
-// the two cout halves), 48 MFMAs and the output-transform exchange; the only vector-memory traffic left is
-// the staging LDS-DMA, the residual and the output.  One 512-thread workgroup per CU (2 waves per SIMD,
-// 128 KB LDS: two staging buffers + a one-round exchange image for both cout halves), two barriers per tile;
-// the weights are reloaded only when a launch group's tiles change weight set.
-template <int EPI>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_wino_ws(stif_conv_args a,
-                                                                                        int ntiles) {
-  __shared__ __attribute__((aligned(16))) float smem[4 * BUF_F];   // staging 0 | staging 1 | exchange [nt 2]
-  float* const ex_all = smem + 2 * BUF_F;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wi = wv & 3;                                     // transform row i
-  const int u = wv >> 2;                                     // cout half of this wave's MFMAs
-  const int hf = lane >> 5;
-  const int tl = lane & 31;
-  const int tyl = tl >> 4, txl = tl & 15;
-  const int tiles_x = (a.Wo + 31) >> 5;
-  const int tiles_y = (a.Ho + WR - 1) / WR;
-  const int H = a.H, W = a.W;
-
-  auto tile_of = [&](int T) {
-    Tile t;
-    t.slice = 0;
-    const int x = T % tiles_x;
-    int r = T / tiles_x;
-    const int y = r % tiles_y;
-    r /= tiles_y;
-    t.g = r / a.nitems;
-    t.n = r - t.g * a.nitems;
-    t.oy0 = y * WR;
-    t.ox0 = x * 32;
-    t.src0 = a.in0[t.g] + (size_t)t.n * a.in0_item;
-    t.src1 = t.src0;
-    return t;
-  };
-  const int lpx = lane / 9, lck = lane - 9 * (lane / 9);
-  auto stage = [&](const Tile& t, int p, int buf) {   // k_wino's image: 30 LDS-DMA instructions over 8 waves
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)t.src0, (short)0, (int)((size_t)H * W * 256), 0x00020000);
-    stage_image(rs, smem + buf * BUF_F, t.oy0 - 1, t.ox0 - 1, H, W, 64, p * 32, wv, 8, lpx, lck);
-  };
-
-  const int rA = (wi == 0) ? 0 : (wi == 2 ? 2 : 1);
-  const int rB = (wi == 3) ? 3 : (wi == 2 ? 1 : 2);
-  const float sB = (wi == 1) ? 1.f : -1.f;
-  const int s0 = col_slot(0) + txl, s1 = col_slot(1) + txl, s2 = col_slot(2) + txl, s3 = col_slot(3) + txl;
-  auto xread = [&](const float* buf, int s, f32x4* rd) {
-    const float* ra = buf + ((2 * tyl + rA) * OM_RP + 2 * s + hf) * 4;
-    const float* rb = buf + ((2 * tyl + rB) * OM_RP + 2 * s + hf) * 4;
-    rd[0] = ld4(ra + s0 * PITCH * 4); rd[1] = ld4(rb + s0 * PITCH * 4);
-    rd[2] = ld4(ra + s1 * PITCH * 4); rd[3] = ld4(rb + s1 * PITCH * 4);
-    rd[4] = ld4(ra + s2 * PITCH * 4); rd[5] = ld4(rb + s2 * PITCH * 4);
-    rd[6] = ld4(ra + s3 * PITCH * 4); rd[7] = ld4(rb + s3 * PITCH * 4);
-  };
-  // (B^T d)_i for the 4 patch columns; column j of B^T d B is then t0 - t2, t1 + t2, t2 - t1, t1 - t3
-  auto xform_t = [&](const f32x4* rd, f32x4* t) {
-    t[0] = rd[0] + sB * rd[1];
-    t[1] = rd[2] + sB * rd[3];
-    t[2] = rd[4] + sB * rd[5];
-    t[3] = rd[6] + sB * rd[7];
-  };
-  auto vcol = [](const f32x4* t, int j) -> f32x4 {
-    return j == 0 ? t[0] - t[2] : j == 1 ? t[1] + t[2] : j == 2 ? t[2] - t[1] : t[1] - t[3];
-  };
-
-  // weights of wave (i, u): B fragment (chunk pair q, j, plane) of the STIF_PACK_WINO | F16X3 packing at
-  // q * 16384 + i * 4096 + ((j * 2 + u) * 2 + plane) * 256 + lane * 4 floats
-  f16x8 wh[4][4], wl[4][4];
-  int wg = -1;
-  auto load_w = [&](int g) {
-    const float* b = a.w[g] + wi * 4096 + lane * 4;
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        wh[q][j] = ldh8(b + q * 16384 + ((j * 2 + u) * 2) * 256);
-        wl[q][j] = ldh8(b + q * 16384 + ((j * 2 + u) * 2 + 1) * 256);
-      }
-  };
-
-  // XCD-aware persistent schedule (k_wino's): XCD x owns a contiguous tile range
-  const int xcd = blockIdx.x & 7, nl = gridDim.x >> 3;
-  const int per = (ntiles + 7) >> 3;
-  const int tend = min((xcd + 1) * per, ntiles);
-  int T = xcd * per + (blockIdx.x >> 3);
-  if (T >= tend) return;
-  Tile cur = tile_of(T);
-  stage(cur, 0, 0);
-  load_w(cur.g);
-  wg = cur.g;
-  lds_dma_barrier();
-
-  // epilogue thread mapping: cout half nt, quad c4, tile column oxl; rows k = 0..3
-  const int nt = tid >> 8, c4 = tid & 7, oxl = (tid >> 3) & 31;
-  const int bb = oxl & 1, txo = oxl >> 1;
-  constexpr int EW = 4 * 2 * 1024;                            // exchange floats per cout half: [i][b][32][32]
-  for (;;) {
-    const int Tn = T + nl;
-    const bool has_next = Tn < tend;
-    const Tile nxt = tile_of(has_next ? Tn : T);
-    if (cur.g != wg) {                                       // a launch group's next weight set
-      load_w(cur.g);
-      wg = cur.g;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    f32x16 acc[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] = f32x16{0};
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      const float* buf = smem + p * BUF_F;
-      f32x4 rd[8];
-      xread(buf, 0, rd);
-      // phase 1 of this tile into buffer 1 while phase 0 computes; the next tile's phase 0 into buffer 0
-      // while phase 1 computes (buffer 0 is free: every wave passed the barrier after phase 0)
-      if (p == 0) stage(cur, 1, 1);
-      else if (has_next) stage(nxt, 0, 0);
-#pragma unroll
-      for (int sp = 0; sp < 2; ++sp) {
-        f32x4 ta[4], tb[4];
-        if (sp) xread(buf, 2, rd);
-        xform_t(rd, ta);
-        xread(buf, 2 * sp + 1, rd);
-        xform_t(rd, tb);
-        const int q = p * 2 + sp;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          f16x8 ah, al;
-          split_f16x3(vcol(ta, j), vcol(tb, j), ah, al);
-          acc[j] = mfma16h(ah, wh[q][j], acc[j]);
-          acc[j] = mfma16h(ah, wl[q][j], acc[j]);
-          acc[j] = mfma16h(al, wh[q][j], acc[j]);
-        }
-      }
-      if (p == 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // phase 1 landed
-        __syncthreads();
-      }
-    }
-
-    // ---- output transform (k_wino's exchange, both cout halves in one round): wave (i, u) writes
-    // P_i = [acc0 + acc1 + acc2, acc1 - acc2 - acc3] into the half-u image
-    const int ox = cur.ox0 + oxl;
-    const size_t slab = (size_t)a.Ho * a.Wo * 64;
-    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(a.out[cur.g] + (size_t)cur.n * a.out_item), (short)0, (int)(slab * 4), 0x00020000);
-    auto voff = [&](int k) -> unsigned {
-      const int oy = cur.oy0 + k;
-      const bool ok = (oy < a.Ho) & (ox < a.Wo);
-      return ok ? (unsigned)(((oy * a.Wo + ox) * 64 + nt * 32 + c4 * 4) * 4) : 0x80000000u;
-    };
-    f32x4 rv[4];
-    if (EPI == STIF_EPI_RES) {   // the youngest vector-memory operations: waited for at their use
-      const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(a.res[cur.g] + (size_t)cur.n * a.res_item), (short)0, (int)(slab * 4), 0x00020000);
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        rv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, voff(k), 0, 0));
-    }
-    {
-      float* const ex = ex_all + u * EW;
-      const f32x16 y0 = acc[0] + acc[1] + acc[2];
-      const f32x16 y1 = acc[1] - acc[2] - acc[3];
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const int fl = (hf ^ b) * 32;
-        float* wb = ex + ((wi * 2 + b) * 32 + 4 * hf) * 32 + tl;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) wb[((r & 3) + 8 * (r >> 2)) * 32 + ((r & 1) ? -fl : fl)] = b ? y1[r] : y0[r];
-      }
-    }
-    // the next tile's phase 0 (buffer 0) has landed -- every older vector-memory op; the residual loads
-    // (4, the youngest) stay in flight
-    if (EPI == STIF_EPI_RES) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const float* ex = ex_all + nt * EW;
-    const int cob = nt * 32 + c4 * 4;
-    const f32x4 bv = ld4(a.bias[cur.g] + cob);
-    float chk = 0.f;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float* rbase = ex + (bb * 32 + (txo ^ (((txo >> 2) ^ bb) & 1))) * 32 + c4 * 4 + (k >> 1) * 512;
-      const f32x4 p1 = ld4(rbase + 1 * 2048), p2 = ld4(rbase + 2 * 2048);
-      const f32x4 pe = ld4(rbase + ((k & 1) ? 3 : 0) * 2048);
-      f32x4 y = (k & 1) ? (p1 - p2 - pe) : (pe + p1 + p2);
-      y = y * F16X3_UNSCALE + bv;   // exact power of two
-      chk += (y[0] + y[1]) + (y[2] + y[3]);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (EPI == STIF_EPI_LRELU) y[e] = lrelu01(y[e]);
-        if (EPI == STIF_EPI_RELU) y[e] = fmaxf(y[e], 0.f);
-      }
-      if (EPI == STIF_EPI_RES) y += rv[k];
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, y), ro,
-                                             voff(k), 0, 0);
-    }
-    report_range(a.status, not_finite(chk));   // a non-finite output makes the sum non-finite
-    if (!has_next) break;
-    T = Tn;
-    cur = nxt;
-  }
-}
-
 int num_cus() {
   static int n = 0;
   if (!n) {
@@ -942,13 +725,6 @@ int launch(const stif_conv_args& a, hipStream_t st) {
     const long long sp = tiles / ((a.cout + 63) / 64);   // spatial tiles: all couts per workgroup
     const int g2 = 8 * (int)std::min<long long>((sp + 7) / 8, (long long)WG_PER_CU * num_cus() / 8);
     hipLaunchKernelGGL((k_wino_om<EPI>), dim3(g2), dim3(256), 0, st, a, (int)sp);
-    return stif_check_launch("stif_conv3x3_wino");
-  }
-  if constexpr (WINO_WS && IN1 == 0 && EPI <= STIF_EPI_RES)
-  if ((a.flags & STIF_CONV_F16X3) && !(a.flags & STIF_CONV_GENERIC) && a.C0 == 64 && a.cout == 64) {
-    // 64 -> 64: weights held in registers, one 512-thread workgroup per CU
-    const int g1 = 8 * (int)std::min<long long>((tiles + 7) / 8, (long long)num_cus() / 8);
-    hipLaunchKernelGGL((k_wino_ws<EPI>), dim3(g1), dim3(512), 0, st, a, (int)tiles);
     return stif_check_launch("stif_conv3x3_wino");
   }
   const int grid = 8 * (int)std::min<long long>((tiles + 7) / 8, (long long)WG_PER_CU * num_cus() / 8);

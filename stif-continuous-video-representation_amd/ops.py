@@ -83,11 +83,6 @@ def _split_by_mode(groups, key):
     return [f16, [g for g in groups if not g[key].mode & L.PACK_F16X3]] if 0 < len(f16) < len(groups) else None
 
 
-# test / benchmark aid: run the 64 -> 64 f16x3 Winograd convs on the generic per-slice kernel instead of
-# the weight-stationary one (stif.h STIF_CONV_GENERIC; bit-identical)
-WINO_GENERIC = False
-
-
 def conv2d(groups, *, epi=L.EPI_NONE, in1_mode=0, in1_scale=1.0, stride=None, status=None):
     """groups: list of dicts {layer: PackedConv, in0, [in1], out, [res], [out2]} with tensors
     [nitems, H, W, C].  All groups share shapes and item strides.  status: optional int32 device
@@ -137,7 +132,7 @@ def conv2d(groups, *, epi=L.EPI_NONE, in1_mode=0, in1_scale=1.0, stride=None, st
     if any(((g["layer"].mode & ~L.PACK_F16X3) in wmodes) != wino or (g["layer"].mode ^ lay.mode) & L.PACK_F16X3
            for g in groups):
         raise ValueError("conv2d: groups mix Winograd / direct or f32 / f16x3 packings")
-    a.flags = (L.CONV_F16X3 if lay.mode & L.PACK_F16X3 else 0) | (L.CONV_GENERIC if WINO_GENERIC else 0)
+    a.flags = L.CONV_F16X3 if lay.mode & L.PACK_F16X3 else 0
     a.status = _vp(status)
     tr = TRACE
     if tr is not None:

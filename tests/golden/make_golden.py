@@ -431,6 +431,8 @@ def large_pins(H, W, seed):
     l3w = W // 4
     seam_x = sorted({0, 1, 31, 32, 63, 64, 127, 128, W // 2, 4 * (l3w // 32) * 32 - 1, 4 * (l3w // 32) * 32,
                      W - 33, W - 32, W - 2, W - 1})
+    seam_y = [v for v in seam_y if 0 <= v < H]
+    seam_x = [v for v in seam_x if 0 <= v < W]
     k = 8
     fy = np.concatenate([np.repeat(seam_y, k), rng.integers(0, H, len(seam_x) * k), rng.integers(0, H, 1536)])
     fx = np.concatenate([rng.integers(0, W, len(seam_y) * k), np.repeat(seam_x, k), rng.integers(0, W, 1536)])

@@ -572,7 +572,9 @@ def test_dcn_sep_fused_reports_range(ops, L, which):
     """k_dcn_sep's own range reporting (advisor finding, round 3): one offset-feature value (phase 1: the
     offset/mask sums go non-finite, the `chk` sum) or one DCN-input value (phase 2: the output goes
     non-finite, `chk2`) far outside the split-fp16 range sets the status word; the same call in range
-    leaves it 0."""
+    leaves it 0.  The phase-2 operand is the *sampled* value (bilinear weight x mask x pixel), so the
+    poisoned input pixel is 1e6: any sample that touches it with weight x mask > 0.004 overflows (a
+    5000 gives in-range samples below weight x mask 0.8 -- correctly not flagged)."""
     H, W, B = 20, 40, 2
     sdx = _dcnsep_weights(40, 2.0)
     x = rnd(B, 64, H, W, seed=41)
@@ -588,6 +590,6 @@ def test_dcn_sep_fused_reports_range(ops, L, which):
         fi[1, 7, 13, 5] = 5000.0
     else:
         xi = xi.clone()
-        xi[0, 11, 30, 60] = 5000.0
+        xi[0, 11, 30, 60] = 1.0e6
     ops.dcn_sep([dict(om_layer=om, layer=core, fea=fi, inp=xi, out=out)], status=st)
     assert int(st.item()) == 1, which

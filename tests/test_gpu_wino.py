@@ -279,34 +279,3 @@ def test_wino_f16x3_range_status_single_element(stif, kind, pos):
         out = torch.empty(2, H, W, cout, device="cuda")
         ops.conv2d([dict(layer=layer, in0=nhwc(xx), out=out)], epi=epi, status=st)
         assert int(st.item()) == want, (big, pos)
-
-
-@pytest.mark.parametrize("epi", ["none", "lrelu", "relu", "res"])
-def test_wino_ws_bit_identical_to_generic(stif, epi):
-    """The weight-stationary 64 -> 64 kernel (k_wino_ws) == the generic per-slice kernel (k_wino), bit for
-    bit (same MFMA accumulation order, same epilogue), on a launch with 3 weight sets over strided items,
-    more tiles than workgroups (several tiles per workgroup, weight reloads where a workgroup's tiles cross
-    weight sets) and partial tiles in both directions."""
-    L, ops = stif._lib, stif.ops
-    H, W, B = 70, 150, 5
-    e = dict(none=L.EPI_NONE, lrelu=L.EPI_LRELU, relu=L.EPI_RELU, res=L.EPI_RES)[epi]
-    x = torch.from_numpy(rnd(3, B, H, W, 64, seed=31)).cuda()
-    r = torch.from_numpy(rnd(3, B, H, W, 64, seed=32)).cuda()
-    lays = [ops.pack_conv(rnd(64, 64, 3, 3, seed=33 + i, scale=0.05), rnd(64, seed=36 + i), L.PACK_WINO | L.PACK_F16X3)
-            for i in range(3)]
-    outs = []
-    for generic in (False, True):
-        out = torch.full((3, B, H, W, 64), float("nan"), device="cuda")
-        ops.WINO_GENERIC = generic
-        try:
-            ops.conv2d([dict(layer=lays[i], in0=x[i], out=out[i], res=r[i] if epi == "res" else None)
-                        for i in range(3)], epi=e)
-        finally:
-            ops.WINO_GENERIC = False
-        outs.append(out)
-    assert torch.equal(outs[0], outs[1])
-    ref = O.conv2d(x[1].cpu().numpy().transpose(0, 3, 1, 2)[:2], rnd(64, 64, 3, 3, seed=34, scale=0.05), rnd(64, seed=37))
-    ref = {"lrelu": O.lrelu, "relu": O.relu}.get(epi, lambda v: v)(ref)
-    if epi == "res":
-        ref = ref + r[1, :2].cpu().numpy().transpose(0, 3, 1, 2)
-    assert relmax(to_nchw(outs[0][1, :2]), ref) < RTOL
