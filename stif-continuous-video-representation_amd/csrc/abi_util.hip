@@ -22,3 +22,13 @@ int stif_check_launch(const char* where) {
 
 extern "C" const char* stif_last_error(void) { return g_err; }
 extern "C" const char* stif_version(void) { return "stif_hip 0.1 gfx950"; }
+
+int stif_num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}

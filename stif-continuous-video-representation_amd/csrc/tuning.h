@@ -42,6 +42,10 @@
 #ifndef DCNSEP_WPE
 #define DCNSEP_WPE 2       // waves per SIMD the kernel is register-budgeted for
 #endif
+#ifndef DCNSEP_PIPE
+// launches with at least this many tiles per CU run the software-pipelined k_dcn_sep_pipe (0: never)
+#define DCNSEP_PIPE 3
+#endif
 #ifndef DCNSEP_EXP
 #define DCNSEP_EXP 0       // probes: 1 no phase 1, 3 no phase 2, 5 no per-pair restaging
 #endif

@@ -703,17 +703,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   }
 }
 
-int num_cus() {
-  static int n = 0;
-  if (!n) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-  }
-  return n;
-}
-
-
 template <int IN1, int EPI>
 int launch(const stif_conv_args& a, hipStream_t st) {
   const long long tiles =
@@ -723,11 +712,11 @@ int launch(const stif_conv_args& a, hipStream_t st) {
     return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: item larger than 2 GB (buffer addressing)");
   if constexpr (WINO_OM && EPI == STIF_EPI_OFFMASK) if ((a.flags & STIF_CONV_F16X3) && a.C0 == 64 && !a.in1_mode) {
     const long long sp = tiles / ((a.cout + 63) / 64);   // spatial tiles: all couts per workgroup
-    const int g2 = 8 * (int)std::min<long long>((sp + 7) / 8, (long long)WG_PER_CU * num_cus() / 8);
+    const int g2 = 8 * (int)std::min<long long>((sp + 7) / 8, (long long)WG_PER_CU * stif_num_cus() / 8);
     hipLaunchKernelGGL((k_wino_om<EPI>), dim3(g2), dim3(256), 0, st, a, (int)sp);
     return stif_check_launch("stif_conv3x3_wino");
   }
-  const int grid = 8 * (int)std::min<long long>((tiles + 7) / 8, (long long)WG_PER_CU * num_cus() / 8);
+  const int grid = 8 * (int)std::min<long long>((tiles + 7) / 8, (long long)WG_PER_CU * stif_num_cus() / 8);
   if (a.flags & STIF_CONV_F16X3)
     hipLaunchKernelGGL((k_wino<IN1, EPI, 1>), dim3(grid), dim3(256), 0, st, a, (int)tiles);
   else
