@@ -606,7 +606,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
   // nx) and, at chunk 3, the biases of the next iteration (offset/mask: nn, DCN: nx)
   f16x8 dh, dl;
   f32x4 x0, x1;
-  float po[27];   // this chunk's 27 offsets of the lane half's group (phase 2)
   auto run_tile = [&](auto P1c, auto P2c, const PTile& cu, const PTile& nx, const PTile& nn, int wait0) {
     constexpr bool P1 = decltype(P1c)::value, P2 = decltype(P2c)::value;
     const int oy = cu.oy0 + wv, ox = cu.ox0 + l32;
@@ -624,37 +623,52 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        // phase 2: the bilinear sample of tap t of group 2c + h (global fallback first: its wait then
-        // covers only DMA issued before this step)
+        // phase 2, the bilinear sample of tap t of group 2c + h (dmcn_im2col_bilinear semantics):
+        // DCNSEP_PIPE_IL = 1 spreads its coordinate math, LDS corner reads and blend over the phase-1
+        // M-tiles below and applies the rare global-load fallback after them; 0 samples first
         f16x8 ah2, al2;
-        if constexpr (P2) {
-          if (t == 0) {
-#pragma unroll
-            for (int k = 0; k < 27; ++k) {
-              const int s0 = k, s1 = 27 + k, s2 = 54 + k, s3 = 81 + k;
-              const float v0 = of[s0 / 16][s0 % 16], v1 = of[s1 / 16][s1 % 16], v2 = of[s2 / 16][s2 % 16],
-                          v3 = of[s3 / 16][s3 % 16];
-              po[k] = c == 0 ? v0 : c == 1 ? v1 : c == 2 ? v2 : v3;
-            }
-          }
+        f32x4 a0, a1, cr[8];
+        float w1 = 0.f, w2 = 0.f, w3 = 0.f, w4 = 0.f;
+        int h_low = 0, w_low = 0;
+        bool fb = false;
+        const float* p0 = st;
+        // offset slot 27 c + 3 t + e of this lane half (the chunk c is a run-time loop index)
+        auto off = [&](int e) {
+          const int k = 3 * t + e, s0 = k, s1 = 27 + k, s2 = 54 + k, s3 = 81 + k;
+          const float v0 = of[s0 / 16][s0 % 16], v1 = of[s1 / 16][s1 % 16], v2 = of[s2 / 16][s2 % 16],
+                      v3 = of[s3 / 16][s3 % 16];
+          return c == 0 ? v0 : c == 1 ? v1 : c == 2 ? v2 : v3;
+        };
+        auto coords = [&]() {
           const int ky = t / 3, kx = t - 3 * ky;
-          const float dy = po[3 * t], dx = po[3 * t + 1], mk = po[3 * t + 2];
-          const float h_im = (float)(oy - 1 + ky) + dy;
-          const float w_im = (float)(ox - 1 + kx) + dx;
+          const float h_im = (float)(oy - 1 + ky) + off(0);
+          const float w_im = (float)(ox - 1 + kx) + off(1);
           const bool valid = pix_ok & (h_im > -1.f) & (w_im > -1.f) & (h_im < (float)H) & (w_im < (float)W);
           const float fh = floorf(h_im), fw = floorf(w_im);
           const float lh = h_im - fh, lw = w_im - fw, hh = 1.f - lh, hw = 1.f - lw;
-          const int h_low = (int)fh, w_low = (int)fw;
+          h_low = (int)fh;
+          w_low = (int)fw;
           const int r0 = h_low - ty0, c0 = w_low - tx0;
           const bool in_tile = ((unsigned)r0 < (unsigned)(TR - 1)) & ((unsigned)c0 < (unsigned)(TC - 1));
-          const float m = valid ? mk : 0.f;
+          const float m = valid ? off(2) : 0.f;
           const float hm = hh * m, lm = lh * m;
-          const float w1 = hm * hw, w2 = hm * lw, w3 = lm * hw, w4 = lm * lw;
-          const float* p0 = st + (((in_tile ? r0 : 0) * 4 + 2 * hf) * TP + (in_tile ? c0 : 0)) * 4;
+          w1 = hm * hw;
+          w2 = hm * lw;
+          w3 = lm * hw;
+          w4 = lm * lw;
+          p0 = st + (((in_tile ? r0 : 0) * 4 + 2 * hf) * TP + (in_tile ? c0 : 0)) * 4;
+          fb = valid & !in_tile;
+        };
+        auto corners = [&]() {
           const float* p1 = p0 + 4 * TP * 4;
-          f32x4 a0 = w1 * ld4(p0) + w2 * ld4(p0 + 4) + w3 * ld4(p1) + w4 * ld4(p1 + 4);
-          f32x4 a1 = w1 * ld4(p0 + TP * 4) + w2 * ld4(p0 + TP * 4 + 4) + w3 * ld4(p1 + TP * 4) + w4 * ld4(p1 + TP * 4 + 4);
-          const bool fb = valid & !in_tile;
+          cr[0] = ld4(p0); cr[1] = ld4(p0 + 4); cr[2] = ld4(p1); cr[3] = ld4(p1 + 4);
+          cr[4] = ld4(p0 + TP * 4); cr[5] = ld4(p0 + TP * 4 + 4); cr[6] = ld4(p1 + TP * 4); cr[7] = ld4(p1 + TP * 4 + 4);
+        };
+        auto blend = [&]() {
+          a0 = w1 * cr[0] + w2 * cr[1] + w3 * cr[2] + w4 * cr[3];
+          a1 = w1 * cr[4] + w2 * cr[5] + w3 * cr[6] + w4 * cr[7];
+        };
+        auto fallback = [&]() {
           if (__builtin_amdgcn_ballot_w64(fb)) {
             if (fb) {
               const int h_high = h_low + 1, w_high = w_low + 1, co = c * 16 + hf * 8;
@@ -670,12 +684,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
                    w4 * (b4 ? ld4(q4 + 4) : z);
             }
           }
+        };
+        auto mfma2 = [&]() {   // k_dcn_sep's 6 MFMAs of the tap (per accumulator: hh, hl, lh)
           split_f16x3(a0, a1, ah2, al2);
+          const float* wp = smem + PP_TW + (t % RING) * 1024 + lane * 4;   // [nt][plane][lane][4]
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) {
+            const f16x8 bh = ldh8(wp + nt * 512), bl = ldh8(wp + nt * 512 + 256);
+            f32x16& acc = nt ? acc1 : acc0;
+            acc = mfma16h(ah2, bh, acc);
+            acc = mfma16h(ah2, bl, acc);
+            acc = mfma16h(al2, bh, acc);
+          }
+        };
+        constexpr bool IL = DCNSEP_PIPE_IL && P1;
+        if constexpr (P2 && !IL) {
+          coords();
+          corners();
+          blend();
+          fallback();
         }
-        // phase 1 MFMAs (weights of this step, one M-tile ahead) with the phase-2 MFMAs and the DMA of
-        // step s + 2 placed among them
+        // phase 1 MFMAs (weights of this step, one M-tile ahead) with the DMA of step s + 2 (and the
+        // interleaved sampling) placed among them
         const float* wb = smem + PP_W + (t % RING) * 4096 + lane * 4;
-        const float* wp = smem + PP_TW + (t % RING) * 1024 + lane * 4;   // [nt][plane][lane][4]
         f16x8 wh[2], wl[2];
         if constexpr (P1) {
           wh[0] = ldh8(wb);
@@ -694,7 +725,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
             om[q] = mfma16h(wh[q & 1], dl, om[q]);
             om[q] = mfma16h(wl[q & 1], dh, om[q]);
           }
-          if (q == 0) {
+          // the sampling of this step (IL): coordinates, LDS corners, blend and the rare global fallback
+          // before the step's DMA is issued, so a fallback load's wait covers only older DMA
+          if constexpr (P2 && IL) {
+            if (q == 0) coords();
+            if (q == 1) corners();
+            if (q == 2) {
+              blend();
+              fallback();
+            }
+          }
+          if (q == (IL ? 3 : 0)) {
             // LDS-DMA of step s + 2 (and, at tap 1, the next chunk's stages)
             const int s2 = 9 * c + t + 2;
             if (s2 < KSTEPS) {
@@ -722,18 +763,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
               x1 = ld4(nb + 4);
             }
           }
-          if constexpr (P2) {
-            if (q == 2 || q == 4) {   // phase-2 MFMAs, 3 per cout half (k_dcn_sep's order per accumulator)
-              const int nt = q == 2 ? 0 : 1;
-              const f16x8 bh = ldh8(wp + nt * 512), bl = ldh8(wp + nt * 512 + 256);
-              f32x16& acc = nt ? acc1 : acc0;
-              acc = mfma16h(ah2, bh, acc);
-              acc = mfma16h(ah2, bl, acc);
-              acc = mfma16h(al2, bh, acc);
-            }
+          if constexpr (P2 && !IL) {
+            if (q == 2) mfma2();
           }
           __builtin_amdgcn_sched_barrier(0);
         }
+        if constexpr (P2 && IL) mfma2();
         if constexpr (P1) {
           if (t < 8) split_f16x3(x0, x1, dh, dl);
         }

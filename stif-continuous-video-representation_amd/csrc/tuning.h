@@ -46,6 +46,9 @@
 // launches with at least this many tiles per CU run the software-pipelined k_dcn_sep_pipe (0: never)
 #define DCNSEP_PIPE 3
 #endif
+#ifndef DCNSEP_PIPE_IL
+#define DCNSEP_PIPE_IL 1   // k_dcn_sep_pipe: phase-2 sampling spread over the phase-1 MFMAs (0: before them)
+#endif
 #ifndef DCNSEP_EXP
 #define DCNSEP_EXP 0       // probes: 1 no phase 1, 3 no phase 2, 5 no per-pair restaging
 #endif
