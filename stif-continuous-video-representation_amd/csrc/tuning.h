@@ -44,7 +44,7 @@
 #endif
 #ifndef DCNSEP_PIPE
 // launches with at least this many tiles per CU run the software-pipelined k_dcn_sep_pipe (0: never)
-#define DCNSEP_PIPE 3
+#define DCNSEP_PIPE 0
 #endif
 #ifndef DCNSEP_PIPE_IL
 #define DCNSEP_PIPE_IL 1   // k_dcn_sep_pipe: phase-2 sampling spread over the phase-1 MFMAs (0: before them)
