@@ -141,15 +141,10 @@ typedef struct {
   long long fea_item, in_item, out_item;
   int ngroups, nitems, H, W;
   int epi;                              /* STIF_EPI_NONE or STIF_EPI_LRELU */
-  int flags;                            /* STIF_CONV_F16X3 (required), optionally | STIF_DCNSEP_PIPE_OFF / _ON */
+  int flags;                            /* STIF_CONV_F16X3 (required) */
   int* status;                          /* optional device word, as stif_conv_args.status */
 } stif_dcn_sep_args;
 
-/* stif_dcn_sep_args.flags, test / benchmark aids: the kernel is chosen by launch size (launches with at least
- * DCNSEP_PIPE tiles per CU run the software-pipelined form, one persistent workgroup per CU); these force the
- * one-tile-per-workgroup form (_OFF) or the pipelined form at any size (_ON).  Bit-identical outputs. */
-#define STIF_DCNSEP_PIPE_OFF 2
-#define STIF_DCNSEP_PIPE_ON 4
 int stif_dcn_sep_nhwc(const stif_dcn_sep_args* args, void* stream);
 
 /* Drop-in for `_ext.dcn_v2_forward` (dcn_v2.h:9-23): NCHW fp32 input [b,c,h,w],

@@ -34,7 +34,6 @@
 #include "tuning.h"
 
 #include <algorithm>
-#include <type_traits>
 
 namespace {
 
@@ -392,419 +391,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_
   report_range(a.status, not_finite(chk2));
 }
 
-// ---------------------------------------------------------------------------------------------------
-// k_dcn_sep_pipe: the same operator, software-pipelined across tiles.  In k_dcn_sep a tile's phase 1
-// (offset/mask conv: MFMA-dense, 0.71 MFMA-busy alone) and phase 2 (bilinear sampling: VALU and
-// data-dependent LDS reads) run one after the other, and the two workgroups of a CU do not overlap them
-// (DESIGN.md section 3d).  Here one persistent 4-wave workgroup per CU runs ONE wave per SIMD with the
-// whole 512-register budget and interleaves the two phases of different tiles inside every wave: step s
-// (= 9 c + t, c = 16-channel chunk of phase 1 = group pair of phase 2, t = tap) runs phase-1 K step s of
-// tile i + 1 (21 MFMAs into its 112 offset/mask accumulators) next to phase-2 step s of tile i (the
-// bilinear samples of tap t of group pair c from tile i's offsets, kept post-processed in another 112
-// registers, and 6 MFMAs) -- the sampling VALU and LDS reads issue between the MFMAs of the same
-// basic block.  One barrier per step publishes both phases' LDS-DMA, issued two steps ahead: phase-1
-// weight ring (3 x 14 KB), phase-2 tap-weight ring (3 x 4 KB), and per chunk the phase-1 halo chunk
-// (2 x 16 KB) and the phase-2 pair tile (2 x 24 KB) one chunk ahead, so no buffer is restaged in the
-// critical path.  Every step issues the same number of LDS-DMA instructions per wave (dummies where a
-// tile does not exist), so the counted vmcnt waits are exact.  The workgroup's first tile runs phase 1
-// alone (prologue) and its last tile phase 2 alone (epilogue).  Same arithmetic, same order as
-// k_dcn_sep: bit-identical outputs.
-constexpr int PP_D0 = 0, PP_D1 = D_F;                      // phase-1 halo chunks
-constexpr int PP_W = 2 * D_F;                              // phase-1 weight ring
-constexpr int PP_T0 = PP_W + RING * 4096;                  // phase-2 pair tiles
-constexpr int PP_T1 = PP_T0 + T_INST * 256;
-constexpr int PP_TW = PP_T1 + T_INST * 256;                // phase-2 tap-weight ring [slot][nt][plane][lane][4]
-constexpr int PP_B = PP_TW + RING * 1024;                  // biases: offset/mask [256] | DCN [64] | 2 dummy slots
-constexpr int PP_E = PP_B + 1024;                          // epilogue blocks, one per wave
-constexpr int PP_F = PP_E + 4 * 1024;
-static_assert(NW == 4 && PP_F * 4 <= 160 * 1024, "k_dcn_sep_pipe LDS map (4 waves, one workgroup per CU)");
-// LDS-DMA instructions per wave and step: phase-1 weights (16 / 4) + phase-2 tap weights (4 / 4); at
-// tap 1 also the next halo chunk (16 / 4), the next pair tile (24 / 4) and the bias pieces (4 / 4)
-constexpr int PP_Q = WK_INS / 4 + 1;
-constexpr int PP_QX = D_INS / 4 + T_INST / 4 + 1;
-
-struct PTile {
-  int oy0, ox0, g, n;
-};
-
-STIF_DEV void wait_vm_pipe(int n) {
-  switch (n) {
-    case PP_Q: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-    case PP_Q + PP_QX: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-    case PP_Q + 8: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-  }
-}
-static_assert(PP_Q == 5 && PP_Q + PP_QX == 16, "wait_vm_pipe immediates");
-
-template <int EPI>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k_dcn_sep_pipe(stif_dcn_sep_args a,
-                                                                                             int ntiles) {
-  __shared__ __attribute__((aligned(16))) float smem[PP_F];
-  const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, hf = lane >> 5;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int H = a.H, W = a.W;
-  const int tiles_x = (W + TW - 1) / TW, tiles_img = tiles_x * ((H + NW - 1) / NW);
-  const unsigned img_bytes = (unsigned)((size_t)H * W * 64 * 4);
-  // XCD-aware persistent schedule: XCD x owns a contiguous tile range, its workgroups stride through it
-  const int xcd = blockIdx.x & 7, nl = gridDim.x >> 3;
-  const int per = (ntiles + 7) >> 3;
-  const int t0 = xcd * per + (blockIdx.x >> 3);
-  const int tend = min((xcd + 1) * per, ntiles);
-  const int ntl = t0 < tend ? (tend - t0 + nl - 1) / nl : 0;   // this workgroup's tiles
-  if (ntl == 0) return;
-  auto tile = [&](int i) {   // i-th tile of this workgroup, clamped (DMA dummies read a valid tile)
-    const int L = t0 + min(max(i, 0), ntl - 1) * nl;
-    const int z = L / tiles_img, tl = L - z * tiles_img;
-    PTile t;
-    t.g = z / a.nitems;
-    t.n = z - t.g * a.nitems;
-    t.oy0 = (tl / tiles_x) * NW;
-    t.ox0 = (tl - (tl / tiles_x) * tiles_x) * TW;
-    return t;
-  };
-  auto fea_rs = [&](const PTile& t) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(a.fea[t.g] + (size_t)t.n * a.fea_item), (short)0, (int)img_bytes,
-                                             0x00020000);
-  };
-  auto in_rs = [&](const PTile& t) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(a.in[t.g] + (size_t)t.n * a.in_item), (short)0, (int)img_bytes,
-                                             0x00020000);
-  };
-
-  // ---- LDS-DMA stages (each: the same count per wave every time it is called)
-  auto stage_data = [&](const PTile& t, int c, float* dst) {   // phase-1 halo chunk c (k_dcn_sep's)
-    const __amdgpu_buffer_rsrc_t rf = fea_rs(t);
-#pragma unroll
-    for (int j = 0; j < D_INS / 4; ++j) {
-      const int i = wv + j * 4;
-      const int s = i * 64 + lane;
-      const int px = s / 5, sub = s - 5 * px;
-      const int row = px / HC1, col = px - HC1 * row;
-      const int y = t.oy0 - 1 + row, x = t.ox0 - 1 + col;
-      const bool ok = (s < D_SLOTS) & (sub < 4) & ((unsigned)y < (unsigned)H) & ((unsigned)x < (unsigned)W);
-      const unsigned voff = ok ? (unsigned)((((size_t)y * W + x) * 64 + 16 * c + 4 * sub) * 4) : 0x80000000u;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rf, dst + i * 256, 16, voff, 0, 0, 0);
-    }
-  };
-  auto stage_w = [&](const PTile& t, int k, int slot) {        // phase-1 weights of step k
-    const __amdgpu_buffer_rsrc_t rw =
-        __builtin_amdgcn_make_buffer_rsrc((void*)a.w_om[t.g], (short)0, KSTEPS * WK_F * 4, 0x00020000);
-    float* dst = smem + PP_W + slot * 4096;
-#pragma unroll
-    for (int j = 0; j < WK_INS / 4; ++j) {
-      const int i = wv + j * 4;
-      const unsigned voff = i < MT * 2 ? (unsigned)((k * WK_F + i * 256) * 4 + lane * 16) : 0x80000000u;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, dst + i * 256, 16, voff, 0, 0, 0);
-    }
-  };
-  auto stage_w2 = [&](const PTile& t, int pa, int tap, int slot) {   // phase-2 B fragments of (pair, tap)
-    const __amdgpu_buffer_rsrc_t rw =
-        __builtin_amdgcn_make_buffer_rsrc((void*)a.w[t.g], (short)0, 4 * WP_F * 4, 0x00020000);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, smem + PP_TW + slot * 1024 + wv * 256, 16,
-                                             (unsigned)((pa * WP_F + tap * 1024 + wv * 256) * 4 + lane * 16), 0, 0, 0);
-  };
-  auto stage_pair = [&](const PTile& t, int pa, float* st) {   // phase-2 tile of group pair pa
-    const __amdgpu_buffer_rsrc_t ri = in_rs(t);
-    const int ty0 = t.oy0 - 1 - M, tx0 = t.ox0 - 1 - M;
-#pragma unroll
-    for (int j = 0; j < T_INST / 4; ++j) {
-      const int i = wv + j * 4;
-      const int e = i * 64 + lane;
-      const int col = e % TP, rq = e / TP, q = rq & 3, row = rq >> 2;
-      const int y = ty0 + row, x = tx0 + col;
-      const bool ok = (e < T_EL) & ((unsigned)y < (unsigned)H) & ((unsigned)x < (unsigned)W);
-      const unsigned voff = ok ? (unsigned)((((size_t)y * W + x) * 64 + pa * 16 + q * 4) * 4) : 0x80000000u;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ri, st + i * 256, 16, voff, 0, 0, 0);
-    }
-  };
-  // biases: piece 0 (wave 0) = the offset/mask bias [256] of t_om's set, piece 1 (wave 1) = the DCN bias
-  // [64] of t_dcn's set (lanes >= 16 out of range); waves 2, 3 load zeros into slots of their own
-  auto stage_bias = [&](const PTile& t_om, const PTile& t_dcn) {
-    const float* src = wv == 0 ? a.b_om[t_om.g] : a.bias[t_dcn.g];
-    const int nb = wv == 0 ? 1024 : 256;
-    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, nb, 0x00020000);
-    const unsigned voff = (wv < 2 && lane * 16 < nb) ? (unsigned)(lane * 16) : 0x80000000u;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, smem + PP_B + wv * 256, 16, voff, 0, 0, 0);
-  };
-
-  // ---- per-tile state: tile i + 1's offset/mask accumulators (phase 1), tile i's offsets and DCN
-  // accumulators (phase 2)
-  f32x16 om[MT], of[MT];
-  f32x16 acc0, acc1;
-  auto init_om = [&](const float* bsrc) {   // bias x 2^14 (k_dcn_sep's slot order)
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const f32x4 bq = ld4(bsrc + m * 32 + 8 * v + 4 * hf) * (1.0f / F16X3_UNSCALE);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) om[m][4 * v + e] = bq[e];
-      }
-  };
-  auto init_acc = [&](const float* bsrc) {
-    const float b0 = bsrc[l32] * (1.0f / F16X3_UNSCALE), b1 = bsrc[32 + l32] * (1.0f / F16X3_UNSCALE);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      acc0[r] = b0;
-      acc1[r] = b1;
-    }
-  };
-  // om -> of: unscale, sigmoid(mask), range sum (k_dcn_sep's post-processing)
-  auto finish_om = [&]() {
-    float chk = 0.f;
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int s = 16 * m + r;
-        float x = om[m][r] * F16X3_UNSCALE;
-        if (s < 108) {
-          chk += x;
-          if (s % 3 == 2) x = sigmoid_fast(x);
-        }
-        of[m][r] = x;
-      }
-    report_range(a.status, not_finite(chk));
-  };
-  // phase-2 epilogue of tile t: k_dcn_sep's LDS-transposed 16-B stores, as buffer stores whose
-  // out-of-image lanes get an out-of-range offset (every wave issues all 8: exact vmcnt bookkeeping)
-  auto store_out = [&](const PTile& t) {
-    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(a.out[t.g] + (size_t)t.n * a.out_item), (short)0, (int)img_bytes, 0x00020000);
-    float* blk = smem + PP_E + wv * 1024;
-    const int rpx = lane >> 3, c4 = lane & 7;
-    const int oy = t.oy0 + wv;
-    float chk2 = 0.f;
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      f32x16 v;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float x = (nt ? acc1[r] : acc0[r]) * F16X3_UNSCALE;
-        chk2 += x;
-        if (EPI == STIF_EPI_LRELU) x = lrelu01(x);
-        v[r] = x;
-      }
-      tile_to_lds(blk, v, lane);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int px = i * 8 + rpx, x = t.ox0 + px;
-        const f32x4 o = lds_row4(blk, px, c4);
-        const unsigned voff = (oy < H && x < W) ? (unsigned)((((size_t)oy * W + x) * 64 + nt * 32 + c4 * 4) * 4)
-                                                : 0x80000000u;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, o), ro,
-                                               voff, 0, 0);
-      }
-    }
-    report_range(a.status, not_finite(chk2));
-  };
-
-  // ---- one step.  P1: phase-1 K step s of tile nx; P2: phase-2 step s of tile cu.  DMA (always):
-  // phase-1 weights and phase-2 tap weights of step s + 2 (of nx / cu, or of nn / nx past the tile's
-  // 36 steps); at tap 1 the next halo chunk (nx, or chunk 0 of nn), the next pair tile (cu, or pair 0 of
-  // nx) and, at chunk 3, the biases of the next iteration (offset/mask: nn, DCN: nx)
-  f16x8 dh, dl;
-  f32x4 x0, x1;
-  auto run_tile = [&](auto P1c, auto P2c, const PTile& cu, const PTile& nx, const PTile& nn, int wait0) {
-    constexpr bool P1 = decltype(P1c)::value, P2 = decltype(P2c)::value;
-    const int oy = cu.oy0 + wv, ox = cu.ox0 + l32;
-    const bool pix_ok = oy < H && ox < W;
-    const int ty0 = cu.oy0 - 1 - M, tx0 = cu.ox0 - 1 - M;
-    const float* in = a.in[cu.g] + (size_t)cu.n * a.in_item;
-#pragma unroll 1
-    for (int c = 0; c < 4; ++c) {
-      const float* dbuf = smem + ((c & 1) ? PP_D1 : PP_D0) + (wv * HC1 + l32) * PX_F + hf * 8;
-      const float* st = smem + ((c & 1) ? PP_T1 : PP_T0);
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        // LDS-DMA of step s landed (issued two steps ago); the previous step's may stay in flight
-        wait_vm_pipe(t == 2 ? PP_Q + PP_QX : (t == 0 && c == 0) ? wait0 : PP_Q);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        // phase 2, the bilinear sample of tap t of group 2c + h (dmcn_im2col_bilinear semantics):
-        // DCNSEP_PIPE_IL = 1 spreads its coordinate math, LDS corner reads and blend over the phase-1
-        // M-tiles below and applies the rare global-load fallback after them; 0 samples first
-        f16x8 ah2, al2;
-        f32x4 a0, a1, cr[8];
-        float w1 = 0.f, w2 = 0.f, w3 = 0.f, w4 = 0.f;
-        int h_low = 0, w_low = 0;
-        bool fb = false;
-        const float* p0 = st;
-        // offset slot 27 c + 3 t + e of this lane half (the chunk c is a run-time loop index)
-        auto off = [&](int e) {
-          const int k = 3 * t + e, s0 = k, s1 = 27 + k, s2 = 54 + k, s3 = 81 + k;
-          const float v0 = of[s0 / 16][s0 % 16], v1 = of[s1 / 16][s1 % 16], v2 = of[s2 / 16][s2 % 16],
-                      v3 = of[s3 / 16][s3 % 16];
-          return c == 0 ? v0 : c == 1 ? v1 : c == 2 ? v2 : v3;
-        };
-        auto coords = [&]() {
-          const int ky = t / 3, kx = t - 3 * ky;
-          const float h_im = (float)(oy - 1 + ky) + off(0);
-          const float w_im = (float)(ox - 1 + kx) + off(1);
-          const bool valid = pix_ok & (h_im > -1.f) & (w_im > -1.f) & (h_im < (float)H) & (w_im < (float)W);
-          const float fh = floorf(h_im), fw = floorf(w_im);
-          const float lh = h_im - fh, lw = w_im - fw, hh = 1.f - lh, hw = 1.f - lw;
-          h_low = (int)fh;
-          w_low = (int)fw;
-          const int r0 = h_low - ty0, c0 = w_low - tx0;
-          const bool in_tile = ((unsigned)r0 < (unsigned)(TR - 1)) & ((unsigned)c0 < (unsigned)(TC - 1));
-          const float m = valid ? off(2) : 0.f;
-          const float hm = hh * m, lm = lh * m;
-          w1 = hm * hw;
-          w2 = hm * lw;
-          w3 = lm * hw;
-          w4 = lm * lw;
-          p0 = st + (((in_tile ? r0 : 0) * 4 + 2 * hf) * TP + (in_tile ? c0 : 0)) * 4;
-          fb = valid & !in_tile;
-        };
-        auto corners = [&]() {
-          const float* p1 = p0 + 4 * TP * 4;
-          cr[0] = ld4(p0); cr[1] = ld4(p0 + 4); cr[2] = ld4(p1); cr[3] = ld4(p1 + 4);
-          cr[4] = ld4(p0 + TP * 4); cr[5] = ld4(p0 + TP * 4 + 4); cr[6] = ld4(p1 + TP * 4); cr[7] = ld4(p1 + TP * 4 + 4);
-        };
-        auto blend = [&]() {
-          a0 = w1 * cr[0] + w2 * cr[1] + w3 * cr[2] + w4 * cr[3];
-          a1 = w1 * cr[4] + w2 * cr[5] + w3 * cr[6] + w4 * cr[7];
-        };
-        auto fallback = [&]() {
-          if (__builtin_amdgcn_ballot_w64(fb)) {
-            if (fb) {
-              const int h_high = h_low + 1, w_high = w_low + 1, co = c * 16 + hf * 8;
-              const bool b1 = h_low >= 0 && w_low >= 0, b2 = h_low >= 0 && w_high <= W - 1;
-              const bool b3 = h_high <= H - 1 && w_low >= 0, b4 = h_high <= H - 1 && w_high <= W - 1;
-              const float* q1 = in + ((size_t)h_low * W + w_low) * 64 + co;
-              const float* q2 = in + ((size_t)h_low * W + w_high) * 64 + co;
-              const float* q3 = in + ((size_t)h_high * W + w_low) * 64 + co;
-              const float* q4 = in + ((size_t)h_high * W + w_high) * 64 + co;
-              const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
-              a0 = w1 * (b1 ? ld4(q1) : z) + w2 * (b2 ? ld4(q2) : z) + w3 * (b3 ? ld4(q3) : z) + w4 * (b4 ? ld4(q4) : z);
-              a1 = w1 * (b1 ? ld4(q1 + 4) : z) + w2 * (b2 ? ld4(q2 + 4) : z) + w3 * (b3 ? ld4(q3 + 4) : z) +
-                   w4 * (b4 ? ld4(q4 + 4) : z);
-            }
-          }
-        };
-        auto mfma2 = [&]() {   // k_dcn_sep's 6 MFMAs of the tap (per accumulator: hh, hl, lh)
-          split_f16x3(a0, a1, ah2, al2);
-          const float* wp = smem + PP_TW + (t % RING) * 1024 + lane * 4;   // [nt][plane][lane][4]
-#pragma unroll
-          for (int nt = 0; nt < 2; ++nt) {
-            const f16x8 bh = ldh8(wp + nt * 512), bl = ldh8(wp + nt * 512 + 256);
-            f32x16& acc = nt ? acc1 : acc0;
-            acc = mfma16h(ah2, bh, acc);
-            acc = mfma16h(ah2, bl, acc);
-            acc = mfma16h(al2, bh, acc);
-          }
-        };
-        constexpr bool IL = DCNSEP_PIPE_IL && P1;
-        if constexpr (P2 && !IL) {
-          coords();
-          corners();
-          blend();
-          fallback();
-        }
-        // phase 1 MFMAs (weights of this step, one M-tile ahead) with the DMA of step s + 2 (and the
-        // interleaved sampling) placed among them
-        const float* wb = smem + PP_W + (t % RING) * 4096 + lane * 4;
-        f16x8 wh[2], wl[2];
-        if constexpr (P1) {
-          wh[0] = ldh8(wb);
-          wl[0] = ldh8(wb + 256);
-          if (t == 0) split_f16x3(ld4(dbuf), ld4(dbuf + 4), dh, dl);
-        }
-#pragma unroll
-        for (int q = 0; q < MT; ++q) {
-          if constexpr (P1) {
-            if (q + 1 < MT) {
-              wh[(q + 1) & 1] = ldh8(wb + (2 * q + 2) * 256);
-              wl[(q + 1) & 1] = ldh8(wb + (2 * q + 3) * 256);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            om[q] = mfma16h(wh[q & 1], dh, om[q]);
-            om[q] = mfma16h(wh[q & 1], dl, om[q]);
-            om[q] = mfma16h(wl[q & 1], dh, om[q]);
-          }
-          // the sampling of this step (IL): coordinates, LDS corners, blend and the rare global fallback
-          // before the step's DMA is issued, so a fallback load's wait covers only older DMA
-          if constexpr (P2 && IL) {
-            if (q == 0) coords();
-            if (q == 1) corners();
-            if (q == 2) {
-              blend();
-              fallback();
-            }
-          }
-          if (q == (IL ? 3 : 0)) {
-            // LDS-DMA of step s + 2 (and, at tap 1, the next chunk's stages)
-            const int s2 = 9 * c + t + 2;
-            if (s2 < KSTEPS) {
-              stage_w(nx, s2, (t + 2) % RING);
-              stage_w2(cu, s2 / 9, s2 % 9, (t + 2) % RING);
-            } else {
-              stage_w(nn, s2 - KSTEPS, (t + 2) % RING);
-              stage_w2(nx, 0, s2 - KSTEPS, (t + 2) % RING);
-            }
-            if (t == 1) {
-              if (c < 3) {
-                stage_data(nx, c + 1, smem + (((c + 1) & 1) ? PP_D1 : PP_D0));
-                stage_pair(cu, c + 1, smem + (((c + 1) & 1) ? PP_T1 : PP_T0));
-              } else {
-                stage_data(nn, 0, smem + PP_D0);
-                stage_pair(nx, 0, smem + PP_T0);
-              }
-              stage_bias(nn, nx);
-            }
-          }
-          if constexpr (P1) {
-            if (q == 1 && t < 8) {   // the next tap of the same chunk
-              const float* nb = dbuf + (((t + 1) / 3) * HC1 + (t + 1) % 3) * PX_F;
-              x0 = ld4(nb);
-              x1 = ld4(nb + 4);
-            }
-          }
-          if constexpr (P2 && !IL) {
-            if (q == 2) mfma2();
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        if constexpr (P2 && IL) mfma2();
-        if constexpr (P1) {
-          if (t < 8) split_f16x3(x0, x1, dh, dl);
-        }
-      }
-    }
-  };
-
-  // ---- prologue: tile 0's phase 1 (its first stages issued here, in the steps' order)
-  const std::integral_constant<bool, true> Y{};
-  const std::integral_constant<bool, false> N{};
-  PTile cu = tile(-1), nx = tile(0), nn = tile(1);
-  init_om(a.b_om[nx.g]);
-  init_acc(a.bias[nx.g]);   // (overwritten before use; keeps the registers defined)
-  stage_data(nx, 0, smem + PP_D0);
-  stage_w(nx, 0, 0);
-  stage_w2(nx, 0, 0, 0);
-  stage_w(nx, 1, 1);
-  stage_w2(nx, 0, 1, 1);
-  run_tile(Y, N, nx, nx, nn, PP_Q);
-  for (int i = 0;; ++i) {
-    // iteration i: phase 2 of tile i, phase 1 of tile i + 1 (if any)
-    finish_om();
-    const float* bb = smem + PP_B;   // landed: issued at step 28 of the iteration that just ended
-    init_acc(bb + 256);
-    if (i + 1 < ntl) init_om(bb);
-    cu = nx;
-    nx = tile(i + 1);
-    nn = tile(i + 2);
-    if (i + 1 < ntl) run_tile(Y, Y, cu, nx, nn, i == 0 ? PP_Q : PP_Q + 8);
-    else run_tile(N, Y, cu, nx, nn, i == 0 ? PP_Q : PP_Q + 8);
-    store_out(cu);
-    if (i + 1 >= ntl) break;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every dummy stage drained before the wave ends
-}
-
 }  // namespace
 
 extern "C" int stif_dcn_sep_nhwc(const stif_dcn_sep_args* pa, void* stream) {
@@ -822,19 +408,6 @@ extern "C" int stif_dcn_sep_nhwc(const stif_dcn_sep_args* pa, void* stream) {
   const long long wgs = (long long)((a.W + TW - 1) / TW) * ((a.H + NW - 1) / NW) * a.ngroups * a.nitems;
   if (wgs > 0x7fffffff) return stif_fail(STIF_E_INVALID, "stif_dcn_sep_nhwc: grid too large");
   dim3 grid((unsigned)wgs);
-  const bool pipe = (a.flags & STIF_DCNSEP_PIPE_ON) ||
-                    (DCNSEP_PIPE && !(a.flags & STIF_DCNSEP_PIPE_OFF) && wgs >= (long long)DCNSEP_PIPE * stif_num_cus());
-  if (NW == 4 && pipe) {
-    // enough tiles for a software pipeline per CU: one persistent 4-wave workgroup per CU
-    const int g1 = 8 * (int)std::min<long long>((wgs + 7) / 8, stif_num_cus() / 8);
-    if (a.epi == STIF_EPI_LRELU)
-      hipLaunchKernelGGL(k_dcn_sep_pipe<STIF_EPI_LRELU>, dim3(g1), dim3(256), 0, (hipStream_t)stream, a, (int)wgs);
-    else if (a.epi == STIF_EPI_NONE)
-      hipLaunchKernelGGL(k_dcn_sep_pipe<STIF_EPI_NONE>, dim3(g1), dim3(256), 0, (hipStream_t)stream, a, (int)wgs);
-    else
-      return stif_fail(STIF_E_INVALID, "stif_dcn_sep_nhwc: epilogue must be NONE or LRELU");
-    return stif_check_launch("stif_dcn_sep_nhwc");
-  }
   if (a.epi == STIF_EPI_LRELU)
     hipLaunchKernelGGL(k_dcn_sep<STIF_EPI_LRELU>, grid, dim3(64 * NW), 0, (hipStream_t)stream, a);
   else if (a.epi == STIF_EPI_NONE)

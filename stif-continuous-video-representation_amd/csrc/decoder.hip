@@ -204,7 +204,7 @@ STIF_DEV __amdgpu_buffer_rsrc_t mlp_rsrc(const float* mlp) {
 }
 
 // acc += W_tile . x, tile in LDS ([v][lane][4]), x = one 32-feature register tile
-template <int F16, bool SB = true>
+template <int F16>
 STIF_DEV void tile_mma(f32x16& acc, const float* t, const XT<F16>& xt, int lane) {
   const float* b = t + lane * 4;
   if constexpr (F16) {
@@ -229,7 +229,7 @@ STIF_DEV void tile_mma(f32x16& acc, const float* t, const XT<F16>& xt, int lane)
     for (int e = 0; e < 4; ++e) acc = mfma32(w3[e], x[12 + e], acc);
   }
   // keep the compiler from hoisting the LDS reads of many tiles ahead (VGPR budget)
-  if (SB) __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 // o[c] += W[c][32 kt + F(r, hf)] . x[r] over this lane's 16 features of register tile kt (W: plain
@@ -265,10 +265,8 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
   const __amdgpu_buffer_rsrc_t rm = mlp_rsrc(mlp);
   if (MODE != 1) dma_tiles<DEC_NW>(W3V, rm, L_W3V, 1, wv, lane);
   // segment 0: feat layer 1 (4 tiles); segments 1..8: feat layer 2 tile kt + layer 3 (0, kt), (1, kt)
-  if (MODE != 2) {
-    dma_tiles<DEC_NW>(B0, rm, F_W1, 4, wv, lane);
-    if (DEC1_SKEW) dma_tiles<DEC_NW>(B0 + 4 * T, rm, F_W2, 2, wv, lane);   // layer-2 rows of tile 0
-  } else {   // flow only: flow layers 0 / 1 straight into B1
+  if (MODE != 2) dma_tiles<DEC_NW>(B0, rm, F_W1, 4, wv, lane);
+  else {   // flow only: flow layers 0 / 1 straight into B1
     dma_tiles<DEC_NW>(B1, rm, L_W0, 4, wv, lane);
     dma_tiles<DEC_NW>(B1 + 4 * T, rm, L_W1, 4, wv, lane);
   }
@@ -305,17 +303,10 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
     dma_tiles<DEC_NW>(dst + 2 * T, rm, F_W3 + kt * T, 1, wv, lane);
     dma_tiles<DEC_NW>(dst + 3 * T, rm, F_W3 + (8 + kt) * T, 1, wv, lane);
   };
-  // DEC1_SKEW: segment kt = W3 (0, kt), (1, kt) + the W2 rows of tile kt + 1 (k_dec2's skew)
-  auto seg_skew = [&](float* dst, int kt, bool last) {
-    dma_tiles<DEC_NW>(dst, rm, F_W3 + kt * T, 1, wv, lane);
-    dma_tiles<DEC_NW>(dst + T, rm, F_W3 + (8 + kt) * T, 1, wv, lane);
-    if (!last) dma_tiles<DEC_NW>(dst + 2 * T, rm, F_W2 + (kt + 1) * 2 * T, 2, wv, lane);
-  };
   lds_dma_barrier();
   const Bias32 fb1[2] = {bias_ld(mlp + F_B1, hf), bias_ld(mlp + F_B1 + 32, hf)};   // before the DMA
   __builtin_amdgcn_sched_barrier(0);
-  if (DEC1_SKEW) seg_skew(B1, 0, false);
-  else seg_feat23(B1, 0);
+  seg_feat23(B1, 0);
   // ---- layer 1: 64 -> 64
   {
     const XT<F16> xs[2] = {xop<F16>(x0[0]), xop<F16>(x0[1])};
@@ -351,50 +342,9 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
     tile_mma<F16>(hr[0], cur + 2 * T, h2, lane);
     tile_mma<F16>(hr[1], cur + 3 * T, h2, lane);
   };
-  if constexpr (DEC1_SKEW) {
-    // k_dec2's skew: layer 2 of tile kt + 1 issued before tile kt's sine + split; bit-identical
-    f32x16 acc = f32x16{0};
-    tile_mma<F16>(acc, B0 + 4 * T, x1s[0], lane);
-    tile_mma<F16>(acc, B0 + 5 * T, x1s[1], lane);
-    // dma: 1 a full segment, 2 the last (no W2 rows), 3 flow layers 0 / 1
-    auto step = [&](int kt, int dma, bool nx) {
-      lds_dma_barrier();
-      const Bias32 b2 = bias_ld(mlp + F_B2 + kt * 32, hf);
-      __builtin_amdgcn_sched_barrier(0);
-      float* cur = (kt & 1) ? B0 : B1;
-      float* nxt = (kt & 1) ? B1 : B0;
-      if (dma < 3) seg_skew(nxt, kt + 1, dma == 2);
-      else {
-        dma_tiles<DEC_NW>(nxt, rm, L_W0, 4, wv, lane);
-        dma_tiles<DEC_NW>(nxt + 4 * T, rm, L_W1, 4, wv, lane);
-      }
-      f32x16 an = f32x16{0};
-      if (nx) {
-        tile_mma<F16, DEC1_SKEW == 1>(an, cur + 2 * T, x1s[0], lane);
-        tile_mma<F16, DEC1_SKEW == 1>(an, cur + 3 * T, x1s[1], lane);
-      }
-      const XT<F16> h2 = xop<F16>(bias_sin<F16>(acc, b2));
-      if (DEC1_SKEW == 2 && nx) {
-#pragma unroll
-        for (int i = 0; i < 12; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
-          __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);   // VALU
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      tile_mma<F16>(hr[0], cur, h2, lane);
-      tile_mma<F16>(hr[1], cur + T, h2, lane);
-      if (nx) acc = an;
-    };
-#pragma unroll 1
-    for (int kt = 0; kt < 6; ++kt) step(kt, 1, true);
-    step(6, 2, true);
-    step(7, 3, false);
-  } else {
 #pragma unroll 1
   for (int kt = 0; kt < 7; ++kt) feat_step(kt, false);
   feat_step(7, true);
-  }
 #pragma unroll
   for (int ot = 0; ot < 2; ++ot) hr[ot] = bias_add<F16>(hr[ot], mlp + F_B3 + ot * 32, hf);
   if (valid) {
@@ -478,40 +428,6 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
   }
   const XT<F16> x1f[2] = {xop<F16>(x1[0]), xop<F16>(x1[1])};
   float fl[4] = {0.f, 0.f, 0.f, 0.f};
-  if constexpr (DEC1_SKEW) {
-    // step kt: layer 2 of tile kt (segment kt), then the sine + layer-3 dot of tile kt - 1 (W3V is
-    // resident, so the segments stay as they are)
-    f32x16 ap = f32x16{0};
-    auto fstep = [&](int kt, bool dma) {
-      lds_dma_barrier();
-      const Bias32 b2 = bias_ld(mlp + L_B2 + (kt > 0 ? kt - 1 : 0) * 32, hf);
-      __builtin_amdgcn_sched_barrier(0);
-      float* cur = (kt & 1) ? B1 : B0;
-      float* nxt = (kt & 1) ? B0 : B1;
-      if (dma) seg_flow23(nxt, kt + 1);
-      f32x16 an = f32x16{0};
-      tile_mma<F16, DEC1_SKEW == 1>(an, cur, x1f[0], lane);
-      tile_mma<F16, DEC1_SKEW == 1>(an, cur + T, x1f[1], lane);
-      if (kt > 0) {
-        const f32x16 h2 = bias_sin<F16>(ap, b2);
-        narrow_dot<4>(fl, W3V, kt - 1, h2, hf);
-        if (DEC1_SKEW == 2) {
-#pragma unroll
-          for (int i = 0; i < 12; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
-            __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);   // VALU
-          }
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      ap = an;
-    };
-    fstep(0, true);
-#pragma unroll 1
-    for (int kt = 1; kt < 7; ++kt) fstep(kt, true);
-    fstep(7, false);
-    narrow_dot<4>(fl, W3V, 7, bias_sin<F16>(ap, mlp + L_B2 + 7 * 32, hf), hf);
-  } else {
   auto flow_step = [&](int kt, bool last) {   // kt = 7 peeled (see feat_step)
     lds_dma_barrier();
     const Bias32 b2 = bias_ld(mlp + L_B2 + kt * 32, hf);   // before the DMA (see feat_step)
@@ -528,7 +444,6 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
 #pragma unroll 1
   for (int kt = 0; kt < 7; ++kt) flow_step(kt, false);
   flow_step(7, true);
-  }
 #pragma unroll
   for (int c = 0; c < 4; ++c) fl[c] += __shfl_xor(fl[c], 32);   // the other lane half's 128 features
   if (valid && hf == 0) {
@@ -603,7 +518,6 @@ __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DE
     gather64(q, HRF, 64, 0, bilin(g1x, g1y, WW, HH), hf);   // q_feat1 -> W0 columns 0..63
     lds_dma_barrier();
     dma_tiles<DEC2_NW>(B1, rm, E_W1, 4, wv, lane);
-    if (DEC2_SKEW) dma_tiles<DEC2_NW>(B1 + 4 * T, rm, E_W2, 2, wv, lane);   // layer-2 rows of tile 0
     {
       const XT<F16> qs[2] = {xop<F16>(q[0]), xop<F16>(q[1])};
 #pragma unroll
@@ -625,79 +539,6 @@ __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DE
   lds_dma_barrier();
   const Bias32 eb1[2] = {bias_ld(mlp + E_B1, hf), bias_ld(mlp + E_B1 + 32, hf)};   // before the DMA
   __builtin_amdgcn_sched_barrier(0);
-  float o4[3] = {0.f, 0.f, 0.f};
-  if constexpr (DEC2_SKEW) {
-    // Layers 2 and 3 skewed by one tile: step kt issues layer 2's MFMAs of tile kt + 1 first, then the
-    // sine + split of tile kt (computed one step earlier, so no wait on a just-issued MFMA) placed among
-    // them, then layer 3's MFMAs of tile kt.  Segment kt = column kt of W3 (8 tiles) + the W2 rows of
-    // tile kt + 1 (2 tiles); segment 7 = column 7 + W4V (plain rows + the layer-3 biases).  The W2 rows
-    // of tile 0 came with W1.  Every accumulator sees the same MFMAs in the same order as the unskewed
-    // loop: bit-identical.
-    auto seg = [&](float* dst, int kt, bool last) {
-#pragma unroll
-      for (int ot = 0; ot < 8; ++ot) dma_tiles<DEC2_NW>(dst + ot * T, rm, E_W3 + (ot * 8 + kt) * T, 1, wv, lane);
-      if (!last) dma_tiles<DEC2_NW>(dst + 8 * T, rm, E_W2 + (kt + 1) * 2 * T, 2, wv, lane);
-      else dma_tiles<DEC2_NW>(dst + 8 * T, rm, E_W4V, 1, wv, lane);
-    };
-    seg(B0, 0, false);
-    f32x16 x1[2];
-    {
-      const XT<F16> xs[2] = {xop<F16>(x0[0]), xop<F16>(x0[1])};
-#pragma unroll
-      for (int ot = 0; ot < 2; ++ot) {
-        f32x16 acc = f32x16{0};
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt) tile_mma<F16>(acc, B1 + (ot * 2 + kt) * T, xs[kt], lane);
-        x1[ot] = bias_sin<F16>(acc, eb1[ot]);
-      }
-    }
-    const XT<F16> x1s[2] = {xop<F16>(x1[0]), xop<F16>(x1[1])};
-    f32x16 acc = f32x16{0};
-    tile_mma<F16>(acc, B1 + 4 * T, x1s[0], lane);
-    tile_mma<F16>(acc, B1 + 5 * T, x1s[1], lane);
-    f32x16 a3[8];
-#pragma unroll
-    for (int ot = 0; ot < 8; ++ot) a3[ot] = f32x16{0};
-    // dma: 0 none, 1 a middle segment, 2 the last one; nx: layer 2 of tile kt + 1 runs in this step
-    auto step = [&](int kt, int dma, bool nx) {
-      lds_dma_barrier();
-      const Bias32 b2 = bias_ld(mlp + E_B2 + kt * 32, hf);   // before the DMA (see k_dec1)
-      __builtin_amdgcn_sched_barrier(0);
-      float* cur = (kt & 1) ? B1 : B0;
-      float* nxt = (kt & 1) ? B0 : B1;
-      if (dma) seg(nxt, kt + 1, dma == 2);
-      f32x16 an = f32x16{0};
-      if (nx) {
-        tile_mma<F16, DEC2_SKEW == 1>(an, cur + 8 * T, x1s[0], lane);
-        tile_mma<F16, DEC2_SKEW == 1>(an, cur + 9 * T, x1s[1], lane);
-      }
-      const XT<F16> h2 = xop<F16>(bias_sin<F16>(acc, b2));
-      if (DEC2_SKEW == 2 && nx) {
-        // 12 MFMAs of layer 2 (tile kt + 1) with the ~100 VALU of tile kt's sine + split in their gaps
-#pragma unroll
-        for (int i = 0; i < 12; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
-          __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);   // VALU
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int ot = 0; ot < 8; ++ot) tile_mma<F16>(a3[ot], cur + ot * T, h2, lane);
-      if (nx) acc = an;
-    };
-#pragma unroll 1
-    for (int kt = 0; kt < 6; ++kt) step(kt, 1, true);
-    step(6, 2, true);
-    step(7, 0, false);
-    // layer 3 sine streamed into layer 4 (256 -> 3, VALU dot products): W4V + the layer-3 biases sit
-    // after column 7 in segment 7 (B1), landed at step 7's barrier
-    const float* w4 = B1 + 8 * T;
-#pragma unroll
-    for (int kt = 0; kt < 8; ++kt) {
-      const f32x16 h3 = bias_sin<F16>(a3[kt], w4 + (E_W4V_B3 - E_W4V) + kt * 32, hf);
-      narrow_dot<3>(o4, w4, kt, h3, hf);
-    }
-  } else {
   auto seg_l23_first = [&](float* dst) {
     dma_tiles<DEC2_NW>(dst, rm, E_W2, 2, wv, lane);
 #pragma unroll
@@ -747,12 +588,12 @@ __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DE
   // layer 3 sine streamed into layer 4 (256 -> 3, linear, VALU dot products); W4 sits in B0 as
   // plain rows, followed by the layer-3 biases (E_W4V_B3; kt = 7 prefetch)
   lds_dma_barrier();
+  float o4[3] = {0.f, 0.f, 0.f};
 #pragma unroll
   for (int kt = 0; kt < 8; ++kt) {
     const f32x16 h3 = bias_sin<F16>(a3[kt], B0 + (E_W4V_B3 - E_W4V) + kt * 32, hf);
     narrow_dot<3>(o4, B0, kt, h3, hf);
   }
-  }   // DEC2_SKEW
 #pragma unroll
   for (int c = 0; c < 3; ++c) o4[c] += __shfl_xor(o4[c], 32);   // the other lane half's 128 features
   if (valid && hf == 0) {

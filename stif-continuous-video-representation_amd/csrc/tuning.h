@@ -42,13 +42,6 @@
 #ifndef DCNSEP_WPE
 #define DCNSEP_WPE 2       // waves per SIMD the kernel is register-budgeted for
 #endif
-#ifndef DCNSEP_PIPE
-// launches with at least this many tiles per CU run the software-pipelined k_dcn_sep_pipe (0: never)
-#define DCNSEP_PIPE 0
-#endif
-#ifndef DCNSEP_PIPE_IL
-#define DCNSEP_PIPE_IL 1   // k_dcn_sep_pipe: phase-2 sampling spread over the phase-1 MFMAs (0: before them)
-#endif
 #ifndef DCNSEP_EXP
 #define DCNSEP_EXP 0       // probes: 1 no phase 1, 3 no phase 2, 5 no per-pair restaging
 #endif
@@ -60,14 +53,6 @@ static_assert(DCNSEP_EXP == 0 || DCNSEP_EXP == 1 || DCNSEP_EXP == 3 || DCNSEP_EX
 // waves per k_dec1 workgroup (~240 VGPRs: 2 waves/SIMD); 4-wave workgroups, 2 per CU (80 KB LDS each):
 // the two waves sharing a SIMD come from different workgroups (4 vs 8 within noise, r01_knob_sweep.log)
 #define DEC1_NW 4
-#endif
-#ifndef DEC1_SKEW
-#define DEC1_SKEW 0        // k_dec1: the same skew for feat_imnet layers 2/3 and flow_imnet layers 2/3
-#endif
-#ifndef DEC2_SKEW
-// k_dec2 layers 2/3 skewed by one tile (layer 2 of tile kt + 1 issued before tile kt's sine): 0 off, 1 on,
-// 2 on with the sine + split interleaved into the layer-2 MFMAs by sched_group_barrier
-#define DEC2_SKEW 0
 #endif
 #ifndef DEC2_WPE
 #define DEC2_WPE 2         // waves per SIMD k_dec2 is register-budgeted for (2 workgroups/CU, 80 KB LDS each)

@@ -219,11 +219,10 @@ def dcn_sep_fusable(om_layer: PackedConv, layer: PackedConv) -> bool:
     return om_layer.mode == (L.PACK_DCNSEP | L.PACK_F16X3) and layer.mode == (L.PACK_DCNPAIR | L.PACK_F16X3)
 
 
-def dcn_sep(groups, *, epi=L.EPI_NONE, status=None, pipe=None):
+def dcn_sep(groups, *, epi=L.EPI_NONE, status=None):
     """Fused DCN_sep (dcn_v2.py:127-140): offset/mask conv + sigmoid + deformable conv in one launch.
     groups: list of {om_layer: PackedConv (STIF_PACK_DCNSEP | F16X3), layer: PackedConv (64->64 3x3,
-    STIF_PACK_DCNPAIR | F16X3), fea, inp, out} with NHWC [nitems, H, W, 64] tensors.  pipe: None = the
-    library's choice by launch size; True / False force the software-pipelined / per-tile kernel (test aid)."""
+    STIF_PACK_DCNPAIR | F16X3), fea, inp, out} with NHWC [nitems, H, W, 64] tensors."""
     if not 1 <= len(groups) <= L.MAXG:
         raise ValueError("dcn_sep: 1..8 groups")
     g0 = groups[0]
@@ -246,7 +245,7 @@ def dcn_sep(groups, *, epi=L.EPI_NONE, status=None, pipe=None):
     a.in_item = _item_stride([g["inp"] for g in groups], "dcn_sep in")
     a.out_item = _item_stride([g["out"] for g in groups], "dcn_sep out")
     a.ngroups, a.nitems, a.H, a.W, a.epi = len(groups), nitems, H, W, epi
-    a.flags = L.CONV_F16X3 | ({True: L.DCNSEP_PIPE_ON, False: L.DCNSEP_PIPE_OFF}.get(pipe, 0))
+    a.flags = L.CONV_F16X3
     a.status = _vp(status)
     tr = TRACE
     if tr is not None:

@@ -594,60 +594,3 @@ def test_dcn_sep_fused_reports_range(ops, L, which):
     ops.dcn_sep([dict(om_layer=om, layer=core, fea=fi, inp=xi, out=out)], status=st)
     assert int(st.item()) == 1, which
 
-
-@pytest.mark.parametrize("epi", ["none", "lrelu"])
-@pytest.mark.parametrize("shape", [(2, 9, 11, 1), (3, 37, 100, 2), (6, 64, 128, 3), (4, 70, 37, 8)],
-                         ids=["one_tile_per_wg", "partial_tiles", "several_tiles_per_wg", "eight_sets"])
-def test_dcn_sep_pipelined_bit_identical(ops, L, epi, shape):
-    """k_dcn_sep_pipe (phase 1 of tile i + 1 interleaved with phase 2 of tile i, one persistent workgroup per
-    CU) == the one-tile-per-workgroup k_dcn_sep, bit for bit, and == the oracle: workgroups with 1 tile (no
-    overlap: prologue + epilogue only), partial tiles in both directions, several tiles per workgroup (the
-    pipelined iterations, tiles of different weight sets following each other), up to 8 weight sets, offsets
-    that leave the staged margin (global fallback inside the pipelined steps)."""
-    B, H, W, G = shape
-    e = L.EPI_LRELU if epi == "lrelu" else L.EPI_NONE
-    sds = [_dcnsep_weights(200 + 10 * i, 2.0 + 2.5 * (i % 3)) for i in range(G)]
-    xs = torch.from_numpy(np.ascontiguousarray(np.stack([rnd(B, H, W, 64, seed=300 + i) for i in range(G)]))).cuda()
-    fs = torch.from_numpy(np.ascontiguousarray(np.stack([rnd(B, H, W, 64, seed=400 + i) for i in range(G)]))).cuda()
-    layers = [_dcnsep_layers(ops, L, sdx) for sdx in sds]
-    outs = {}
-    for pipe in (True, False):
-        out = torch.full((G, B, H, W, 64), float("nan"), device="cuda")
-        st = torch.zeros(1, dtype=torch.int32, device="cuda")
-        ops.dcn_sep([dict(om_layer=layers[i][0], layer=layers[i][1], fea=fs[i], inp=xs[i], out=out[i]) for i in range(G)],
-                    epi=e, status=st, pipe=pipe)
-        assert int(st.item()) == 0
-        outs[pipe] = out
-    assert torch.equal(outs[True], outs[False])
-    for i in sorted({0, G - 1}):
-        x = xs[i].cpu().numpy().transpose(0, 3, 1, 2)
-        f = fs[i].cpu().numpy().transpose(0, 3, 1, 2)
-        ref = O.dcn_sep(x, f, sds[i], "x")
-        if epi == "lrelu":
-            ref = O.lrelu(ref)
-        assert relmax(to_nchw(outs[True][i]), ref) < RTOL, i
-
-
-def test_dcn_sep_pipelined_deterministic_and_range(ops, L):
-    """The pipelined kernel: three launches agree bit for bit (the counted vmcnt waits leave no stage race),
-    and its range reporting works from both phases (a poisoned offset feature / DCN input sets the status)."""
-    B, H, W = 4, 64, 96
-    sdx = _dcnsep_weights(500, 3.0)
-    om, core = _dcnsep_layers(ops, L, sdx)
-    x = torch.from_numpy(rnd(B, H, W, 64, seed=501)).cuda()
-    f = torch.from_numpy(rnd(B, H, W, 64, seed=502)).cuda()
-    runs = []
-    for _ in range(3):
-        out = torch.full((B, H, W, 64), float("nan"), device="cuda")
-        ops.dcn_sep([dict(om_layer=om, layer=core, fea=f, inp=x, out=out)], pipe=True)
-        runs.append(out)
-    assert torch.equal(runs[0], runs[1]) and torch.equal(runs[0], runs[2])
-    for which in ("fea", "inp"):
-        st = torch.zeros(1, dtype=torch.int32, device="cuda")
-        fi, xi = f.clone(), x.clone()
-        if which == "fea":
-            fi[2, 40, 50, 3] = 5000.0
-        else:
-            xi[1, 20, 70, 33] = 1.0e6
-        ops.dcn_sep([dict(om_layer=om, layer=core, fea=fi, inp=xi, out=runs[0])], status=st, pipe=True)
-        assert int(st.item()) == 1, which

@@ -28,17 +28,19 @@ for v in $LIBS; do
   fi
 done
 if [ "${DUMP:-1}" != 0 ]; then
-  timeout -k 10 200 python -u tools/r4/dump_out.py 2>&1 | grep -v amdgpu.ids || exit 1
+  timeout -k 10 200 python -u tools/r4/dump_out.py 2>&1 | sed '/amdgpu.ids/d' || exit 1
   for v in $LIBS; do
     STIF_HIP_LIB=$R/$v TAG=$(basename $v .so) CMP=in-tree timeout -k 10 200 python -u tools/r4/dump_out.py 2>&1 \
-      | grep -v amdgpu.ids || exit 1
+      | sed '/amdgpu.ids/d' || exit 1
+    rm -f $O/out_$(basename $v .so).npy
   done
+  rm -f $O/out_in-tree.npy
 fi
 for rep in $(seq $REPS); do
   for v in in-tree $LIBS; do
     if [ "$v" != in-tree ]; then export STIF_HIP_LIB=$R/$v; else unset STIF_HIP_LIB; fi
     if [ -n "$MICRO" ]; then
-      echo "$v: $(timeout -k 10 200 bash -c "$MICRO" 2>&1 | grep -v amdgpu.ids | tr '\n' ' ')" || exit 1
+      echo "$v: $(timeout -k 10 200 bash -c "$MICRO" 2>&1 | sed '/amdgpu.ids/d' | tr '\n' ' ')" || exit 1
     fi
     timeout -k 10 300 python -u bench.py --no-extras --no-cpu-baseline --steps 20 --kernel-report > $O/ab.json 2> $O/ab.err \
       || { tail -30 $O/ab.err; exit 1; }
