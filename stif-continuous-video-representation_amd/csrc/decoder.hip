@@ -152,6 +152,36 @@ STIF_DEV void gather64(f32x16* dst, const float* __restrict__ base, int stride, 
   }
 }
 
+// gather64 with at most 16 corner loads (64 VGPRs) in flight: two memory latencies instead of one, for
+// kernels budgeted below the 128 VGPRs of the one-shot form
+STIF_DEV void gather64_h(f32x16* dst, const float* __restrict__ base, int stride, int c0, const Bilin& b, int hf) {
+  const int c = c0 + 4 * hf;
+  const float* p00 = base + (size_t)b.o00 * stride + c;
+  const float* p01 = base + (size_t)b.o01 * stride + c;
+  const float* p10 = base + (size_t)b.o10 * stride + c;
+  const float* p11 = base + (size_t)b.o11 * stride + c;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    f32x4 cr[4][4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int o = 8 * (4 * half + g);
+      cr[g][0] = ld4(p00 + o);
+      cr[g][1] = ld4(p01 + o);
+      cr[g][2] = ld4(p10 + o);
+      cr[g][3] = ld4(p11 + o);
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      f32x4 s = b.w00 * cr[g][0] + b.w01 * cr[g][1] + b.w10 * cr[g][2] + b.w11 * cr[g][3];
+      asm volatile("" : "+v"(s));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dst[half][4 * g + e] = s[e];
+    }
+    asm volatile("" ::: "memory");
+  }
+}
+
 // z[ot] += W_img . img: the 6 image channels (padded to 8) are one K chunk, so lane half h supplies
 // channels 4h..4h+3 as the B operand of the first 4 MFMAs of a packed tile (features F(e, h), e < 4)
 STIF_DEV void img_mma(f32x16* z, const float* __restrict__ wt, const f32x4 im4, int lane) {
@@ -174,9 +204,9 @@ STIF_DEV f32x4 img_sample(const float* __restrict__ I, const Bilin& b, int hf) {
 // (a few 4-KB tiles: one layer, or one output tile's K-tiles) is LDS-DMA'd while the previous one
 // is being consumed (double-buffered, one barrier per segment), and every wave reads its A
 // operands from LDS -- one tile feeds 16 MFMAs in each wave of the workgroup.
-// waves per workgroup of k_dec1 (~240 VGPRs: 2 waves/SIMD).  4-wave workgroups, 2 per CU (80 KB LDS
-// each): the two waves sharing a SIMD come from different workgroups, so one's segment barrier or
-// sin stretch overlaps the other's MFMAs
+// waves per workgroup of k_dec1: 4-wave workgroups, 3 per CU (DEC1_OCC: 52 KB LDS and <= 168 VGPRs each):
+// the waves sharing a SIMD come from different workgroups, so one's segment barrier, gather or sin
+// stretch overlaps the others' MFMAs
 constexpr int DEC_NW = DEC1_NW;
 constexpr int DEC2_NW = 4;   // k_dec2: 8 layer-3 accumulator tiles (128 VGPRs) live
 constexpr int SEG = 10;      // max tiles per segment (k_dec2)
@@ -249,19 +279,24 @@ STIF_DEV void narrow_dot(float* o, const float* W, int kt, const f32x16& x, int 
 // MODE 0: feat_imnet + flow_imnet fused (the flow stage reads the pixel's own HRfeat);
 // MODE 1: feat_imnet only; MODE 2: flow_imnet only, reading HRfeat at (hr_y, hr_x) of the query
 // (local ensemble).  HRIMG: the flow stage's image input comes from the high-resolution image.
+// DEC1_OCC = 3 (MODE 0 / 1): 6-tile segments (52 KB of LDS) and a 168-register budget, so three workgroups
+// (three waves per SIMD) share a CU; flow layer 1's second output tile then arrives after the last feat step
+template <int MODE>
+constexpr int S1 = (DEC1_OCC == 3 && MODE != 2) ? 6 : SEG1;
 template <int MODE, bool HRIMG, int F16>
-__global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))) void k_dec1(const float* __restrict__ proj, const float* __restrict__ mlp,
+__global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(MODE != 2 ? DEC1_OCC : 2))) void k_dec1(const float* __restrict__ proj, const float* __restrict__ mlp,
                                                      stif_dec_tables tb, stif_dec_image im,
                                                      const float* __restrict__ tq, float* __restrict__ hrfeat,
                                                      float* __restrict__ flow, int n, int h, int w, int HH,
                                                      int WW) {
   // two segment buffers of SEG1 tiles + the flow's last layer (plain [4][256], resident)
-  __shared__ __attribute__((aligned(16))) float wbuf[2 * SEG1 * T + T];
+  constexpr bool OCC3 = S1<MODE> != SEG1;
+  __shared__ __attribute__((aligned(16))) float wbuf[2 * S1<MODE> * T + T];
   const int lane = threadIdx.x & 63, hf = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
   float* const B0 = wbuf;
-  float* const B1 = wbuf + SEG1 * T;
-  float* const W3V = wbuf + 2 * SEG1 * T;
+  float* const B1 = wbuf + S1<MODE> * T;
+  float* const W3V = wbuf + 2 * S1<MODE> * T;
   const __amdgpu_buffer_rsrc_t rm = mlp_rsrc(mlp);
   if (MODE != 1) dma_tiles<DEC_NW>(W3V, rm, L_W3V, 1, wv, lane);
   // segment 0: feat layer 1 (4 tiles); segments 1..8: feat layer 2 tile kt + layer 3 (0, kt), (1, kt)
@@ -331,9 +366,9 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
     float* cur = (kt & 1) ? B0 : B1;
     float* nxt = (kt & 1) ? B1 : B0;
     if (!last) seg_feat23(nxt, kt + 1);
-    else {   // prefetch flow layer 0 (4 tiles) + layer 1 (4 tiles)
+    else {   // prefetch flow layer 0 (4 tiles) + layer 1 (4 tiles; OCC3: its first output tile)
       dma_tiles<DEC_NW>(nxt, rm, L_W0, 4, wv, lane);
-      dma_tiles<DEC_NW>(nxt + 4 * T, rm, L_W1, 4, wv, lane);
+      dma_tiles<DEC_NW>(nxt + 4 * T, rm, L_W1, OCC3 ? 2 : 4, wv, lane);
     }
     f32x16 acc = f32x16{0};
     tile_mma<F16>(acc, cur, x1s[0], lane);
@@ -379,7 +414,8 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
     const float wy0 = tb.wy0[py], wy1 = tb.wy1[py], wx0 = tb.wx0[px], wx1 = tb.wx1[px];
     b.o00 = y0 * w + x0_; b.o01 = y0 * w + x1_; b.o10 = y1 * w + x0_; b.o11 = y1 * w + x1_;
     b.w00 = wx0 * wy0; b.w01 = wx1 * wy0; b.w10 = wx0 * wy1; b.w11 = wx1 * wy1;
-    gather64(z, P, PROJ_C, 64, b, hf);
+    if (OCC3) gather64_h(z, P, PROJ_C, 64, b, hf);
+    else gather64(z, P, PROJ_C, 64, b, hf);
 #pragma unroll
     for (int ot = 0; ot < 2; ++ot)
 #pragma unroll
@@ -405,7 +441,10 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
   auto seg_flow23 = [&](float* dst, int kt) {   // W2 rows kt (2 tiles); W3 is resident (W3V)
     dma_tiles<DEC_NW>(dst, rm, L_W2 + kt * 2 * T, 2, wv, lane);
   };
-  seg_flow23(B0, 0);
+  // OCC3: layer 1's second output tile (2 tiles) into B0, segment 0 after it
+  constexpr bool L1B0 = OCC3 && MODE == 0;
+  if (L1B0) dma_tiles<DEC_NW>(B0, rm, L_W1 + 2 * T, 2, wv, lane);
+  seg_flow23(B0 + (L1B0 ? 2 * T : 0), 0);
   {
     const XT<F16> hs[2] = {xop<F16>(hr[0]), xop<F16>(hr[1])};
 #pragma unroll
@@ -416,13 +455,15 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
       for (int r = 0; r < 16; ++r) z[ot][r] = siren_sin<F16>(z[ot][r] * ACC_S<F16>);
     }
   }
+  if (L1B0) lds_dma_barrier();   // layer 1's second output tile landed in B0
   {
     const XT<F16> zs[2] = {xop<F16>(z[0]), xop<F16>(z[1])};
 #pragma unroll
     for (int ot = 0; ot < 2; ++ot) {
       f32x16 acc = f32x16{0};
+      const float* w1t = (L1B0 && ot == 1) ? B0 : B1 + (4 + ot * 2) * T;
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) tile_mma<F16>(acc, B1 + (4 + ot * 2 + kt) * T, zs[kt], lane);
+      for (int kt = 0; kt < 2; ++kt) tile_mma<F16>(acc, w1t + kt * T, zs[kt], lane);
       x1[ot] = bias_sin<F16>(acc, lb1[ot]);
     }
   }
@@ -432,7 +473,7 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(2))
     lds_dma_barrier();
     const Bias32 b2 = bias_ld(mlp + L_B2 + kt * 32, hf);   // before the DMA (see feat_step)
     __builtin_amdgcn_sched_barrier(0);
-    float* cur = (kt & 1) ? B1 : B0;
+    float* cur = (kt & 1) ? B1 : (L1B0 && kt == 0 ? B0 + 2 * T : B0);
     float* nxt = (kt & 1) ? B0 : B1;
     if (!last) seg_flow23(nxt, kt + 1);
     f32x16 acc = f32x16{0};

@@ -54,6 +54,11 @@ static_assert(DCNSEP_EXP == 0 || DCNSEP_EXP == 1 || DCNSEP_EXP == 3 || DCNSEP_EX
 // the two waves sharing a SIMD come from different workgroups (4 vs 8 within noise, r01_knob_sweep.log)
 #define DEC1_NW 4
 #endif
+#ifndef DEC1_OCC
+// k_dec1 (MODE 0 / 1) workgroups per CU: 3 (52 KB LDS, 168 registers, the flow projection gathered in two
+// halves) or 2 (69 KB, 256): C0 dec1 869 -> 758 us, C2 12.6 -> 11.5 ms, bit-identical (r04_dec1_occ_ab.log)
+#define DEC1_OCC 3
+#endif
 #ifndef DEC2_WPE
 #define DEC2_WPE 2         // waves per SIMD k_dec2 is register-budgeted for (2 workgroups/CU, 80 KB LDS each)
 #endif

@@ -1,32 +1,32 @@
-"""Per-dispatch view of a rocprofv3 --kernel-trace CSV: the dispatches of the last N_STEP_KERNELS (default: the
-dispatches after the last gap >= 2 ms, i.e. the last bench step), each with its workgroup count and duration,
-and the time in launches that fill less than one round of the chip (< 512 four-wave workgroups).
-usage: python tools/r4/ktrace.py run_kernel_trace.csv"""
+"""Per-dispatch view of a rocprofv3 --kernel-trace CSV: the last bench step (from the last k_conv_first dispatch
+on), each dispatch's workgroup count and duration (with -v), and per kernel the time in dispatches that launch
+fewer workgroups than one round of the chip (512 = two per CU).
+usage: python tools/r4/ktrace.py run_kernel_trace.csv [-v]"""
 import csv
 import sys
 from collections import defaultdict
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-# the last step: walk back from the end until a gap of >= 2 ms (the bench's barrier / sync between steps)
-i = len(rows) - 1
-while i > 0 and int(rows[i]["Start_Timestamp"]) - int(rows[i - 1]["End_Timestamp"]) < 2_000_000:
-    i -= 1
-step = rows[i:]
+first = max(i for i, r in enumerate(rows) if "k_conv_first" in r["Kernel_Name"])
+step = rows[first:]
 t0, t1 = int(step[0]["Start_Timestamp"]), int(step[-1]["End_Timestamp"])
 busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in step)
 print(f"last step: {len(step)} dispatches, span {(t1 - t0) / 1e6:.3f} ms, kernel time {busy / 1e6:.3f} ms")
 small = defaultdict(lambda: [0, 0.0])
+allk = defaultdict(lambda: [0, 0.0])
 for r in step:
-    wg = int(r["Grid_Size"]) // max(1, int(r["Workgroup_Size"]))
+    wg = int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"]))
     d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-    name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")[:60]
+    name = r["Kernel_Name"].split("(stif")[0].split("(float")[0].replace("void ", "").replace("(anonymous namespace)::", "")[:48]
+    allk[name][0] += 1
+    allk[name][1] += d
     if wg < 512:
         small[name][0] += 1
         small[name][1] += d
-    if len(sys.argv) > 2:
+    if "-v" in sys.argv:
         print(f"  {d:8.1f} us  {wg:7d} WG  {name}")
 tot = sum(v[1] for v in small.values())
 print(f"dispatches with < 512 workgroups: {sum(v[0] for v in small.values())}, {tot / 1e3:.3f} ms")
 for k, (n, d) in sorted(small.items(), key=lambda kv: -kv[1][1]):
-    print(f"  {n:4d} x {d / n:7.1f} us = {d / 1e3:6.3f} ms  {k}")
+    print(f"  {n:4d} x {d / n:7.1f} us = {d / 1e3:6.3f} ms  {k}   (all: {allk[k][0]} x, {allk[k][1] / 1e3:.3f} ms)")
