@@ -25,12 +25,16 @@ def main():
     shards = P.pair_shards(nframes, world)
     a, b = shards[rank]
     res = {"shard": (a, b)}
+    fr = None
     if b > a:
         fr = torch.empty(b - a, 3, H, W)
         for i in range(b - a):
             fr[i] = torch.rand(3, H, W, generator=torch.Generator().manual_seed(1234 + a + i))
-        with torch.no_grad():
-            P.gen_feat_shard(m, fr.cuda(), rank, world, shards=shards, exchange=True)
+        fr = fr.cuda()
+    with torch.no_grad():
+        # every rank calls it, an empty shard too (frames=None: it only joins the first call's barrier)
+        P.gen_feat_shard(m, fr, rank, world, shards=shards, exchange=True)
+        if fr is not None:
             res["feat"] = m.feat.cpu().clone()
             res["out"] = m.decoding([torch.tensor([[0.5]])])[0].cpu()
     torch.save(res, os.path.join(outdir, f"r{rank}.pt"))
