@@ -14,6 +14,9 @@
 #ifndef WINO_OM_SCHED
 #define WINO_OM_SCHED 1    // a scheduling barrier after every k_wino_om B block (keeps the B loads early)
 #endif
+#ifndef WINO_TAIL
+#define WINO_TAIL 0        // k_wino: which workgroups of an XCD take the remainder tiles (see wg_rank)
+#endif
 #ifndef WINO_EXP
 #define WINO_EXP 0         // probes: 1 no LDS-DMA after the first phase, 2 no B refills, 3 no output exchange
 #endif
