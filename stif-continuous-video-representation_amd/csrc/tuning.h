@@ -14,9 +14,6 @@
 #ifndef WINO_OM_SCHED
 #define WINO_OM_SCHED 1    // a scheduling barrier after every k_wino_om B block (keeps the B loads early)
 #endif
-#ifndef WINO_TAIL
-#define WINO_TAIL 0        // k_wino: which workgroups of an XCD take the remainder tiles (see wg_rank)
-#endif
 #ifndef WINO_EXP
 #define WINO_EXP 0         // probes: 1 no LDS-DMA after the first phase, 2 no B refills, 3 no output exchange
 #endif
@@ -61,6 +58,9 @@ static_assert(DCNSEP_EXP == 0 || DCNSEP_EXP == 1 || DCNSEP_EXP == 3 || DCNSEP_EX
 // k_dec1 (MODE 0 / 1) workgroups per CU: 3 (52 KB LDS, 168 registers, the flow projection gathered in two
 // halves) or 2 (69 KB, 256): C0 dec1 869 -> 758 us, C2 12.6 -> 11.5 ms, bit-identical (r04_dec1_occ_ab.log)
 #define DEC1_OCC 3
+#endif
+#ifndef DEC2_OCC
+#define DEC2_OCC 2         // k_dec2 workgroups per CU: 2 (k_dec2) or 3 (k_dec2o: two-pass layer 3, 52 KB LDS)
 #endif
 #ifndef DEC2_WPE
 #define DEC2_WPE 2         // waves per SIMD k_dec2 is register-budgeted for (2 workgroups/CU, 80 KB LDS each)

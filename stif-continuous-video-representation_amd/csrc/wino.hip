@@ -87,15 +87,6 @@ constexpr int UP_R = 4, UP_C = 18;                    // coarse rows / columns p
 constexpr int SCR_F = UP_R * UP_C * 2 * PSUB * 4;      // scratch floats: [row][col][chunk][4]
 constexpr int SCR_INS = (UP_R * UP_C * 2 * PSUB + 63) / 64;
 
-// Rank of workgroup j of an XCD's nl in its tile stride (tiles j', j' + nl, ...).  With a tile count that is not
-// a multiple of nl, the ranks below the remainder take one tile more.  WINO_TAIL = 1 gives those extra tiles
-// to the even-numbered workgroups (rank (j & 1) * nl / 2 + j / 2) instead of the first half -- which spreads
-// them one per CU when the dispatcher places workgroups 2k and 2k + 1 of an XCD on the same CU.
-STIF_DEV int wg_rank(int j, int nl) {
-  if (WINO_TAIL && !(nl & 1)) return (j & 1) * (nl >> 1) + (j >> 1);
-  return j;
-}
-
 struct Tile {
   int oy0, ox0, slice, g, n;
   const float* src0;   // the item's input maps (k_wino: in0 and in1 of group g, item n), loaded from the
@@ -242,7 +233,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   const int xcd = blockIdx.x & 7, nl = gridDim.x >> 3;   // host: grid is a multiple of 8
   const int per = (ntiles + 7) >> 3;
   const int tend = min((xcd + 1) * per, ntiles);
-  int T = xcd * per + wg_rank(blockIdx.x >> 3, nl);
+  int T = xcd * per + (blockIdx.x >> 3);
   if (T >= tend) return;
   Tile cur = tile_of(T);
   const float* wsl = wbase(cur);
@@ -671,7 +662,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   const int xcd = blockIdx.x & 7, nl = gridDim.x >> 3;
   const int per = (ntiles + 7) >> 3;
   const int tend = min((xcd + 1) * per, ntiles);
-  int T = xcd * per + wg_rank(blockIdx.x >> 3, nl);
+  int T = xcd * per + (blockIdx.x >> 3);
   if (T >= tend) return;
   Tile cur = tile_of(T);
   __amdgpu_buffer_rsrc_t wr = wres(cur.g);
