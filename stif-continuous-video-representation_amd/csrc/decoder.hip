@@ -653,172 +653,6 @@ __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DE
   }
 }
 
-// k_dec2 at three workgroups per CU (DEC2_OCC = 3): <= 168 registers and 52 KB of LDS per 4-wave
-// workgroup.  The 8 layer-3 accumulator tiles (128 registers) of k_dec2 become two passes of 4 (layer 2 is
-// recomputed in the second pass: +96 MFMAs per 32 pixels), the 64-channel gathers keep 16 loads in flight
-// (gather64_h), and the weights stream in 6-tile segments: [W2 rows kt (2) + W3 tiles (4 p + ot, kt), ot < 4]
-// per (pass p, tile kt); W0 (8 tiles) is split over both buffers, W4V + the layer-3 biases sit in a resident
-// slot.  Every accumulator and o4 sees the same MFMAs / FMAs in the same order as k_dec2: bit-identical.
-constexpr int SEGO = 6;
-template <bool HRIMG, int F16>
-__global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(3))) void k_dec2o(const float* __restrict__ proj, const float* __restrict__ mlp,
-                                                     const float* __restrict__ hrfeat, const float* __restrict__ flow,
-                                                     stif_dec_tables tb, stif_dec_image im,
-                                                     const float* __restrict__ tq, float* __restrict__ out, int n,
-                                                     int h, int w, int HH, int WW, int* status) {
-  __shared__ __attribute__((aligned(16))) float wbuf[2 * SEGO * T + T];
-  const int lane = threadIdx.x & 63, hf = lane >> 5;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
-  float* const B0 = wbuf;
-  float* const B1 = wbuf + SEGO * T;
-  float* const W4S = wbuf + 2 * SEGO * T;
-  const __amdgpu_buffer_rsrc_t rm = mlp_rsrc(mlp);
-  // W0 tile (ot, kt) = E_W0 + (4 ot + kt) T: the q_feat1 columns (kt 0, 1) into B0, q_feat2's (kt 2, 3) into B1
-#pragma unroll
-  for (int ot = 0; ot < 2; ++ot) {
-    dma_tiles<DEC2_NW>(B0 + 2 * ot * T, rm, E_W0 + 4 * ot * T, 2, wv, lane);
-    dma_tiles<DEC2_NW>(B1 + 2 * ot * T, rm, E_W0 + (4 * ot + 2) * T, 2, wv, lane);
-  }
-  dma_tiles<DEC2_NW>(W4S, rm, E_W4V, 1, wv, lane);
-  const long long total = (long long)n * HH * WW;
-  const long long p = ((long long)xcd_block(blockIdx.x, gridDim.x) * DEC2_NW + wv) * 32 + (lane & 31);
-  const bool valid = p < total;
-  const long long pc = valid ? p : total - 1;
-  const int item = (int)(pc / ((long long)HH * WW));
-  const int rem = (int)(pc - (long long)item * HH * WW);
-  const int py = rem / WW, px = rem - py * WW;
-  const float t = tq[item];
-  const float* P = proj + (size_t)item * h * w * PROJ_C;
-  const float* HRF = hrfeat + (size_t)item * HH * WW * 64;
-
-  // warpgrid (warplayer.py:25-39) and the decoder's clamp (Sakuya_arch_test.py:428,441), as k_dec2
-  const f32x4 fv = ld4(flow + (size_t)pc * 4);
-  const float lo = -1.f + 1e-6f, hi = 1.f - 1e-6f;
-  const float dx = ((float)WW - 1.f) / 2.f, dy = ((float)HH - 1.f) / 2.f;
-  const float bx = tb.lin_x[px], by = tb.lin_y[py];
-  const float g1x = fminf(fmaxf(bx + fv[0] / dx, lo), hi), g1y = fminf(fmaxf(by + fv[1] / dy, lo), hi);
-  const float g2x = fminf(fmaxf(bx + fv[2] / dx, lo), hi), g2y = fminf(fmaxf(by + fv[3] / dy, lo), hi);
-
-  auto seg = [&](float* dst, int pp, int kt) {   // (pass pp, tile kt)
-    dma_tiles<DEC2_NW>(dst, rm, E_W2 + kt * 2 * T, 2, wv, lane);
-#pragma unroll
-    for (int ot = 0; ot < 4; ++ot) dma_tiles<DEC2_NW>(dst + (2 + ot) * T, rm, E_W3 + ((4 * pp + ot) * 8 + kt) * T, 1, wv, lane);
-  };
-  // ---- encode_imnet layer 0 (k_dec2's order of operations)
-  f32x16 x0[2];
-  {
-    f32x16 z[2], q[2];
-    gather64_h(z, P, PROJ_C, 128, bilin(g1x, g1y, w, h), hf);
-    asm volatile("" ::: "memory");
-    gather64_h(q, P, PROJ_C, 192, bilin(g2x, g2y, w, h), hf);
-#pragma unroll
-    for (int ot = 0; ot < 2; ++ot)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int f = ot * 32 + 8 * v + 4 * hf;
-        const f32x4 wt = ld4(mlp + E_WT + f), bb = ld4(mlp + E_B0 + f);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) z[ot][4 * v + e] = (z[ot][4 * v + e] + (q[ot][4 * v + e] + wt[e] * t + bb[e])) * ACC_IN<F16>;
-      }
-    if constexpr (HRIMG) {
-      const float* I = im.img + (size_t)item * im.ih * im.iw * IMG_C;
-      img_mma(z, mlp + I_E1, img_sample(I, bilin(g1x, g1y, im.iw, im.ih), hf), lane);
-      img_mma(z, mlp + I_E2, img_sample(I, bilin(g2x, g2y, im.iw, im.ih), hf), lane);
-    }
-    asm volatile("" ::: "memory");
-    gather64_h(q, HRF, 64, 0, bilin(g1x, g1y, WW, HH), hf);   // q_feat1 -> W0 columns 0..63 (B0)
-    lds_dma_barrier();
-    {
-      const XT<F16> qs[2] = {xop<F16>(q[0]), xop<F16>(q[1])};
-#pragma unroll
-      for (int ot = 0; ot < 2; ++ot)
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt) tile_mma<F16>(z[ot], B0 + (ot * 2 + kt) * T, qs[kt], lane);
-    }
-    __syncthreads();                                          // every wave is done with B0
-    dma_tiles<DEC2_NW>(B0, rm, E_W1, 4, wv, lane);            // layer 1, landing under the next gather
-    asm volatile("" ::: "memory");
-    gather64_h(q, HRF, 64, 0, bilin(g2x, g2y, WW, HH), hf);   // q_feat2 -> W0 columns 64..127 (B1)
-    const XT<F16> qs[2] = {xop<F16>(q[0]), xop<F16>(q[1])};
-#pragma unroll
-    for (int ot = 0; ot < 2; ++ot) {
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) tile_mma<F16>(z[ot], B1 + (ot * 2 + kt) * T, qs[kt], lane);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) x0[ot][r] = siren_sin<F16>(z[ot][r] * ACC_S<F16>);
-    }
-  }
-  lds_dma_barrier();                                          // W1 landed, B1 free
-  const Bias32 eb1[2] = {bias_ld(mlp + E_B1, hf), bias_ld(mlp + E_B1 + 32, hf)};   // before the DMA
-  __builtin_amdgcn_sched_barrier(0);
-  seg(B1, 0, 0);
-  f32x16 x1[2];
-  {
-    const XT<F16> xs[2] = {xop<F16>(x0[0]), xop<F16>(x0[1])};
-#pragma unroll
-    for (int ot = 0; ot < 2; ++ot) {
-      f32x16 acc = f32x16{0};
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) tile_mma<F16>(acc, B0 + (ot * 2 + kt) * T, xs[kt], lane);
-      x1[ot] = bias_sin<F16>(acc, eb1[ot]);
-    }
-  }
-  const XT<F16> x1s[2] = {xop<F16>(x1[0]), xop<F16>(x1[1])};
-  float o4[3] = {0.f, 0.f, 0.f};
-  f32x16 a3[4];
-  // step s = 8 pp + kt reads segment s from (s & 1) ? B0 : B1 and DMAs segment s + 1 into the other buffer
-  auto step = [&](int pp, int kt, bool dma) {
-    lds_dma_barrier();
-    const Bias32 b2 = bias_ld(mlp + E_B2 + kt * 32, hf);   // before the DMA (see k_dec1)
-    __builtin_amdgcn_sched_barrier(0);
-    float* cur = (kt & 1) ? B0 : B1;
-    float* nxt = (kt & 1) ? B1 : B0;
-    if (dma) seg(nxt, kt == 7 ? pp + 1 : pp, kt == 7 ? 0 : kt + 1);
-    f32x16 acc = f32x16{0};
-    tile_mma<F16>(acc, cur, x1s[0], lane);
-    tile_mma<F16>(acc, cur + T, x1s[1], lane);
-    const XT<F16> h2 = xop<F16>(bias_sin<F16>(acc, b2));
-#pragma unroll
-    for (int ot = 0; ot < 4; ++ot) tile_mma<F16>(a3[ot], cur + (2 + ot) * T, h2, lane);
-  };
-  // layer 3's sine of the pass's 4 output tiles streamed into layer 4 (W4V resident in W4S)
-  auto layer4 = [&](int pp) {
-#pragma unroll
-    for (int ot = 0; ot < 4; ++ot) {
-      const f32x16 h3 = bias_sin<F16>(a3[ot], W4S + (E_W4V_B3 - E_W4V) + (4 * pp + ot) * 32, hf);
-      narrow_dot<3>(o4, W4S, 4 * pp + ot, h3, hf);
-    }
-    // pin the pass's layer-4 sums here: o4 is only read at the end, and the compiler would otherwise sink
-    // pass 0's layer 4 below pass 1, keeping its four accumulator tiles live across it (300 spilled VGPRs)
-    asm volatile("" : "+v"(o4[0]), "+v"(o4[1]), "+v"(o4[2]));
-  };
-#pragma unroll
-  for (int ot = 0; ot < 4; ++ot) a3[ot] = f32x16{0};
-#pragma unroll 1
-  for (int kt = 0; kt < 8; ++kt) step(0, kt, true);
-  layer4(0);
-#pragma unroll
-  for (int ot = 0; ot < 4; ++ot) a3[ot] = f32x16{0};
-#pragma unroll 1
-  for (int kt = 0; kt < 7; ++kt) step(1, kt, true);
-  step(1, 7, false);
-  layer4(1);
-#pragma unroll
-  for (int c = 0; c < 3; ++c) o4[c] += __shfl_xor(o4[c], 32);   // the other lane half's 128 features
-  if (valid && hf == 0) {
-    const size_t plane = (size_t)HH * WW;
-    float* o = out + (size_t)item * 3 * plane + (size_t)py * WW + px;
-    bool bad = not_finite((fv[0] + fv[1]) + (fv[2] + fv[3]));
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      const float v = o4[c] + mlp[E_B4 + c];
-      bad |= not_finite(v);
-      o[c * plane] = v;
-    }
-    if (F16) report_range(status, bad);
-  }
-}
-
 __global__ __launch_bounds__(256) void k_pack_lr(const float* __restrict__ f0, const float* __restrict__ f1,
                                                  const float* __restrict__ f2, const float* __restrict__ x,
                                                  float* __restrict__ out, int n, int h, int w) {
@@ -939,13 +773,6 @@ extern "C" int stif_dec_stage2_ex(const float* proj, const float* mlp, const flo
   const stif_dec_image im = img ? *img : stif_dec_image{};
   hipStream_t st = (hipStream_t)stream;
   const dim3 g((unsigned)blocks), b(DEC2_NW * 64);
-  if (DEC2_OCC == 3) {
-    if (img && f16) hipLaunchKernelGGL((k_dec2o<true, 1>), g, b, 0, st, proj, mlp, hrfeat, flow, *tab, im, t, out, n, h, w, HH, WW, status);
-    else if (img) hipLaunchKernelGGL((k_dec2o<true, 0>), g, b, 0, st, proj, mlp, hrfeat, flow, *tab, im, t, out, n, h, w, HH, WW, status);
-    else if (f16) hipLaunchKernelGGL((k_dec2o<false, 1>), g, b, 0, st, proj, mlp, hrfeat, flow, *tab, im, t, out, n, h, w, HH, WW, status);
-    else hipLaunchKernelGGL((k_dec2o<false, 0>), g, b, 0, st, proj, mlp, hrfeat, flow, *tab, im, t, out, n, h, w, HH, WW, status);
-    return stif_check_launch("stif_dec_stage2");
-  }
   if (img && f16) hipLaunchKernelGGL((k_dec2<true, 1>), g, b, 0, st, proj, mlp, hrfeat, flow, *tab, im, t, out, n, h, w, HH, WW, status);
   else if (img) hipLaunchKernelGGL((k_dec2<true, 0>), g, b, 0, st, proj, mlp, hrfeat, flow, *tab, im, t, out, n, h, w, HH, WW, status);
   else if (f16) hipLaunchKernelGGL((k_dec2<false, 1>), g, b, 0, st, proj, mlp, hrfeat, flow, *tab, im, t, out, n, h, w, HH, WW, status);

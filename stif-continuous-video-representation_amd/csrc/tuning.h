@@ -59,9 +59,6 @@ static_assert(DCNSEP_EXP == 0 || DCNSEP_EXP == 1 || DCNSEP_EXP == 3 || DCNSEP_EX
 // halves) or 2 (69 KB, 256): C0 dec1 869 -> 758 us, C2 12.6 -> 11.5 ms, bit-identical (r04_dec1_occ_ab.log)
 #define DEC1_OCC 3
 #endif
-#ifndef DEC2_OCC
-#define DEC2_OCC 2         // k_dec2 workgroups per CU: 2 (k_dec2) or 3 (k_dec2o: two-pass layer 3, 52 KB LDS)
-#endif
 #ifndef DEC2_WPE
 #define DEC2_WPE 2         // waves per SIMD k_dec2 is register-budgeted for (2 workgroups/CU, 80 KB LDS each)
 #endif
