@@ -12,6 +12,7 @@ Layout:
 (integration/_ext.py at the repo root is the DCNv2 `_ext` shim over ops.dcn_v2_forward)
   parallel.py frame-pair sharding over ranks
   serving.py  option files, define_G / load_network / VideoSRModel (checkpoint drop-in)
+  train.py    Charbonnier loss, the two restart LR schedules, Adam set-up (training drop-ins)
 """
 from . import weights  # noqa: F401
 from . import coords  # noqa: F401
@@ -19,7 +20,7 @@ from . import coords  # noqa: F401
 
 def __getattr__(name):
     # torch-dependent parts load lazily so that weight/coords utilities work without torch/GPU
-    if name in ("ops", "model", "video", "parallel", "_lib", "serving"):
+    if name in ("ops", "model", "video", "parallel", "_lib", "serving", "train"):
         import importlib
         return importlib.import_module(f"{__name__}.{name}")
     if name == "LunaTokis":

@@ -28,6 +28,7 @@ Usage:  python tests/golden/make_golden.py             (model, window and per-op
         python tests/golden/make_golden.py c1          (BASELINE config C1: one full 256x256 pair, pinned pixels)
         python tests/golden/make_golden.py c2|c3|c4    (the encoder's latent of one full-size C2 / C3 / C4 pair, pinned)
         python tests/golden/make_golden.py chunk-check (the row-chunked DCN shim == the unchunked one)
+        python tests/golden/make_golden.py sched       (lr sequences of the reference's two restart schedules)
 """
 import json
 import os
@@ -563,7 +564,51 @@ def gratings_c0():
     print("gratings pair:", tuple(out.shape), float(out.min()), float(out.max()))
 
 
+def sched():
+    """lr_scheduler.py (CosineAnnealingLR_Restart, MultiStepLR_Restart) driven as VideoSRBaseModel drives them
+    (base_model.py:51-63 update_learning_rate: scheduler.step() per iteration, then the warm-up override),
+    recorded per iteration -> lr_schedules.json.  Pure torch: no shims needed."""
+    sys.path.insert(0, os.path.join(REF, "models"))
+    import lr_scheduler as LS
+    cases = {
+        # the shipped option file's shape (train_zsm.yml:57-65), periods scaled down 15,000x
+        "cosine_zsm": dict(kind="cos", lr=2e-4, T_period=[10, 10, 10, 10], restarts=[10, 20, 30],
+                           weights=[1, 1, 1], eta_min=1e-7, iters=45, warmup=-1),
+        # one period, no restarts: the schedule runs past T_max (the k = T + 1 (mod 2T) branch)
+        "cosine_wrap": dict(kind="cos", lr=1e-3, T_period=[5], restarts=None, weights=None, eta_min=1e-6,
+                            iters=23, warmup=-1),
+        # weighted restarts of different lengths, with a 3-iteration warm-up
+        "cosine_weighted": dict(kind="cos", lr=4e-4, T_period=[6, 4, 8], restarts=[6, 10], weights=[0.5, 0.25],
+                                eta_min=0, iters=24, warmup=3),
+        "multistep": dict(kind="ms", lr=2e-4, milestones=[3, 6, 6, 9, 15], restarts=[12], weights=[0.3],
+                          gamma=0.5, iters=20, warmup=-1),
+    }
+    out = {}
+    for name, c in cases.items():
+        p = torch.zeros(3, requires_grad=True)
+        opt = torch.optim.Adam([p], lr=c["lr"], weight_decay=0, betas=(0.9, 0.99))
+        if c["kind"] == "cos":
+            sch = LS.CosineAnnealingLR_Restart(opt, c["T_period"], eta_min=c["eta_min"], restarts=c["restarts"],
+                                               weights=c["weights"])
+        else:
+            sch = LS.MultiStepLR_Restart(opt, c["milestones"], restarts=c["restarts"], weights=c["weights"],
+                                         gamma=c["gamma"])
+        lrs = [opt.param_groups[0]["lr"]]
+        for it in range(1, c["iters"] + 1):
+            sch.step()
+            if it < c["warmup"]:
+                opt.param_groups[0]["lr"] = opt.param_groups[0]["initial_lr"] / c["warmup"] * it
+            lrs.append(opt.param_groups[0]["lr"])
+        out[name] = dict(case={k: v for k, v in c.items()}, lr=lrs)
+        print(name, ["%.3e" % v for v in lrs[:8]], "...")
+    with open(os.path.join(HERE, "lr_schedules.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["sched"]:
+        sched()
+        sys.exit(0)
     if sys.argv[1:] == ["gratings"]:
         gratings_c0()
         sys.exit(0)

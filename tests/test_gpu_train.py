@@ -136,3 +136,64 @@ def test_training_step_through_ext_shim_matches_oracle(sd):
         e_firm, e_all = float(d[firm].max()), float(d.max())
         assert e_firm <= 1e-6, (k, e_firm)
         assert e_all <= 2 * 2e-5 + 1e-6, (k, e_all)
+
+
+def test_training_loop_with_restart_schedule_matches_oracle(sd):
+    """Six iterations of the reference's training loop (VideoSRBaseModel: update_learning_rate -- the
+    CosineAnnealingLR_Restart schedule of train.py, base_model.py:51-63 -- then optimize_parameters,
+    VideoSR_base_model.py:113-134, Charbonnier + Adam) on the DCN_sep module through the `_ext` drop-in, vs the
+    same loop on the oracle in float64: the losses agree every iteration, the schedule's learning rates are the
+    ones the run used, and every parameter whose gradient is firm at every iteration ends where the oracle's
+    does (Adam normalises each update, so only entries whose gradient sign rounding could flip may differ, by
+    at most one lr-sized step per iteration)."""
+    import stif_pkg
+    T = stif_pkg.load().train
+    rng = np.random.default_rng(22)
+    B, H, W = 2, 10, 13
+    p = "pcd_align.L2_dcnpack_1"
+    init = {"weight": sd[p + ".weight"], "bias": sd[p + ".bias"],
+            "conv_offset_mask.weight": sd[p + ".conv_offset_mask.weight"] * 0.2,
+            "conv_offset_mask.bias": sd[p + ".conv_offset_mask.bias"]}
+    inp = rng.standard_normal((B, 64, H, W)).astype(np.float32)
+    fea = rng.standard_normal((B, 64, H, W)).astype(np.float32)
+
+    def make(backend, dt, dev):
+        net = DcnSep(make_dcn_conv(backend), dt, dev)
+        with torch.no_grad():
+            for k, v in net.named_parameters():
+                v.copy_(torch.from_numpy(np.asarray(init[k])))
+        return net
+
+    with torch.no_grad():
+        out0 = make(_OracleBackend, torch.float64, "cpu")(torch.from_numpy(inp).double(),
+                                                          torch.from_numpy(fea).double()).numpy()
+    gt = (out0 + np.where(rng.random(out0.shape) < 0.5, -1.0, 1.0) * (1.0 + rng.random(out0.shape))).astype(np.float32)
+    opts = dict(lr_G=2e-5, beta1=0.9, beta2=0.99, weight_decay_G=0, lr_scheme="CosineAnnealingLR_Restart",
+                T_period=[3, 3], restarts=[3], restart_weights=[0.5], eta_min=1e-7)
+    runs = {}
+    for name, backend, dt, dev in (("gpu", _ext(), torch.float32, "cuda"), ("oracle", _OracleBackend, torch.float64, "cpu")):
+        net = make(backend, dt, dev)
+        opt, sch = T.make_optimizer(net, opts)
+        X = [torch.from_numpy(a).to(dev, dt) for a in (inp, fea)]
+        G = torch.from_numpy(gt).to(dev, dt)
+        crit = T.CharbonnierLoss()
+        losses, lrs, grads = [], [], []
+        for it in range(1, 7):
+            T.update_learning_rate([sch], [opt], it)
+            lrs.append(opt.param_groups[0]["lr"])
+            losses.append(T.optimize_step(net, opt, crit, X, G))
+            grads.append({k: v.grad.detach().double().cpu().clone() for k, v in net.named_parameters()})
+        runs[name] = (losses, lrs, grads, {k: v.detach().double().cpu() for k, v in net.named_parameters()})
+    (lg, rg, gg, pg), (lo, ro, go, po) = runs["gpu"], runs["oracle"]
+    assert rg == ro
+    # cosine from 2e-5 over 3 steps, restart at 3 to 1e-5, then down again
+    assert abs(ro[2] - 1e-5) < 1e-18 and ro[0] < 2e-5 and ro[1] < ro[0] and ro[3] < ro[2], ro
+    for a, b in zip(lg, lo):
+        assert abs(a - b) <= 1e-5 * abs(b), (lg, lo)
+    for k in po:
+        firm = torch.ones_like(po[k], dtype=torch.bool)
+        for gi in go:
+            firm &= gi[k].abs() > 1e-3 * gi[k].abs().max()
+        d = (pg[k] - po[k]).abs()
+        assert float(d[firm].max()) <= 6e-6, (k, float(d[firm].max()))
+        assert float(d.max()) <= 6 * 2 * 2e-5 + 1e-6, (k, float(d.max()))
