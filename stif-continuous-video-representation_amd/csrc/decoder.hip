@@ -152,6 +152,36 @@ STIF_DEV void gather64(f32x16* dst, const float* __restrict__ base, int stride, 
   }
 }
 
+// gather64 with at most 8 corner loads (32 VGPRs) in flight: four memory latencies
+STIF_DEV void gather64_q(f32x16* dst, const float* __restrict__ base, int stride, int c0, const Bilin& b, int hf) {
+  const int c = c0 + 4 * hf;
+  const float* p00 = base + (size_t)b.o00 * stride + c;
+  const float* p01 = base + (size_t)b.o01 * stride + c;
+  const float* p10 = base + (size_t)b.o10 * stride + c;
+  const float* p11 = base + (size_t)b.o11 * stride + c;
+#pragma unroll
+  for (int qr = 0; qr < 4; ++qr) {
+    f32x4 cr[2][4];
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const int o = 8 * (2 * qr + g);
+      cr[g][0] = ld4(p00 + o);
+      cr[g][1] = ld4(p01 + o);
+      cr[g][2] = ld4(p10 + o);
+      cr[g][3] = ld4(p11 + o);
+    }
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      f32x4 s = b.w00 * cr[g][0] + b.w01 * cr[g][1] + b.w10 * cr[g][2] + b.w11 * cr[g][3];
+      asm volatile("" : "+v"(s));
+      const int gg = 2 * qr + g;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dst[gg >> 2][4 * (gg & 3) + e] = s[e];
+    }
+    asm volatile("" ::: "memory");
+  }
+}
+
 // gather64 with at most 16 corner loads (64 VGPRs) in flight: two memory latencies instead of one, for
 // kernels budgeted below the 128 VGPRs of the one-shot form
 STIF_DEV void gather64_h(f32x16* dst, const float* __restrict__ base, int stride, int c0, const Bilin& b, int hf) {
@@ -281,16 +311,21 @@ STIF_DEV void narrow_dot(float* o, const float* W, int kt, const f32x16& x, int 
 // (local ensemble).  HRIMG: the flow stage's image input comes from the high-resolution image.
 // DEC1_OCC = 3 (MODE 0 / 1): 6-tile segments (52 KB of LDS) and a 168-register budget, so three workgroups
 // (three waves per SIMD) share a CU; flow layer 1's second output tile then arrives after the last feat step
+// DEC1_OCC = 4: 4-tile segments (36 KB) and 128 registers; flow layer 1 then arrives after the last feat
+// step and flow segment 0 after flow layer 0
 template <int MODE>
-constexpr int S1 = (DEC1_OCC == 3 && MODE != 2) ? 6 : SEG1;
+constexpr int OCC1 = MODE != 2 ? DEC1_OCC : 2;
+template <int MODE>
+constexpr int S1 = OCC1<MODE> == 4 ? 4 : OCC1<MODE> == 3 ? 6 : SEG1;
 template <int MODE, bool HRIMG, int F16>
-__global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(MODE != 2 ? DEC1_OCC : 2))) void k_dec1(const float* __restrict__ proj, const float* __restrict__ mlp,
+__global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(OCC1<MODE>))) void k_dec1(const float* __restrict__ proj, const float* __restrict__ mlp,
                                                      stif_dec_tables tb, stif_dec_image im,
                                                      const float* __restrict__ tq, float* __restrict__ hrfeat,
                                                      float* __restrict__ flow, int n, int h, int w, int HH,
                                                      int WW) {
   // two segment buffers of SEG1 tiles + the flow's last layer (plain [4][256], resident)
-  constexpr bool OCC3 = S1<MODE> != SEG1;
+  constexpr bool OCC3 = S1<MODE> != SEG1;             // 3 or 4 workgroups per CU
+  constexpr bool OCC4 = OCC1<MODE> == 4;
   __shared__ __attribute__((aligned(16))) float wbuf[2 * S1<MODE> * T + T];
   const int lane = threadIdx.x & 63, hf = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
@@ -368,7 +403,7 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(MOD
     if (!last) seg_feat23(nxt, kt + 1);
     else {   // prefetch flow layer 0 (4 tiles) + layer 1 (4 tiles; OCC3: its first output tile)
       dma_tiles<DEC_NW>(nxt, rm, L_W0, 4, wv, lane);
-      dma_tiles<DEC_NW>(nxt + 4 * T, rm, L_W1, OCC3 ? 2 : 4, wv, lane);
+      if (!OCC4) dma_tiles<DEC_NW>(nxt + 4 * T, rm, L_W1, OCC3 ? 2 : 4, wv, lane);
     }
     f32x16 acc = f32x16{0};
     tile_mma<F16>(acc, cur, x1s[0], lane);
@@ -414,7 +449,8 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(MOD
     const float wy0 = tb.wy0[py], wy1 = tb.wy1[py], wx0 = tb.wx0[px], wx1 = tb.wx1[px];
     b.o00 = y0 * w + x0_; b.o01 = y0 * w + x1_; b.o10 = y1 * w + x0_; b.o11 = y1 * w + x1_;
     b.w00 = wx0 * wy0; b.w01 = wx1 * wy0; b.w10 = wx0 * wy1; b.w11 = wx1 * wy1;
-    if (OCC3) gather64_h(z, P, PROJ_C, 64, b, hf);
+    if (OCC4) gather64_q(z, P, PROJ_C, 64, b, hf);
+    else if (OCC3) gather64_h(z, P, PROJ_C, 64, b, hf);
     else gather64(z, P, PROJ_C, 64, b, hf);
 #pragma unroll
     for (int ot = 0; ot < 2; ++ot)
@@ -442,9 +478,12 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(MOD
     dma_tiles<DEC_NW>(dst, rm, L_W2 + kt * 2 * T, 2, wv, lane);
   };
   // OCC3: layer 1's second output tile (2 tiles) into B0, segment 0 after it
-  constexpr bool L1B0 = OCC3 && MODE == 0;
-  if (L1B0) dma_tiles<DEC_NW>(B0, rm, L_W1 + 2 * T, 2, wv, lane);
-  seg_flow23(B0 + (L1B0 ? 2 * T : 0), 0);
+  constexpr bool L1B0 = OCC3 && !OCC4 && MODE == 0;
+  if (OCC4) dma_tiles<DEC_NW>(B0, rm, L_W1, 4, wv, lane);   // all of layer 1 into B0; segment 0 later
+  else {
+    if (L1B0) dma_tiles<DEC_NW>(B0, rm, L_W1 + 2 * T, 2, wv, lane);
+    seg_flow23(B0 + (L1B0 ? 2 * T : 0), 0);
+  }
   {
     const XT<F16> hs[2] = {xop<F16>(hr[0]), xop<F16>(hr[1])};
 #pragma unroll
@@ -455,13 +494,14 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(MOD
       for (int r = 0; r < 16; ++r) z[ot][r] = siren_sin<F16>(z[ot][r] * ACC_S<F16>);
     }
   }
-  if (L1B0) lds_dma_barrier();   // layer 1's second output tile landed in B0
+  if (L1B0 || OCC4) lds_dma_barrier();   // layer 1 (OCC3: its second output tile) landed in B0
+  if (OCC4) seg_flow23(B1, 0);             // every wave is done with layer 0's B1
   {
     const XT<F16> zs[2] = {xop<F16>(z[0]), xop<F16>(z[1])};
 #pragma unroll
     for (int ot = 0; ot < 2; ++ot) {
       f32x16 acc = f32x16{0};
-      const float* w1t = (L1B0 && ot == 1) ? B0 : B1 + (4 + ot * 2) * T;
+      const float* w1t = OCC4 ? B0 + ot * 2 * T : (L1B0 && ot == 1) ? B0 : B1 + (4 + ot * 2) * T;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) tile_mma<F16>(acc, w1t + kt * T, zs[kt], lane);
       x1[ot] = bias_sin<F16>(acc, lb1[ot]);
@@ -473,8 +513,9 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(MOD
     lds_dma_barrier();
     const Bias32 b2 = bias_ld(mlp + L_B2 + kt * 32, hf);   // before the DMA (see feat_step)
     __builtin_amdgcn_sched_barrier(0);
-    float* cur = (kt & 1) ? B1 : (L1B0 && kt == 0 ? B0 + 2 * T : B0);
-    float* nxt = (kt & 1) ? B0 : B1;
+    // OCC4: segment 0 sits in B1, so the buffers alternate the other way round
+    float* cur = OCC4 ? ((kt & 1) ? B0 : B1) : (kt & 1) ? B1 : (L1B0 && kt == 0 ? B0 + 2 * T : B0);
+    float* nxt = OCC4 ? ((kt & 1) ? B1 : B0) : (kt & 1) ? B0 : B1;
     if (!last) seg_flow23(nxt, kt + 1);
     f32x16 acc = f32x16{0};
     tile_mma<F16>(acc, cur, x1f[0], lane);
