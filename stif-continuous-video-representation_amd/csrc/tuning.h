@@ -55,9 +55,10 @@ static_assert(DCNSEP_EXP == 0 || DCNSEP_EXP == 1 || DCNSEP_EXP == 3 || DCNSEP_EX
 #define DEC1_NW 4
 #endif
 #ifndef DEC1_OCC
-// k_dec1 (MODE 0 / 1) workgroups per CU: 3 (52 KB LDS, 168 registers, the flow projection gathered in two
-// halves) or 2 (69 KB, 256): C0 dec1 869 -> 758 us, C2 12.6 -> 11.5 ms, bit-identical (r04_dec1_occ_ab.log)
-#define DEC1_OCC 3
+// k_dec1 (MODE 0 / 1) workgroups per CU: 4 (36 KB LDS, 128 registers, the flow projection gathered in four
+// 8-load quarters), 3 (52 KB, 168, halves) or 2 (69 KB, 256).  C0 dec1 869 -> 758 us (2 -> 3,
+// r04_dec1_occ_ab.log) -> 720 us (3 -> 4; C2 11.6 -> 11.1 ms, r04_dec1_occ4_ab.log); all bit-identical
+#define DEC1_OCC 4
 #endif
 #ifndef DEC2_WPE
 #define DEC2_WPE 2         // waves per SIMD k_dec2 is register-budgeted for (2 workgroups/CU, 80 KB LDS each)
