@@ -313,25 +313,26 @@ STIF_DEV void narrow_dot(float* o, const float* W, int kt, const f32x16& x, int 
 // (three waves per SIMD) share a CU; flow layer 1's second output tile then arrives after the last feat step
 // DEC1_OCC = 4: 4-tile segments (36 KB) and 128 registers; flow layer 1 then arrives after the last feat
 // step and flow segment 0 after flow layer 0
-template <int MODE>
-constexpr int OCC1 = MODE != 2 ? DEC1_OCC : 2;
-template <int MODE>
-constexpr int S1 = OCC1<MODE> == 4 ? 4 : OCC1<MODE> == 3 ? 6 : SEG1;
+// (the HRIMG variants, decoding_test's, stay at 3: at 128 registers their image gather spills)
+template <int MODE, bool HRIMG>
+constexpr int OCC1 = MODE == 2 ? 2 : (HRIMG && DEC1_OCC > 3) ? 3 : DEC1_OCC;
+template <int MODE, bool HRIMG>
+constexpr int S1 = OCC1<MODE, HRIMG> == 4 ? 4 : OCC1<MODE, HRIMG> == 3 ? 6 : SEG1;
 template <int MODE, bool HRIMG, int F16>
-__global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(OCC1<MODE>))) void k_dec1(const float* __restrict__ proj, const float* __restrict__ mlp,
+__global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(OCC1<MODE, HRIMG>))) void k_dec1(const float* __restrict__ proj, const float* __restrict__ mlp,
                                                      stif_dec_tables tb, stif_dec_image im,
                                                      const float* __restrict__ tq, float* __restrict__ hrfeat,
                                                      float* __restrict__ flow, int n, int h, int w, int HH,
                                                      int WW) {
   // two segment buffers of SEG1 tiles + the flow's last layer (plain [4][256], resident)
-  constexpr bool OCC3 = S1<MODE> != SEG1;             // 3 or 4 workgroups per CU
-  constexpr bool OCC4 = OCC1<MODE> == 4;
-  __shared__ __attribute__((aligned(16))) float wbuf[2 * S1<MODE> * T + T];
+  constexpr bool OCC3 = S1<MODE, HRIMG> != SEG1;             // 3 or 4 workgroups per CU
+  constexpr bool OCC4 = OCC1<MODE, HRIMG> == 4;
+  __shared__ __attribute__((aligned(16))) float wbuf[2 * S1<MODE, HRIMG> * T + T];
   const int lane = threadIdx.x & 63, hf = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
   float* const B0 = wbuf;
-  float* const B1 = wbuf + S1<MODE> * T;
-  float* const W3V = wbuf + 2 * S1<MODE> * T;
+  float* const B1 = wbuf + S1<MODE, HRIMG> * T;
+  float* const W3V = wbuf + 2 * S1<MODE, HRIMG> * T;
   const __amdgpu_buffer_rsrc_t rm = mlp_rsrc(mlp);
   if (MODE != 1) dma_tiles<DEC_NW>(W3V, rm, L_W3V, 1, wv, lane);
   // segment 0: feat layer 1 (4 tiles); segments 1..8: feat layer 2 tile kt + layer 3 (0, kt), (1, kt)
