@@ -16,7 +16,9 @@ print(f"last step: {len(step)} dispatches, span {(t1 - t0) / 1e6:.3f} ms, kernel
 small = defaultdict(lambda: [0, 0.0])
 allk = defaultdict(lambda: [0, 0.0])
 for r in step:
-    wg = int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"]))
+    wg = 1
+    for d in "XYZ":
+        wg *= int(r[f"Grid_Size_{d}"]) // max(1, int(r[f"Workgroup_Size_{d}"]))
     d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
     name = r["Kernel_Name"].split("(stif")[0].split("(float")[0].replace("void ", "").replace("(anonymous namespace)::", "")[:48]
     allk[name][0] += 1
