@@ -141,19 +141,11 @@ typedef struct {
   long long fea_item, in_item, out_item;
   int ngroups, nitems, H, W;
   int epi;                              /* STIF_EPI_NONE or STIF_EPI_LRELU */
-  int flags;                            /* STIF_CONV_F16X3 (required) | STIF_DCNSEP_P16 */
+  int flags;                            /* STIF_CONV_F16X3 (required) */
   int* status;                          /* optional device word, as stif_conv_args.status */
 } stif_dcn_sep_args;
 
-/* stif_dcn_sep_args.flags: w_om / b_om packed STIF_PACK_DCNSEP16 and w STIF_PACK_DCNPAIR16 (both |
- * STIF_PACK_F16X3): the 16-pixels-per-wave kernel (8 waves per 4 x 32 tile, v_mfma_f32_16x16x32_f16,
- * four waves per SIMD); without it the STIF_PACK_DCNSEP / DCNPAIR layouts of the 32-pixel kernel. */
-#define STIF_DCNSEP_P16 2
-
 int stif_dcn_sep_nhwc(const stif_dcn_sep_args* args, void* stream);
-/* The stif_dcn_sep_args.flags layout bit (0 or STIF_DCNSEP_P16) of the kernel this build runs by default:
- * callers pack with the matching modes and pass it in flags. */
-int stif_dcn_sep_layout(void);
 
 /* Drop-in for `_ext.dcn_v2_forward` (dcn_v2.h:9-23): NCHW fp32 input [b,c,h,w],
  * weight [co,c,kh,kw], bias [co], offset [b, dg*2*kh*kw, ho, wo],
@@ -274,8 +266,7 @@ int stif_frames_to_u8(const float* nchw, unsigned char* hwc, int n, int H, int W
 
 /* ---- host-side weight packing (pure CPU, callable without a GPU) ---- */
 enum { STIF_PACK_PLAIN = 0, STIF_PACK_OFFMASK = 1, STIF_PACK_LSTM = 2, STIF_PACK_WINO = 3, STIF_PACK_WINO_OFFMASK = 4,
-       STIF_PACK_WINO_LSTM = 5, STIF_PACK_DCNSEP = 6, STIF_PACK_DCNPAIR = 7, STIF_PACK_DCNSEP16 = 8,
-       STIF_PACK_DCNPAIR16 = 9 };
+       STIF_PACK_WINO_LSTM = 5, STIF_PACK_DCNSEP = 6, STIF_PACK_DCNPAIR = 7 };
 /* OR'ed into a STIF_PACK_WINO* mode: the f16x3 split packing for stif_conv3x3_wino with
  * flags = STIF_CONV_F16X3 (same size in bytes) */
 #define STIF_PACK_F16X3 16
@@ -310,19 +301,7 @@ size_t stif_conv_bias_floats(int cout, int mode);
  * (s % 27) / 3 of group 2 (s / 27) + h (slots 108..111 zero).  Bias: [8][32] in the same row order.
  * STIF_PACK_DCNPAIR | STIF_PACK_F16X3 (the 64 -> 64 3x3 DCN weight of stif_dcn_sep_nhwc): [group pair
  * a 4][tap 9][nt 2][plane h|l][lane 64][8 halves], element e of lane l holding input channel
- * 8 (2 a + (l >> 5)) + e, cout nt * 32 + (l & 31).
- * STIF_PACK_DCNSEP16 | STIF_PACK_F16X3 (conv_offset_mask for stif_dcn_sep_nhwc with STIF_DCNSEP_P16): the
- * 16x16x32 A operands [step s 18][M-tile m 14][plane h|l][lane 64][8 halves] of W * 2^10, lane l holding
- * row R = 16 m + (l & 15) and, with q = l >> 4, input channel 16 c + 8 (q & 1) + e of tap t, where
- * (c, t) = unit u = 2 s + (q >> 1) as u = 9 c + t.  Row R is accumulator element R & 3 of the lanes
- * q = (R >> 2) & 3, slot v = 4 (R >> 4) + (R & 3) < 54: component v % 3 (dy, dx, mask) of sampling
- * position v / 3 of lane group q -- position 4 a + j (j < 4) is tap 2 j + (q >> 1) of group 2 a + (q & 1),
- * position 16 + b is tap 8 of group 2 a + (q & 1) with a = 2 b + 1 - (q >> 1) (slots 54, 55 zero).
- * Bias: [224] (of 256) in row order.
- * STIF_PACK_DCNPAIR16 | STIF_PACK_F16X3 (the DCN weight for STIF_DCNSEP_P16): [group pair a 4][step j 5]
- * [M-tile 4][plane h|l][lane 64][8 halves], lane l holding cout 16 M-tile + (l & 15) and, with
- * q = l >> 4, input channel 8 (2 a + (q & 1)) + e at tap 2 j + (q >> 1) (j < 4) or tap 8 (j = 4: zero
- * unless q >> 1 = 1 - (a & 1)). */
+ * 8 (2 a + (l >> 5)) + e, cout nt * 32 + (l & 31). */
 int stif_pack_conv_weight(const float* w_oihw, const float* b, int cout, int cin, int ks, int mode,
                           float* w_dst, float* b_dst);
 

@@ -13,11 +13,9 @@ LIB_PATH = os.environ.get("STIF_HIP_LIB") or os.path.join(os.path.dirname(os.pat
 
 MAXG = 8
 EPI_NONE, EPI_LRELU, EPI_RELU, EPI_RES, EPI_OFFMASK, EPI_LSTM = range(6)
-(PACK_PLAIN, PACK_OFFMASK, PACK_LSTM, PACK_WINO, PACK_WINO_OFFMASK, PACK_WINO_LSTM, PACK_DCNSEP, PACK_DCNPAIR,
- PACK_DCNSEP16, PACK_DCNPAIR16) = range(10)
+PACK_PLAIN, PACK_OFFMASK, PACK_LSTM, PACK_WINO, PACK_WINO_OFFMASK, PACK_WINO_LSTM, PACK_DCNSEP, PACK_DCNPAIR = range(8)
 PACK_F16X3 = 16          # OR'ed into a PACK_WINO* mode (stif.h STIF_PACK_F16X3)
 CONV_F16X3 = 1           # stif_conv_args.flags
-DCNSEP_P16 = 2           # stif_dcn_sep_args.flags: the 16-pixel fused DCN_sep layout (stif.h STIF_DCNSEP_P16)
 DEC_REVOLUTIONS = 2      # stif_pack_dec_proj_ex lr_image bit (stif.h STIF_DEC_REVOLUTIONS)
 
 _P = C.c_void_p
@@ -74,7 +72,6 @@ EXPORTS = {
     "stif_conv_first": (C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, C.c_int, _P]),
     "stif_dcn_nhwc": (C.c_int, [C.POINTER(DcnArgs), _P]),
     "stif_dcn_sep_nhwc": (C.c_int, [C.POINTER(DcnSepArgs), _P]),
-    "stif_dcn_sep_layout": (C.c_int, []),
     "stif_dcn_v2_workspace_size": (C.c_size_t, [C.c_int] * 14),
     "stif_dcn_v2_forward": (C.c_int, [_P] * 6 + [C.c_int] * 14 + [_P, C.c_size_t, _P]),
     "stif_dcn_v2_backward_workspace_size": (C.c_size_t, [C.c_int] * 14),

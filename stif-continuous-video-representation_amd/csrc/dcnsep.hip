@@ -391,286 +391,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_
   report_range(a.status, not_finite(chk2));
 }
 
-
-// ---------------------------------------------------------------------------------------------
-// k_dcn_sep16: the same fused DCN_sep with 16 pixels per wave, on v_mfma_f32_16x16x32_f16.  A wave's
-// state halves (offset/mask accumulators 112 -> 56 VGPRs, DCN accumulators 32 -> 16), so the 4 x 32 tile
-// takes 8 waves (wave w: output row w >> 1, columns 16 (w & 1) .. + 15) and two 80-KB workgroups per CU
-// run FOUR waves per SIMD (k_dcn_sep: two) -- the waves sharing a SIMD come from two workgroups in
-// different phases more of the time.  Lane l = (p = l & 15, lane group q = l >> 4).
-//
-// Phase 1: K steps of 32 = two (16-channel chunk, tap) units 2 s, 2 s + 1 (lane group q supplies unit
-// 2 s + (q >> 1), channels 8 (q & 1) .. + 7), 14 M-tiles of 16 offset/mask rows, each step split in two
-// half-steps of 7 M-tiles (a 3-slot ring of 14-KB weight stages, one barrier per half-step) -- the same
-// LDS map and halo image as k_dcn_sep.  Lane p works on pixel column pi16(p) of its 16: even pixels on
-// lanes 0-3 / 12-15, odd on 4-11, which makes both 16-lane ds_read_b128 groups of the 80-B-pitch halo
-// image conflict-free (5 pi16(p) + 2 (q & 1) covers all 16 bank quads).
-//
-// Phase 2: per group pair five K steps of 32: lane group q samples tap 2 j + (q >> 1) (step j < 4) or tap
-// 8 (step 4: real for q >> 1 = 1 - (pair & 1), zero weights and a zeroed sample otherwise) of group
-// 2 pair + (q & 1) -- 20 steps x 12 MFMAs instead of 18 (+11 % phase-2 MFMAs, 2.5 % of the kernel's).
-// The offsets come from accumulator slot v = 3 position + component (STIF_PACK_DCNSEP16, stif.h).
-// Epilogue: lane (p, q) holds couts 16 mt + 4 q .. + 3 of its pixel: direct 16-B stores.
-namespace p16 {
-constexpr int NW16 = 8;
-constexpr int MT16 = 14;
-constexpr int HC = TW + 2;                   // halo columns (6 halo rows)
-constexpr int D_SLOTS16 = 6 * HC * 5;
-constexpr int D_INS16 = 16;
-constexpr int WK_F16 = 7 * 2 * 256;          // one half-step's packed weights
-constexpr int TR16 = 4 + 2 + 2 * M, TC16 = TW + 2 + 2 * M, TP16 = TC16;
-constexpr int T_EL16 = TR16 * 4 * TP16;
-constexpr int T_INST16 = (T_EL16 + 63) / 64;  // 24
-constexpr int WP_F16 = 5 * 4 * 2 * 256;       // one pair's phase-2 A fragments (40 KB)
-constexpr int P_INS16 = T_INST16 + WP_F16 / 256;
-constexpr int O16_D0 = 0, O16_D1 = D_INS16 * 256, O16_W = 2 * D_INS16 * 256;
-constexpr int O16_XT = 0, O16_XW = T_INST16 * 256;
-constexpr int LDS_F16 = O16_W + 3 * 4096;
-static_assert(D_SLOTS16 <= D_INS16 * 64 && P_INS16 % NW16 == 0 && O16_XW + WP_F16 <= LDS_F16 && LDS_F16 * 4 <= 80 * 1024,
-              "k_dcn_sep16 LDS map");
-// DMA instructions a wave issues in half-step h: the weights of h + 2, data chunks 1 / 2 / 3 at h = 1 / 8 / 16
-constexpr int dma_at(int h) { return (h + 2 < 36 ? 2 : 0) + ((h == 1 || h == 8 || h == 16) ? 2 : 0); }
-}  // namespace p16
-
-STIF_DEV int pi16(int p) { return p < 4 ? 2 * p : (p < 12 ? 2 * p - 7 : 2 * p - 16); }
-STIF_DEV f32x4 mfma16x16h(f16x8 a, f16x8 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
-}
-
-template <int EPI>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_dcn_sep16(stif_dcn_sep_args a) {
-  using namespace p16;
-  __shared__ __attribute__((aligned(16))) float smem[LDS_F16];
-  const int tid = threadIdx.x, lane = tid & 63, p = lane & 15, q = lane >> 4, qu = q >> 1, qg = q & 1;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int H = a.H, W = a.W;
-  const int tiles_x = (W + TW - 1) / TW, tiles = tiles_x * ((H + 3) / 4);
-  const int L = xcd_block(blockIdx.x, gridDim.x);
-  const int z = L / tiles, tl = L - z * tiles;
-  const int tx = tl % tiles_x, ty = tl / tiles_x;
-  const int g = z / a.nitems, n = z - g * a.nitems;
-  const float* fea = a.fea[g] + (size_t)n * a.fea_item;
-  const float* in = a.in[g] + (size_t)n * a.in_item;
-  const float* wt = a.w[g];
-  const int oy0 = ty * 4, ox0 = tx * TW;
-  const int rw = wv >> 1, colw = 16 * (wv & 1) + pi16(p);
-  const int oy = oy0 + rw, ox = ox0 + colw;
-  const bool pix_ok = oy < H && ox < W;
-  const unsigned img_bytes = (unsigned)((size_t)H * W * 64 * 4);
-  const __amdgpu_buffer_rsrc_t rfea = __builtin_amdgcn_make_buffer_rsrc((void*)fea, (short)0, (int)img_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc((void*)in, (short)0, (int)img_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rwom =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.w_om[g], (short)0, 36 * WK_F16 * 4, 0x00020000);
-
-  // data chunk c (channels 16 c .. + 15) of the 6 x 34 halo: k_dcn_sep's image (pixel * 5 + sub, sub 4 pad)
-  auto stage_data = [&](int c, float* dst) {
-#pragma unroll
-    for (int j = 0; j < D_INS16 / NW16; ++j) {
-      const int i = wv + j * NW16;
-      const int s = i * 64 + lane;
-      const int px = s / 5, sub = s - 5 * px;
-      const int row = px / HC, col = px - HC * row;
-      const int y = oy0 - 1 + row, x = ox0 - 1 + col;
-      const bool ok = (s < D_SLOTS16) & (sub < 4) & ((unsigned)y < (unsigned)H) & ((unsigned)x < (unsigned)W);
-      const unsigned voff = ok ? (unsigned)((((size_t)y * W + x) * 64 + 4 * sub) * 4) : 0x80000000u;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rfea, dst + i * 256, 16, voff, 64 * c, 0, 0);
-    }
-  };
-  // the lane's byte offset in the VGPR operand, the stage's in the scalar one (no per-stage address VGPRs)
-  const unsigned lane16 = (unsigned)lane * 16u;
-  auto stage_w = [&](int h, int slot) {
-    float* dst = smem + O16_W + slot * 4096;
-#pragma unroll
-    for (int j = 0; j < 16 / NW16; ++j) {
-      const int i = wv + j * NW16;   // wave-uniform
-      const unsigned voff = i < 14 ? lane16 : 0x80000000u;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rwom, dst + i * 256, 16, voff, (h * WK_F16 + i * 256) * 4, 0, 0);
-    }
-  };
-  const int ty0 = oy0 - 1 - M, tx0 = ox0 - 1 - M;
-  auto stage_pair = [&](int pa) {
-    const float* wc = wt + (size_t)pa * WP_F16;
-    float* st = smem + O16_XT;
-    float* sw = smem + O16_XW;
-#pragma unroll 1
-    for (int j = 0; j < P_INS16 / NW16; ++j) {
-      const int i = wv + j * NW16;   // wave-uniform
-      if (i >= T_INST16) {
-        __builtin_amdgcn_global_load_lds(wc + ((i - T_INST16) * 64 + lane) * 4, sw + (i - T_INST16) * 256, 16, 0, 0);
-      } else {
-        const int e = i * 64 + lane;
-        const int col = e % TP16, rq = e / TP16, qd = rq & 3, row = rq >> 2;
-        const int y = ty0 + row, x = tx0 + col;
-        const bool ok = (e < T_EL16) & ((unsigned)y < (unsigned)H) & ((unsigned)x < (unsigned)W);
-        const unsigned voff = ok ? (unsigned)((((size_t)y * W + x) * 64 + pa * 16 + qd * 4) * 4) : 0x80000000u;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, st + i * 256, 16, voff, 0, 0, 0);
-      }
-    }
-  };
-
-  // ---------------------------------------------------------------- phase 1
-  f32x4 om[MT16];
-#pragma unroll
-  for (int m = 0; m < MT16; ++m) om[m] = ld4(a.b_om[g] + 16 * m + 4 * q) * (1.0f / F16X3_UNSCALE);
-  stage_data(0, smem + O16_D0);
-  stage_w(0, 0);
-  stage_w(1, 1);
-  // this lane's B operand of step s: unit 2 s + qu -> (chunk c, tap t), buffer c & 1
-  const float* dbase = smem + (rw * HC + colw) * PX_F + 8 * qg;
-  auto dptr = [&](int s) {   // offA folds into the ds_read offset: one multiply-add per step
-    const int uA = 2 * s, uB = 2 * s + 1;
-    const int tA = uA % 9, tB = uB % 9;
-    const int offA = ((uA / 9) & 1 ? O16_D1 : O16_D0) + ((tA / 3) * HC + tA % 3) * PX_F;
-    const int offB = ((uB / 9) & 1 ? O16_D1 : O16_D0) + ((tB / 3) * HC + tB % 3) * PX_F;
-    return dbase + qu * (offB - offA) + offA;
-  };
-  f16x8 dh, dl;
-  f32x4 x0, x1;
-#pragma unroll
-  for (int h = 0; h < 36; ++h) {
-    const int s = h >> 1, hh = h & 1;
-    wait_vm(h == 0 ? 2 : dma_at(h - 1));
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    const float* wb = smem + O16_W + (h % 3) * 4096 + lane * 4;
-    f16x8 wh[2], wl[2];
-    wh[0] = ldh8(wb);
-    wl[0] = ldh8(wb + 256);
-    if (h == 0) {
-      const float* d = dptr(0);
-      split_f16x3(ld4(d), ld4(d + 4), dh, dl);
-    }
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {
-      if (k + 1 < 7) {
-        wh[(k + 1) & 1] = ldh8(wb + (2 * k + 2) * 256);
-        wl[(k + 1) & 1] = ldh8(wb + (2 * k + 3) * 256);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      const int m = 7 * hh + k;
-      om[m] = mfma16x16h(wh[k & 1], dh, om[m]);
-      om[m] = mfma16x16h(wh[k & 1], dl, om[m]);
-      om[m] = mfma16x16h(wl[k & 1], dh, om[m]);
-      if (k == 0) {
-        if (h + 2 < 36) stage_w(h + 2, (h + 2) % 3);
-        if (h == 1) stage_data(1, smem + O16_D1);
-        if (h == 8) stage_data(2, smem + O16_D0);
-        if (h == 16) stage_data(3, smem + O16_D1);
-      }
-      if (k == 1 && hh == 1 && s < 17) {
-        const float* d = dptr(s + 1);
-        x0 = ld4(d);
-        x1 = ld4(d + 4);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (hh == 1 && s < 17) split_f16x3(x0, x1, dh, dl);
-  }
-  // slot v = 4 m + i: unscale, sigmoid(mask) (component v % 3 == 2), range sum over the 54 used slots
-  float chk = 0.f;
-#pragma unroll
-  for (int m = 0; m < MT16; ++m) {   // whole-vector accesses of om (element stores kept it in scratch)
-    f32x4 x = om[m] * F16X3_UNSCALE;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int v = 4 * m + i;
-      if (v < 54) {
-        chk += x[i];
-        if (v % 3 == 2) x[i] = sigmoid_fast(x[i]);
-      }
-    }
-    om[m] = x;
-  }
-  report_range(a.status, not_finite(chk));
-
-  // ---------------------------------------------------------------- phase 2
-  auto sample = [&](const float* st, int pa, int ky, int kx, float dy, float dx, float mk, f32x4& a0, f32x4& a1) {
-    const float h_im = (float)(oy - 1 + ky) + dy;
-    const float w_im = (float)(ox - 1 + kx) + dx;
-    const bool valid = pix_ok & (h_im > -1.f) & (w_im > -1.f) & (h_im < (float)H) & (w_im < (float)W);
-    const float fh = floorf(h_im), fw = floorf(w_im);
-    const float lh = h_im - fh, lw = w_im - fw, hh = 1.f - lh, hw = 1.f - lw;
-    const int h_low = (int)fh, w_low = (int)fw;
-    const int r0 = h_low - ty0, c0 = w_low - tx0;
-    const bool in_tile = ((unsigned)r0 < (unsigned)(TR16 - 1)) & ((unsigned)c0 < (unsigned)(TC16 - 1));
-    const float m = valid ? mk : 0.f;
-    const float hm = hh * m, lm = lh * m;
-    const float w1 = hm * hw, w2 = hm * lw, w3 = lm * hw, w4 = lm * lw;
-    const float* p0 = st + (((in_tile ? r0 : 0) * 4 + 2 * qg) * TP16 + (in_tile ? c0 : 0)) * 4;
-    const float* p1 = p0 + 4 * TP16 * 4;
-    a0 = w1 * ld4(p0) + w2 * ld4(p0 + 4) + w3 * ld4(p1) + w4 * ld4(p1 + 4);
-    a1 = w1 * ld4(p0 + TP16 * 4) + w2 * ld4(p0 + TP16 * 4 + 4) + w3 * ld4(p1 + TP16 * 4) + w4 * ld4(p1 + TP16 * 4 + 4);
-    const bool fb = valid & !in_tile;
-    if (__builtin_amdgcn_ballot_w64(fb)) {
-      if (fb) {
-        // buffer loads on 32-bit offsets (an out-of-map corner reads the out-of-range offset: zero)
-        const int h_high = h_low + 1, w_high = w_low + 1;
-        const unsigned cb = (unsigned)(pa * 16 + qg * 8) * 4u;
-        auto ldc = [&](bool ok, int y, int x, int o) {
-          const unsigned vo = ok ? (unsigned)(y * W + x) * 256u + cb + 16u * o : 0x80000000u;
-          return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rin, vo, 0, 0));
-        };
-        const bool b1 = h_low >= 0 && w_low >= 0, b2 = h_low >= 0 && w_high <= W - 1;
-        const bool b3 = h_high <= H - 1 && w_low >= 0, b4 = h_high <= H - 1 && w_high <= W - 1;
-        a0 = w1 * ldc(b1, h_low, w_low, 0) + w2 * ldc(b2, h_low, w_high, 0) + w3 * ldc(b3, h_high, w_low, 0) +
-             w4 * ldc(b4, h_high, w_high, 0);
-        a1 = w1 * ldc(b1, h_low, w_low, 1) + w2 * ldc(b2, h_low, w_high, 1) + w3 * ldc(b3, h_high, w_low, 1) +
-             w4 * ldc(b4, h_high, w_high, 1);
-      }
-    }
-  };
-  f32x4 acc[4];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) acc[mt] = ld4(a.bias[g] + 16 * mt + 4 * q) * (1.0f / F16X3_UNSCALE);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();   // phase-1 buffers free
-  const float* st = smem + O16_XT;
-  const float* sw = smem + O16_XW;
-#pragma unroll
-  for (int pa = 0; pa < 4; ++pa) {
-    if (pa) __syncthreads();   // every wave is done with the previous pair's buffer
-    stage_pair(pa);
-    lds_dma_barrier();
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      const int pos = j < 4 ? 4 * pa + j : 16 + (pa >> 1), v = 3 * pos;
-      // tap 2 j + qu (j < 4) or 8
-      const int tA = j < 4 ? 2 * j : 8, tB = j < 4 ? 2 * j + 1 : 8;
-      const int ky = qu ? tB / 3 : tA / 3, kx = qu ? tB % 3 : tA % 3;
-      f32x4 a0, a1;
-      sample(st, pa, ky, kx, om[v >> 2][v & 3], om[(v + 1) >> 2][(v + 1) & 3], om[(v + 2) >> 2][(v + 2) & 3], a0, a1);
-      if (j == 4 && qu == (pa & 1)) {   // this lane group's step 4 belongs to the other pair: zero weights, zero sample
-        a0 = f32x4{0.f, 0.f, 0.f, 0.f};
-        a1 = a0;
-      }
-      f16x8 ah, al;
-      split_f16x3(a0, a1, ah, al);
-      const float* wp = sw + (j * 4) * 512 + lane * 4;   // [step][M-tile][plane][lane][8 halves]
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        const f16x8 bh = ldh8(wp + mt * 512), bl = ldh8(wp + mt * 512 + 256);
-        acc[mt] = mfma16x16h(bh, ah, acc[mt]);
-        acc[mt] = mfma16x16h(bh, al, acc[mt]);
-        acc[mt] = mfma16x16h(bl, ah, acc[mt]);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  // epilogue: couts 16 mt + 4 q .. + 3 of this lane's pixel, straight from the accumulators
-  float* out = a.out[g] + (size_t)n * a.out_item;
-  float chk2 = 0.f;
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
-    f32x4 y = acc[mt] * F16X3_UNSCALE;
-    chk2 += (y[0] + y[1]) + (y[2] + y[3]);
-    if (EPI == STIF_EPI_LRELU)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) y[e] = lrelu01(y[e]);
-    if (pix_ok) st4(out + ((size_t)oy * W + ox) * 64 + 16 * mt + 4 * q, y);
-  }
-  report_range(a.status, pix_ok & not_finite(chk2));
-}
 }  // namespace
 
 extern "C" int stif_dcn_sep_nhwc(const stif_dcn_sep_args* pa, void* stream) {
@@ -685,19 +405,9 @@ extern "C" int stif_dcn_sep_nhwc(const stif_dcn_sep_args* pa, void* stream) {
   for (int i = 0; i < a.ngroups; ++i)
     if (!a.fea[i] || !a.in[i] || !a.w_om[i] || !a.b_om[i] || !a.w[i] || !a.bias[i] || !a.out[i])
       return stif_fail(STIF_E_INVALID, "stif_dcn_sep_nhwc: null tensor");
-  const int rows = (a.flags & STIF_DCNSEP_P16) ? 4 : NW;   // tile rows
-  const long long wgs = (long long)((a.W + TW - 1) / TW) * ((a.H + rows - 1) / rows) * a.ngroups * a.nitems;
+  const long long wgs = (long long)((a.W + TW - 1) / TW) * ((a.H + NW - 1) / NW) * a.ngroups * a.nitems;
   if (wgs > 0x7fffffff) return stif_fail(STIF_E_INVALID, "stif_dcn_sep_nhwc: grid too large");
   dim3 grid((unsigned)wgs);
-  if (a.flags & STIF_DCNSEP_P16) {
-    if (a.epi == STIF_EPI_LRELU)
-      hipLaunchKernelGGL(k_dcn_sep16<STIF_EPI_LRELU>, grid, dim3(512), 0, (hipStream_t)stream, a);
-    else if (a.epi == STIF_EPI_NONE)
-      hipLaunchKernelGGL(k_dcn_sep16<STIF_EPI_NONE>, grid, dim3(512), 0, (hipStream_t)stream, a);
-    else
-      return stif_fail(STIF_E_INVALID, "stif_dcn_sep_nhwc: epilogue must be NONE or LRELU");
-    return stif_check_launch("stif_dcn_sep_nhwc");
-  }
   if (a.epi == STIF_EPI_LRELU)
     hipLaunchKernelGGL(k_dcn_sep<STIF_EPI_LRELU>, grid, dim3(64 * NW), 0, (hipStream_t)stream, a);
   else if (a.epi == STIF_EPI_NONE)
@@ -706,5 +416,3 @@ extern "C" int stif_dcn_sep_nhwc(const stif_dcn_sep_args* pa, void* stream) {
     return stif_fail(STIF_E_INVALID, "stif_dcn_sep_nhwc: epilogue must be NONE or LRELU");
   return stif_check_launch("stif_dcn_sep_nhwc");
 }
-
-extern "C" int stif_dcn_sep_layout(void) { return DCNSEP_P16 ? STIF_DCNSEP_P16 : 0; }

@@ -103,8 +103,6 @@ extern "C" size_t stif_conv_weight_floats(int cout, int cin, int ks, int mode) {
   // DCNSEP | F16X3 (the fused DCN_sep's offset/mask conv): 36 steps x 8 groups x 2 planes x 1 KB
   if (mode == (STIF_PACK_DCNSEP | STIF_PACK_F16X3)) return (size_t)36 * 7 * 2 * 256;
   if (mode == (STIF_PACK_DCNPAIR | STIF_PACK_F16X3)) return (size_t)4 * 9 * 2 * 2 * 256;
-  if (mode == (STIF_PACK_DCNSEP16 | STIF_PACK_F16X3)) return (size_t)18 * 14 * 2 * 256;
-  if (mode == (STIF_PACK_DCNPAIR16 | STIF_PACK_F16X3)) return (size_t)4 * 5 * 4 * 2 * 256;
   // PLAIN | F16X3 (the DCN core, 64 -> 64 3x3): 5 tap pairs x 2 nt x 2 planes x 1 KB per 8-channel group
   if (mode == (STIF_PACK_PLAIN | STIF_PACK_F16X3) && ks == 3) return (size_t)(cin / 8) * 5 * 2 * 2 * 256;
   // PLAIN | F16X3 1x1 (k_conv1x1): 2 nt x 2 planes x 1 KB per (64-cout slice, 16-channel chunk)
@@ -118,8 +116,6 @@ extern "C" size_t stif_conv_weight_floats(int cout, int cin, int ks, int mode) {
 extern "C" size_t stif_conv_bias_floats(int cout, int mode) {
   if (mode == (STIF_PACK_DCNSEP | STIF_PACK_F16X3)) return 256;
   if (mode == (STIF_PACK_DCNPAIR | STIF_PACK_F16X3)) return 64;
-  if (mode == (STIF_PACK_DCNSEP16 | STIF_PACK_F16X3)) return 256;
-  if (mode == (STIF_PACK_DCNPAIR16 | STIF_PACK_F16X3)) return 64;
   mode &= ~STIF_PACK_F16X3;
   return (mode == STIF_PACK_WINO || mode == STIF_PACK_WINO_OFFMASK || mode == STIF_PACK_WINO_LSTM)
              ? (size_t)round64(cout)
@@ -318,76 +314,6 @@ int pack_dcnpair_f16x3(const float* w, const float* b, int cout, int cin, int ks
     for (int j = 0; j < cout; ++j) b_dst[j] = b ? b[j] : 0.f;
   return STIF_OK;
 }
-// DCNSEP16 | F16X3: conv_offset_mask as the 16x16x32 A operands of k_dcn_sep16's phase 1 (stif.h).
-// Packed row R of M-tile R >> 4 is accumulator element R & 3 of lane group q = (R >> 2) & 3, slot
-// v = 4 (R >> 4) + (R & 3); slot v holds component v % 3 of sampling position v / 3 of that lane group
-// in phase 2: position 4 a + j (j < 4) = tap 2 j + (q >> 1) of group 2 a + (q & 1); position 16 + b = tap
-// 8 of group 2 a + (q & 1) of the pair a = 2 b + 1 - (q >> 1) whose step 4 is real for this lane group
-// (pairs 2 b and 2 b + 1 share the three slots; the other lane groups' step-4 weights are zero)
-int dcnsep16_src_row(int R) {
-  const int q = (R >> 2) & 3, v = 4 * (R >> 4) + (R & 3);
-  if (v >= 54) return -1;
-  const int pos = v / 3, comp = v % 3;
-  int g, tap;
-  if (pos < 16) {
-    g = 2 * (pos >> 2) + (q & 1);
-    tap = 2 * (pos & 3) + (q >> 1);
-  } else {
-    g = 2 * (2 * (pos - 16) + 1 - (q >> 1)) + (q & 1);
-    tap = 8;
-  }
-  return comp == 0 ? g * 18 + 2 * tap : (comp == 1 ? g * 18 + 2 * tap + 1 : 144 + g * 9 + tap);
-}
-int pack_dcnsep16_f16x3(const float* w, const float* b, int cout, int cin, int ks, float* w_dst, float* b_dst) {
-  if (cout != 216 || cin != 64 || ks != 3)
-    return stif_fail(STIF_E_INVALID, "STIF_PACK_DCNSEP16 packing needs the 64 -> 216 3x3 conv_offset_mask weight");
-  for (size_t i = 0; i < (size_t)cout * cin * 9; ++i)
-    if (!f16x3_ok(w[i])) return range_fail("stif_pack_conv_weight: a weight is outside the f16x3 range (|w| < 64); pack it without STIF_PACK_F16X3");
-  _Float16* dst = reinterpret_cast<_Float16*>(w_dst);
-  for (int st = 0; st < 18; ++st)
-    for (int m = 0; m < 14; ++m)
-      for (int l = 0; l < 64; ++l) {
-        const int src = dcnsep16_src_row(16 * m + (l & 15)), q = l >> 4, u = 2 * st + (q >> 1);
-        const int c = u / 9, t = u % 9;
-        for (int e = 0; e < 8; ++e) {
-          const int ci = 16 * c + 8 * (q & 1) + e;
-          const double x = src >= 0 ? (double)w[((size_t)src * cin + ci) * 9 + t] : 0.0;
-          const size_t o = (((size_t)st * 14 + m) * 2) * 512 + l * 8 + e;
-          split_f16x3_host(x, dst + o, dst + o + 512);
-        }
-      }
-  if (b_dst)
-    for (int R = 0; R < 256; ++R) {
-      const int src = R < 224 ? dcnsep16_src_row(R) : -1;
-      b_dst[R] = (src >= 0 && b) ? b[src] : 0.f;
-    }
-  return STIF_OK;
-}
-// DCNPAIR16 | F16X3: the DCN weight as the 16x16x32 A operands of k_dcn_sep16's phase 2 (stif.h)
-int pack_dcnpair16_f16x3(const float* w, const float* b, int cout, int cin, int ks, float* w_dst, float* b_dst) {
-  if (cout != 64 || cin != 64 || ks != 3)
-    return stif_fail(STIF_E_INVALID, "STIF_PACK_DCNPAIR16 packing needs a 64 -> 64 3x3 weight");
-  for (size_t i = 0; i < (size_t)cout * cin * 9; ++i)
-    if (!f16x3_ok(w[i])) return range_fail("stif_pack_conv_weight: a weight is outside the f16x3 range (|w| < 64); pack it without STIF_PACK_F16X3");
-  _Float16* dst = reinterpret_cast<_Float16*>(w_dst);
-  for (int a = 0; a < 4; ++a)
-    for (int j = 0; j < 5; ++j)
-      for (int mt = 0; mt < 4; ++mt)
-        for (int l = 0; l < 64; ++l) {
-          const int q = l >> 4, co = 16 * mt + (l & 15);
-          const int tap = j < 4 ? 2 * j + (q >> 1) : 8;
-          const bool real = j < 4 || (q >> 1) == 1 - (a & 1);
-          for (int e = 0; e < 8; ++e) {
-            const int ci = 8 * (2 * a + (q & 1)) + e;
-            const double x = real ? (double)w[((size_t)co * cin + ci) * 9 + tap] : 0.0;
-            const size_t o = ((((size_t)a * 5 + j) * 4 + mt) * 2) * 512 + l * 8 + e;
-            split_f16x3_host(x, dst + o, dst + o + 512);
-          }
-        }
-  if (b_dst)
-    for (int c = 0; c < cout; ++c) b_dst[c] = b ? b[c] : 0.f;
-  return STIF_OK;
-}
 }  // namespace
 
 extern "C" int stif_pack_conv_weight(const float* w, const float* b, int cout, int cin, int ks, int mode,
@@ -403,11 +329,6 @@ extern "C" int stif_pack_conv_weight(const float* w, const float* b, int cout, i
   if (mode == STIF_PACK_DCNPAIR) {
     if (!f16x3) return stif_fail(STIF_E_INVALID, "STIF_PACK_DCNPAIR exists for split-fp16 operands only (| STIF_PACK_F16X3)");
     return pack_dcnpair_f16x3(w, b, cout, cin, ks, w_dst, b_dst);
-  }
-  if (mode == STIF_PACK_DCNSEP16 || mode == STIF_PACK_DCNPAIR16) {
-    if (!f16x3) return stif_fail(STIF_E_INVALID, "STIF_PACK_DCNSEP16 / DCNPAIR16 exist for split-fp16 operands only (| STIF_PACK_F16X3)");
-    return mode == STIF_PACK_DCNSEP16 ? pack_dcnsep16_f16x3(w, b, cout, cin, ks, w_dst, b_dst)
-                                      : pack_dcnpair16_f16x3(w, b, cout, cin, ks, w_dst, b_dst);
   }
   if ((mode == STIF_PACK_OFFMASK || mode == STIF_PACK_WINO_OFFMASK) && cout != 216)
     return stif_fail(STIF_E_INVALID, "offmask pack needs cout=216");

@@ -42,9 +42,6 @@
 #ifndef DCNSEP_WPE
 #define DCNSEP_WPE 2       // waves per SIMD the kernel is register-budgeted for
 #endif
-#ifndef DCNSEP_P16
-#define DCNSEP_P16 0       // stif_dcn_sep_layout(): 1 = the 16-pixel kernel (k_dcn_sep16) is this build's default
-#endif
 #ifndef DCNSEP_EXP
 #define DCNSEP_EXP 0       // probes: 1 no phase 1, 3 no phase 2, 5 no per-pair restaging
 #endif

@@ -217,10 +217,10 @@ class LunaTokis(nn.Module):
                         if f16 and self.fused_dcn:
                             # the fused DCN_sep kernel (k_dcn_sep); out of the split range -> the two-kernel path
                             try:
-                                m_om, m_core = ops.dcn_sep_modes()   # the library's default kernel layout
-                                pom = ops.pack_conv(h[om + ".weight"], h[om + ".bias"], m_om, dev, range_fallback=False)
-                                pcore = ops.pack_conv(h[n + ".weight"], h[n + ".bias"], m_core, dev,
-                                                      range_fallback=False)
+                                pom = ops.pack_conv(h[om + ".weight"], h[om + ".bias"], L.PACK_DCNSEP | L.PACK_F16X3,
+                                                    dev, range_fallback=False)
+                                pcore = ops.pack_conv(h[n + ".weight"], h[n + ".bias"], L.PACK_DCNPAIR | L.PACK_F16X3,
+                                                      dev, range_fallback=False)
                                 put(n, pcore)
                                 put(om, pom)
                                 continue

@@ -214,45 +214,23 @@ def dcn(groups, *, epi=L.EPI_NONE, status=None):
         tr.end()
 
 
-def dcn_sep_modes(layout: int | None = None):
-    """(conv_offset_mask mode, DCN weight mode) of the fused DCN_sep for a stif_dcn_sep_args.flags layout bit
-    (None: the library's default, stif_dcn_sep_layout()): the 32-pixel kernel's STIF_PACK_DCNSEP / DCNPAIR or
-    the 16-pixel kernel's STIF_PACK_DCNSEP16 / DCNPAIR16, all | F16X3."""
-    if layout is None:
-        layout = L.lib().stif_dcn_sep_layout()
-    if layout & L.DCNSEP_P16:
-        return L.PACK_DCNSEP16 | L.PACK_F16X3, L.PACK_DCNPAIR16 | L.PACK_F16X3
-    return L.PACK_DCNSEP | L.PACK_F16X3, L.PACK_DCNPAIR | L.PACK_F16X3
-
-
-def _dcn_sep_layout(om_layer: PackedConv, layer: PackedConv):
-    for bit in (0, L.DCNSEP_P16):
-        if (om_layer.mode, layer.mode) == dcn_sep_modes(bit):
-            return bit
-    return None
-
-
 def dcn_sep_fusable(om_layer: PackedConv, layer: PackedConv) -> bool:
-    """Both layers of a DCN_sep packed for the fused kernel (stif_dcn_sep_nhwc), in either layout."""
-    return _dcn_sep_layout(om_layer, layer) is not None
+    """Both layers of a DCN_sep packed for the fused kernel (stif_dcn_sep_nhwc)."""
+    return om_layer.mode == (L.PACK_DCNSEP | L.PACK_F16X3) and layer.mode == (L.PACK_DCNPAIR | L.PACK_F16X3)
 
 
 def dcn_sep(groups, *, epi=L.EPI_NONE, status=None):
     """Fused DCN_sep (dcn_v2.py:127-140): offset/mask conv + sigmoid + deformable conv in one launch.
     groups: list of {om_layer: PackedConv (STIF_PACK_DCNSEP | F16X3), layer: PackedConv (64->64 3x3,
-    STIF_PACK_DCNPAIR | F16X3), fea, inp, out} with NHWC [nitems, H, W, 64] tensors -- or every group packed
-    STIF_PACK_DCNSEP16 / DCNPAIR16 (the 16-pixel kernel, dcn_sep_modes)."""
+    STIF_PACK_DCNPAIR | F16X3), fea, inp, out} with NHWC [nitems, H, W, 64] tensors."""
     if not 1 <= len(groups) <= L.MAXG:
         raise ValueError("dcn_sep: 1..8 groups")
     g0 = groups[0]
     nitems, H, W, Cc = g0["inp"].shape
     a = L.DcnSepArgs()
-    layout = _dcn_sep_layout(g0["om_layer"], g0["layer"])
     for i, g in enumerate(groups):
         if not dcn_sep_fusable(g["om_layer"], g["layer"]):
             raise ValueError("dcn_sep: layers not packed for the fused kernel")
-        if _dcn_sep_layout(g["om_layer"], g["layer"]) != layout:
-            raise ValueError("dcn_sep: groups packed for different kernel layouts")
         for k in ("fea", "inp", "out"):
             if tuple(g[k].shape) != (nitems, H, W, 64):
                 raise ValueError(f"dcn_sep: {k} shape {tuple(g[k].shape)} != {(nitems, H, W, 64)}")
@@ -267,7 +245,7 @@ def dcn_sep(groups, *, epi=L.EPI_NONE, status=None):
     a.in_item = _item_stride([g["inp"] for g in groups], "dcn_sep in")
     a.out_item = _item_stride([g["out"] for g in groups], "dcn_sep out")
     a.ngroups, a.nitems, a.H, a.W, a.epi = len(groups), nitems, H, W, epi
-    a.flags = L.CONV_F16X3 | layout
+    a.flags = L.CONV_F16X3
     a.status = _vp(status)
     tr = TRACE
     if tr is not None:

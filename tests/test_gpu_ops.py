@@ -450,24 +450,17 @@ def _dcnsep_weights(seed, oscale, boundary=False, H=0):
     return {"x.conv_offset_mask.weight": w_om, "x.conv_offset_mask.bias": b_om, "x.weight": w, "x.bias": b}
 
 
-@pytest.fixture(params=[0, 2], ids=["p32", "p16"])
-def dcnsep_layout(request):
-    """Both fused DCN_sep kernels: k_dcn_sep (32 pixels per wave, STIF_PACK_DCNSEP / DCNPAIR) and k_dcn_sep16
-    (16 pixels per wave on 16x16x32 MFMAs, STIF_PACK_DCNSEP16 / DCNPAIR16, flags STIF_DCNSEP_P16 = 2)."""
-    return request.param
-
-
-def _dcnsep_layers(ops, L, sdx, layout=0):
-    m_om, m_core = ops.dcn_sep_modes(layout)
-    om = ops.pack_conv(sdx["x.conv_offset_mask.weight"], sdx["x.conv_offset_mask.bias"], m_om, range_fallback=False)
-    core = ops.pack_conv(sdx["x.weight"], sdx["x.bias"], m_core, range_fallback=False)
+def _dcnsep_layers(ops, L, sdx):
+    om = ops.pack_conv(sdx["x.conv_offset_mask.weight"], sdx["x.conv_offset_mask.bias"], L.PACK_DCNSEP | L.PACK_F16X3,
+                       range_fallback=False)
+    core = ops.pack_conv(sdx["x.weight"], sdx["x.bias"], L.PACK_DCNPAIR | L.PACK_F16X3, range_fallback=False)
     return om, core
 
 
 @pytest.mark.parametrize("epi", ["none", "lrelu"])
 @pytest.mark.parametrize("hw", [(9, 11), (8, 32), (16, 40), (21, 70), (70, 37)])
 @pytest.mark.parametrize("oscale", [0.7, 2.0, 7.0])   # 7.0: many samples leave the staged margin
-def test_dcn_sep_fused_matches_oracle(ops, L, epi, hw, oscale, dcnsep_layout):
+def test_dcn_sep_fused_matches_oracle(ops, L, epi, hw, oscale):
     """k_dcn_sep (stif_dcn_sep_nhwc): conv_offset_mask + chunk/cat/sigmoid + the deformable conv in one
     launch == DCN_sep.forward (dcn_v2.py:127-140) restated by the oracle; partial tiles (9x11, 21x70,
     70x37), exact tiles (8x32), samples beyond the staged margin, two items."""
@@ -479,7 +472,7 @@ def test_dcn_sep_fused_matches_oracle(ops, L, epi, hw, oscale, dcnsep_layout):
     ref = O.dcn_sep(x, fea, sdx, "x")
     if epi == "lrelu":
         ref = O.lrelu(ref)
-    om, core = _dcnsep_layers(ops, L, sdx, dcnsep_layout)
+    om, core = _dcnsep_layers(ops, L, sdx)
     out = torch.full((B, H, W, 64), float("nan"), device="cuda")
     st = torch.zeros(1, dtype=torch.int32, device="cuda")
     ops.dcn_sep([dict(om_layer=om, layer=core, fea=nhwc(fea), inp=nhwc(x), out=out)],
@@ -488,7 +481,7 @@ def test_dcn_sep_fused_matches_oracle(ops, L, epi, hw, oscale, dcnsep_layout):
     assert relmax(to_nchw(out), ref) < RTOL
 
 
-def test_dcn_sep_fused_many_workgroups(ops, L, dcnsep_layout):
+def test_dcn_sep_fused_many_workgroups(ops, L):
     """k_dcn_sep with more workgroups than CUs (two resident per CU, several rounds, two weight sets):
     == the oracle, and three launches agree bit for bit."""
     H, W, B = 64, 128, 6
@@ -497,7 +490,7 @@ def test_dcn_sep_fused_many_workgroups(ops, L, dcnsep_layout):
     fs = [rnd(B, 64, H, W, seed=93 + i) for i in range(2)]
     groups, outs = [], []
     for i in range(2):
-        om, core = _dcnsep_layers(ops, L, sds[i], dcnsep_layout)
+        om, core = _dcnsep_layers(ops, L, sds[i])
         outs.append(torch.full((B, H, W, 64), float("nan"), device="cuda"))
         groups.append(dict(om_layer=om, layer=core, fea=nhwc(fs[i]), inp=nhwc(xs[i]), out=outs[i]))
     st = torch.zeros(1, dtype=torch.int32, device="cuda")
@@ -513,7 +506,7 @@ def test_dcn_sep_fused_many_workgroups(ops, L, dcnsep_layout):
 
 
 @pytest.mark.parametrize("oscale", [2.0, 7.0])
-def test_dcn_sep_fused_batch_independent(ops, L, oscale, dcnsep_layout):
+def test_dcn_sep_fused_batch_independent(ops, L, oscale):
     """k_dcn_sep: an item's output does not depend on the other items of the launch (tile placement,
     workgroup scheduling, which lanes of a wave take the global fallback), bit for bit, and two launches
     of the same batch agree bit for bit."""
@@ -521,7 +514,7 @@ def test_dcn_sep_fused_batch_independent(ops, L, oscale, dcnsep_layout):
     sdx = _dcnsep_weights(80, oscale)
     x = torch.from_numpy(rnd(B, H, W, 64, seed=81)).cuda()
     fea = torch.from_numpy(rnd(B, H, W, 64, seed=82)).cuda()
-    om, core = _dcnsep_layers(ops, L, sdx, dcnsep_layout)
+    om, core = _dcnsep_layers(ops, L, sdx)
 
     def run(xs, fs):
         out = torch.full(xs.shape, float("nan"), device="cuda")
@@ -534,7 +527,7 @@ def test_dcn_sep_fused_batch_independent(ops, L, oscale, dcnsep_layout):
         assert torch.equal(full[i:i + 1], run(x[i:i + 1].clone(), fea[i:i + 1].clone())), i
 
 
-def test_dcn_sep_fused_gates_and_groups(ops, L, dcnsep_layout):
+def test_dcn_sep_fused_gates_and_groups(ops, L):
     """Offsets exactly on the sampling gates (bias-only offset channels), and a launch of 3 weight sets
     over strided items (a [3, n, H, W, 64] buffer's sub-tensors), each against its own oracle."""
     H, W = 19, 45
@@ -545,7 +538,7 @@ def test_dcn_sep_fused_gates_and_groups(ops, L, dcnsep_layout):
     sds = [_dcnsep_weights(70 + 10 * i, 2.0 + i, boundary=True, H=H) for i in range(3)]
     groups = []
     for i, sdx in enumerate(sds):
-        om, core = _dcnsep_layers(ops, L, sdx, dcnsep_layout)
+        om, core = _dcnsep_layers(ops, L, sdx)
         groups.append(dict(om_layer=om, layer=core, fea=fs[i], inp=xs[i], out=out[i]))
     ops.dcn_sep(groups, epi=L.EPI_NONE)
     for i, sdx in enumerate(sds):
@@ -554,13 +547,13 @@ def test_dcn_sep_fused_gates_and_groups(ops, L, dcnsep_layout):
         assert relmax(to_nchw(out[i]), O.dcn_sep(x, f, sdx, "x")) < RTOL, i
 
 
-def test_dcn_sep_fused_equals_two_kernel_path(ops, L, dcnsep_layout):
+def test_dcn_sep_fused_equals_two_kernel_path(ops, L):
     """The fused kernel and the two-launch path it replaces (k_wino_om -> 216-channel map -> k_dcn, both
     f16x3) agree to the parity bar on the STIF shape."""
     H, W = 32, 48
     sdx = _dcnsep_weights(80, 3.0)
     x, fea = rnd(2, 64, H, W, seed=81), rnd(2, 64, H, W, seed=82)
-    om, core = _dcnsep_layers(ops, L, sdx, dcnsep_layout)
+    om, core = _dcnsep_layers(ops, L, sdx)
     a = torch.empty(2, H, W, 64, device="cuda")
     ops.dcn_sep([dict(om_layer=om, layer=core, fea=nhwc(fea), inp=nhwc(x), out=a)])
     omw = ops.pack_conv(sdx["x.conv_offset_mask.weight"], sdx["x.conv_offset_mask.bias"],
@@ -575,7 +568,7 @@ def test_dcn_sep_fused_equals_two_kernel_path(ops, L, dcnsep_layout):
 
 
 @pytest.mark.parametrize("which", ["fea", "inp"])
-def test_dcn_sep_fused_reports_range(ops, L, which, dcnsep_layout):
+def test_dcn_sep_fused_reports_range(ops, L, which):
     """k_dcn_sep's own range reporting (advisor finding, round 3): one offset-feature value (phase 1: the
     offset/mask sums go non-finite, the `chk` sum) or one DCN-input value (phase 2: the output goes
     non-finite, `chk2`) far outside the split-fp16 range sets the status word; the same call in range
@@ -586,7 +579,7 @@ def test_dcn_sep_fused_reports_range(ops, L, which, dcnsep_layout):
     sdx = _dcnsep_weights(40, 2.0)
     x = rnd(B, 64, H, W, seed=41)
     fea = rnd(B, 64, H, W, seed=42)
-    om, core = _dcnsep_layers(ops, L, sdx, dcnsep_layout)
+    om, core = _dcnsep_layers(ops, L, sdx)
     st = torch.zeros(1, dtype=torch.int32, device="cuda")
     out = torch.empty(B, H, W, 64, device="cuda")
     xi, fi = nhwc(x), nhwc(fea)

@@ -281,80 +281,3 @@ def test_pack_dcnsep_layout(stif):
         with pytest.raises(L.StifError):
             L.check(lib.stif_pack_conv_weight(w.ctypes.data, b.ctypes.data, 216 if md == L.PACK_DCNSEP else 64, 64, 3,
                                               md, wd.ctypes.data, bd.ctypes.data), "pack")
-
-
-def test_pack_dcnsep16_emulated_matches_oracle(stif):
-    """STIF_PACK_DCNSEP16 / DCNPAIR16 (include/stif.h), checked by emulating k_dcn_sep16's algebra on the
-    packed buffers in float64: phase 1 forms accumulator slot v of lane group q from the A operands of every
-    half-step exactly as the kernel orders K (unit 2 s + (q >> 1), channels 8 (q & 1) ..), phase 2 reads
-    (dy, dx, mask) from slot 3 pos + comp, samples tap 2 j + (q >> 1) / tap 8 of group 2 pair + (q & 1)
-    (the shared step-4 slots, a zeroed sample on the lane groups whose step 4 is the other pair's) and
-    contracts with the DCNPAIR16 fragments; the result equals the oracle's DCN_sep (dcn_v2.py:127-140).
-    This pins every index of the two packings and of the kernel's slot map before any GPU run."""
-    from oracle import stif_oracle as O
-    L = stif._lib
-    lib = L.lib()
-    rng = np.random.default_rng(3)
-    H, W = 5, 7
-    sd = {"x.conv_offset_mask.weight": (rng.standard_normal((216, 64, 3, 3)) * 0.08).astype(np.float32),
-          "x.conv_offset_mask.bias": (rng.standard_normal(216) * 0.7).astype(np.float32),
-          "x.weight": (rng.standard_normal((64, 64, 3, 3)) * 0.05).astype(np.float32),
-          "x.bias": rng.standard_normal(64).astype(np.float32)}
-    x = rng.standard_normal((1, 64, H, W)).astype(np.float32)
-    fea = rng.standard_normal((1, 64, H, W)).astype(np.float32)
-
-    def pack(w, b, cout, mode):
-        wd = np.empty(lib.stif_conv_weight_floats(cout, 64, 3, mode), np.float32)
-        bd = np.empty(lib.stif_conv_bias_floats(cout, mode), np.float32)
-        L.check(lib.stif_pack_conv_weight(w.ctypes.data, b.ctypes.data, cout, 64, 3, mode, wd.ctypes.data,
-                                          bd.ctypes.data), "pack")
-        return wd, bd
-
-    w1, b1 = pack(sd["x.conv_offset_mask.weight"], sd["x.conv_offset_mask.bias"], 216, L.PACK_DCNSEP16 | L.PACK_F16X3)
-    w2, b2 = pack(sd["x.weight"], sd["x.bias"], 64, L.PACK_DCNPAIR16 | L.PACK_F16X3)
-    h1 = w1.view(np.float16).reshape(18, 14, 2, 64, 8).astype(np.float64)
-    A1 = (h1[:, :, 0] + h1[:, :, 1]) / 1024.0                   # [step][M-tile][lane][e]
-    h2 = w2.view(np.float16).reshape(4, 5, 4, 2, 64, 8).astype(np.float64)
-    A2 = (h2[:, :, :, 0] + h2[:, :, :, 1]) / 1024.0             # [pair][step][M-tile][lane][e]
-    xp = np.pad(x[0].astype(np.float64), ((0, 0), (1, 1), (1, 1)))
-    fp = np.pad(fea[0].astype(np.float64), ((0, 0), (1, 1), (1, 1)))
-    img = x[0].astype(np.float64)
-    out = np.zeros((64, H, W))
-    for y in range(H):
-        for xx in range(W):
-            om = np.zeros((4, 56))
-            for R in range(224):
-                m, r = divmod(R, 16)
-                q, i = r >> 2, r & 3
-                acc = float(b1[R])
-                for s in range(18):
-                    for kg in range(4):
-                        c, t = divmod(2 * s + (kg >> 1), 9)
-                        ch = 16 * c + 8 * (kg & 1) + np.arange(8)
-                        acc += float(A1[s, m, kg * 16 + r] @ fp[ch, y + t // 3, xx + t % 3])
-                om[q, 4 * m + i] = acc
-            om[:, 2::3] = 1.0 / (1.0 + np.exp(-om[:, 2::3]))
-            o = sd["x.bias"].astype(np.float64).copy()
-            for pa in range(4):
-                for j in range(5):
-                    pos = 4 * pa + j if j < 4 else 16 + (pa >> 1)
-                    for q in range(4):
-                        t = 2 * j + (q >> 1) if j < 4 else 8
-                        dy, dx, mk = om[q, 3 * pos:3 * pos + 3]
-                        smp = np.zeros(8)
-                        if not (j == 4 and (q >> 1) == (pa & 1)):
-                            hi, wi = y - 1 + t // 3 + dy, xx - 1 + t % 3 + dx
-                            if hi > -1 and wi > -1 and hi < H and wi < W:
-                                y0, x0 = int(np.floor(hi)), int(np.floor(wi))
-                                ly, lx = hi - y0, wi - x0
-                                ch = 16 * pa + 8 * (q & 1) + np.arange(8)
-                                for yy, xc, wt in ((y0, x0, (1 - ly) * (1 - lx)), (y0, x0 + 1, (1 - ly) * lx),
-                                                   (y0 + 1, x0, ly * (1 - lx)), (y0 + 1, x0 + 1, ly * lx)):
-                                    if 0 <= yy < H and 0 <= xc < W:
-                                        smp += wt * img[ch, yy, xc]
-                                smp *= mk
-                        for mt in range(4):
-                            o[16 * mt:16 * mt + 16] += A2[pa, j, mt, q * 16:q * 16 + 16] @ smp
-            out[:, y, xx] = o
-    ref = O.dcn_sep(x, fea, sd, "x")[0]
-    assert np.abs(out - ref).max() <= 1e-5 * np.abs(ref).max(), np.abs(out - ref).max()

@@ -23,11 +23,10 @@ g = torch.Generator(device="cuda").manual_seed(0)
 fea = torch.randn(N, HW, HW, 64, device="cuda", generator=g) * (OSCALE / 23.0)
 inp = torch.randn(N, HW, HW, 64, device="cuda", generator=g)
 out = torch.empty_like(inp)
-m_om, m_core = ops.dcn_sep_modes()   # the library's default fused layout
-core = ops.pack_conv(sd[p + ".weight"], sd[p + ".bias"], m_core if FUSED else L.PACK_PLAIN | L.PACK_F16X3)
+core = ops.pack_conv(sd[p + ".weight"], sd[p + ".bias"], (L.PACK_DCNPAIR if FUSED else L.PACK_PLAIN) | L.PACK_F16X3)
 if FUSED:
-    om = ops.pack_conv(sd[p + ".conv_offset_mask.weight"], sd[p + ".conv_offset_mask.bias"], m_om,
-                       range_fallback=False)
+    om = ops.pack_conv(sd[p + ".conv_offset_mask.weight"], sd[p + ".conv_offset_mask.bias"],
+                       L.PACK_DCNSEP | L.PACK_F16X3, range_fallback=False)
     run = lambda: ops.dcn_sep([dict(om_layer=om, layer=core, fea=fea, inp=inp, out=out)])
 else:
     omw = ops.pack_conv(sd[p + ".conv_offset_mask.weight"], sd[p + ".conv_offset_mask.bias"],
