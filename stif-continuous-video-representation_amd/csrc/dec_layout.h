@@ -50,7 +50,14 @@ constexpr int E_W4V = L_W3V + 4 * 256;   // [3][256], padded to a whole 4-KB til
 constexpr int E_W4V_B3 = E_W4V + 768;    // the pad holds a copy of E_B3 (k_dec2 reads it from LDS)
 constexpr int V_END = E_W4V + 1024;
 
-constexpr int MLP_FLOATS = V_END;
+// encode_imnet's MFMA tiles again for the 16-pixel stage 2 (k_dec2q, f16x3 packing only; zero otherwise): the
+// same [ot][kt] tile order, each 32x32 tile as two 16-row sub-tiles s of v_mfma_f32_16x16x32_f16 A operands
+// [s][plane h|l][lane][8 halves], lane l holding row 16 s + (l & 15) and input feature
+// 16 (e >> 2) + 4 (l >> 4) + (e & 3) -- the order in which a 16x16 accumulator pair holds a 32-feature tile
+constexpr int Q_W0 = V_END, Q_W1 = Q_W0 + 8 * T, Q_W2 = Q_W1 + 4 * T, Q_W3 = Q_W2 + 16 * T;
+constexpr int Q_END = Q_W3 + 64 * T;
+
+constexpr int MLP_FLOATS = Q_END;
 constexpr int IMG_C = 8;      // high-resolution image channels: rgb0 rgb1 + 2 zero (16-B aligned pixels)
 constexpr int PROJ_C = 256;   // LR projection channels: P1 | P2 | P3 | P4
 constexpr int SRC_C = 200;    // LR source channels: feat t0|t1|t2 (192) + rgb0 rgb1 (6) + 2 zero

@@ -695,6 +695,239 @@ __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DE
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// k_dec2q: stage 2 (split-fp16, LR-projection image inputs) at 16 pixels per wave on
+// v_mfma_f32_16x16x32_f16.  Lane l = (p = l & 15: the wave's pixel, q = l >> 4).  A 32-feature register
+// tile is two 16x16 accumulators: lane (p, q) holds features 16 s + 4 q + i (s = 0, 1; i = 0..3) of pixel
+// p -- which is also the B-operand order of the next layer's K (dec_layout.h Q_*), so features stay in
+// registers between layers as in k_dec2.  The layer-3 state halves (8 tiles x 8 floats = 64 VGPRs): 128 VGPRs,
+// and 4-wave 64-pixel workgroups streaming the weights in 5-tile segments (2 x 20 KB of LDS) run FOUR
+// workgroups per CU -- more independent workgroups, the occupancy that paid in k_dec1 (2 -> 3 -> 4).
+// Gathers: each lane fetches its own quarter of a 64-channel block (16 corner loads in flight).
+constexpr int DEC2Q_NW = 4;
+constexpr int SEGQ = 5;   // tiles per segment
+struct R32 {
+  f32x4 s[2];
+};
+struct XQ {
+  f16x8 h, l;
+};
+STIF_DEV XQ xq(const R32& x) {
+  XQ o;
+  split_f16x3(x.s[0], x.s[1], o.h, o.l);
+  return o;
+}
+STIF_DEV void tile_q(R32& acc, const float* t, const XQ& x, int lane) {
+  const float* b = t + lane * 4;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const f16x8 ah = ldh8(b + (2 * s) * 256), al = ldh8(b + (2 * s + 1) * 256);
+    acc.s[s] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, x.h, acc.s[s], 0, 0, 0);
+    acc.s[s] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, x.h, acc.s[s], 0, 0, 0);
+    acc.s[s] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, x.l, acc.s[s], 0, 0, 0);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+// sin(z * 2^-14 + b) of a register tile whose features start at fb (biases carry omega_0 / 2 pi, pack.cpp)
+STIF_DEV R32 bias_sin_q(const R32& z, const float* __restrict__ b, int q) {
+  R32 o;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const f32x4 bb = ld4(b + 16 * s + 4 * q);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o.s[s][e] = siren_sin<1>(fmaf(z.s[s][e], ACC_S<1>, bb[e]));
+  }
+  return o;
+}
+// bilinear sample of this lane's channels c0 + 32 ot + 16 s + 4 q .. + 3 (ot, s = 0, 1) of an NHWC map
+STIF_DEV void gather_q(R32* dst, const float* __restrict__ base, int stride, int c0, const Bilin& b, int q) {
+  const int c = c0 + 4 * q;
+  const float* p00 = base + (size_t)b.o00 * stride + c;
+  const float* p01 = base + (size_t)b.o01 * stride + c;
+  const float* p10 = base + (size_t)b.o10 * stride + c;
+  const float* p11 = base + (size_t)b.o11 * stride + c;
+  f32x4 cr[4][4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {   // g = 2 ot + s: channel offset 16 g
+    cr[g][0] = ld4(p00 + 16 * g);
+    cr[g][1] = ld4(p01 + 16 * g);
+    cr[g][2] = ld4(p10 + 16 * g);
+    cr[g][3] = ld4(p11 + 16 * g);
+  }
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    f32x4 v = b.w00 * cr[g][0] + b.w01 * cr[g][1] + b.w10 * cr[g][2] + b.w11 * cr[g][3];
+    asm volatile("" : "+v"(v));
+    dst[g >> 1].s[g & 1] = v;
+  }
+}
+
+__global__ __launch_bounds__(DEC2Q_NW * 64) __attribute__((amdgpu_waves_per_eu(4))) void k_dec2q(
+    const float* __restrict__ proj, const float* __restrict__ mlp, const float* __restrict__ hrfeat,
+    const float* __restrict__ flow, stif_dec_tables tb, const float* __restrict__ tq, float* __restrict__ out, int n,
+    int h, int w, int HH, int WW, int* status) {
+  __shared__ __attribute__((aligned(16))) float wbuf[2 * SEGQ * T];
+  const int lane = threadIdx.x & 63, q = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float* const B0 = wbuf;
+  float* const B1 = wbuf + SEGQ * T;
+  const __amdgpu_buffer_rsrc_t rm = mlp_rsrc(mlp);
+  // segments: [L0 kt 0-1: 4 tiles] [L0 kt 2-3: 4] [L1: 4], per layer-2 tile kt [W2 rows kt (2) + W3 column kt,
+  // ot 0-2 (3)] [W3 column kt, ot 3-7 (5)], then [W4 rows + B3]
+  auto seg_l0 = [&](float* dst, int k0) {   // W0 tiles (ot, k0), (ot, k0 + 1): tile index 4 ot + kt
+    dma_tiles<DEC2Q_NW>(dst, rm, Q_W0 + k0 * T, 2, wv, lane);
+    dma_tiles<DEC2Q_NW>(dst + 2 * T, rm, Q_W0 + (4 + k0) * T, 2, wv, lane);
+  };
+  seg_l0(B0, 0);
+  const long long total = (long long)n * HH * WW;
+  const long long pix = ((long long)xcd_block(blockIdx.x, gridDim.x) * DEC2Q_NW + wv) * 16 + (lane & 15);
+  const bool valid = pix < total;
+  const long long pc = valid ? pix : total - 1;
+  const int item = (int)(pc / ((long long)HH * WW));
+  const int rem = (int)(pc - (long long)item * HH * WW);
+  const int py = rem / WW, px = rem - py * WW;
+  const float t = tq[item];
+  const float* P = proj + (size_t)item * h * w * PROJ_C;
+  const float* HRF = hrfeat + (size_t)item * HH * WW * 64;
+
+  // warpgrid (warplayer.py:25-39) and the decoder's clamp (Sakuya_arch_test.py:428,441), as k_dec2
+  const f32x4 fv = ld4(flow + (size_t)pc * 4);
+  const float lo = -1.f + 1e-6f, hi = 1.f - 1e-6f;
+  const float dx = ((float)WW - 1.f) / 2.f, dy = ((float)HH - 1.f) / 2.f;
+  const float bx = tb.lin_x[px], by = tb.lin_y[py];
+  const float g1x = fminf(fmaxf(bx + fv[0] / dx, lo), hi), g1y = fminf(fmaxf(by + fv[1] / dy, lo), hi);
+  const float g2x = fminf(fmaxf(bx + fv[2] / dx, lo), hi), g2y = fminf(fmaxf(by + fv[3] / dy, lo), hi);
+
+  // ---- encode_imnet layer 0: W[:, :128] . [q_feat1 | q_feat2] + P3(grid1) + P4(grid2) + w_t t + b
+  R32 x0[2];
+  {
+    R32 z[2], g[2];
+    gather_q(z, P, PROJ_C, 128, bilin(g1x, g1y, w, h), q);
+    asm volatile("" ::: "memory");
+    gather_q(g, P, PROJ_C, 192, bilin(g2x, g2y, w, h), q);
+#pragma unroll
+    for (int ot = 0; ot < 2; ++ot)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int f = 32 * ot + 16 * s + 4 * q;
+        const f32x4 wt = ld4(mlp + E_WT + f), bb = ld4(mlp + E_B0 + f);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          z[ot].s[s][e] = (z[ot].s[s][e] + (g[ot].s[s][e] + wt[e] * t + bb[e])) * ACC_IN<1>;
+      }
+    asm volatile("" ::: "memory");
+    gather_q(g, HRF, 64, 0, bilin(g1x, g1y, WW, HH), q);   // q_feat1 -> W0 columns 0..63
+    lds_dma_barrier();
+    seg_l0(B1, 2);
+    {
+      const XQ qs[2] = {xq(g[0]), xq(g[1])};
+#pragma unroll
+      for (int ot = 0; ot < 2; ++ot)
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) tile_q(z[ot], B0 + (ot * 2 + kt) * T, qs[kt], lane);
+    }
+    asm volatile("" ::: "memory");
+    gather_q(g, HRF, 64, 0, bilin(g2x, g2y, WW, HH), q);   // q_feat2 -> W0 columns 64..127
+    lds_dma_barrier();
+    dma_tiles<DEC2Q_NW>(B0, rm, Q_W1, 4, wv, lane);
+    const XQ qs[2] = {xq(g[0]), xq(g[1])};
+#pragma unroll
+    for (int ot = 0; ot < 2; ++ot) {
+#pragma unroll
+      for (int kt = 2; kt < 4; ++kt) tile_q(z[ot], B1 + (ot * 2 + kt - 2) * T, qs[kt - 2], lane);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x0[ot].s[s][e] = siren_sin<1>(z[ot].s[s][e] * ACC_S<1>);
+    }
+  }
+  lds_dma_barrier();
+  // layer-2/3 segment 2 kt + h: h = 0 the W2 rows of tile kt + W3 (ot 0-2, kt), h = 1 W3 (ot 3-7, kt)
+  auto seg_l23 = [&](float* dst, int kt, int h) {
+    if (h == 0) {
+      dma_tiles<DEC2Q_NW>(dst, rm, Q_W2 + kt * 2 * T, 2, wv, lane);
+#pragma unroll
+      for (int ot = 0; ot < 3; ++ot) dma_tiles<DEC2Q_NW>(dst + (2 + ot) * T, rm, Q_W3 + (ot * 8 + kt) * T, 1, wv, lane);
+    } else {
+#pragma unroll
+      for (int ot = 3; ot < 8; ++ot) dma_tiles<DEC2Q_NW>(dst + (ot - 3) * T, rm, Q_W3 + (ot * 8 + kt) * T, 1, wv, lane);
+    }
+  };
+  seg_l23(B1, 0, 0);
+  R32 x1[2];
+  {
+    const XQ xs[2] = {xq(x0[0]), xq(x0[1])};
+#pragma unroll
+    for (int ot = 0; ot < 2; ++ot) {
+      R32 acc;
+      acc.s[0] = acc.s[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) tile_q(acc, B0 + (ot * 2 + kt) * T, xs[kt], lane);
+      x1[ot] = bias_sin_q(acc, mlp + E_B1 + 32 * ot, q);
+    }
+  }
+  const XQ x1s[2] = {xq(x1[0]), xq(x1[1])};
+  // layer 2 (64 -> 256, sine) streamed tile by tile into the 8 register tiles of layer 3 (256 -> 256)
+  R32 a3[8];
+#pragma unroll
+  for (int ot = 0; ot < 8; ++ot) a3[ot].s[0] = a3[ot].s[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // segment 2 kt sits in B1, 2 kt + 1 in B0
+  auto l23_step = [&](int kt, bool last) {
+    lds_dma_barrier();
+    seg_l23(B0, kt, 1);
+    R32 acc;
+    acc.s[0] = acc.s[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    tile_q(acc, B1, x1s[0], lane);
+    tile_q(acc, B1 + T, x1s[1], lane);
+    const XQ h2 = xq(bias_sin_q(acc, mlp + E_B2 + kt * 32, q));
+#pragma unroll
+    for (int ot = 0; ot < 3; ++ot) tile_q(a3[ot], B1 + (2 + ot) * T, h2, lane);
+    lds_dma_barrier();
+    if (!last) seg_l23(B1, kt + 1, 0);
+    else dma_tiles<DEC2Q_NW>(B1, rm, E_W4V, 1, wv, lane);
+#pragma unroll
+    for (int ot = 3; ot < 8; ++ot) tile_q(a3[ot], B0 + (ot - 3) * T, h2, lane);
+  };
+#pragma unroll 1
+  for (int kt = 0; kt < 7; ++kt) l23_step(kt, false);
+  l23_step(7, true);
+  // layer 3 sine streamed into layer 4 (256 -> 3, VALU dot products over this lane's 64 features); W4 rows
+  // and the layer-3 biases in B1 (k_dec2's tile)
+  lds_dma_barrier();
+  float* const B4 = B1;
+  float o4[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kt = 0; kt < 8; ++kt) {
+    const R32 h3 = bias_sin_q(a3[kt], B4 + (E_W4V_B3 - E_W4V) + kt * 32, q);
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const f32x4 wr = ld4(B4 + c * 256 + kt * 32 + 16 * s + 4 * q);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o4[c] = fmaf(wr[e], h3.s[s][e], o4[c]);
+      }
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {   // the other three lane groups' features
+    o4[c] += __shfl_xor(o4[c], 16);
+    o4[c] += __shfl_xor(o4[c], 32);
+  }
+  if (valid && q == 0) {
+    const size_t plane = (size_t)HH * WW;
+    float* o = out + (size_t)item * 3 * plane + (size_t)py * WW + px;
+    bool bad = not_finite((fv[0] + fv[1]) + (fv[2] + fv[3]));
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float v = o4[c] + mlp[E_B4 + c];
+      bad |= not_finite(v);
+      o[c * plane] = v;
+    }
+    report_range(status, bad);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_pack_lr(const float* __restrict__ f0, const float* __restrict__ f1,
                                                  const float* __restrict__ f2, const float* __restrict__ x,
                                                  float* __restrict__ out, int n, int h, int w) {
@@ -814,6 +1047,12 @@ extern "C" int stif_dec_stage2_ex(const float* proj, const float* mlp, const flo
   const long long blocks = (total + DEC2_NW * 32 - 1) / (DEC2_NW * 32);
   const stif_dec_image im = img ? *img : stif_dec_image{};
   hipStream_t st = (hipStream_t)stream;
+  if (DEC2_Q16 && f16 && !img) {
+    const long long qblocks = (total + DEC2Q_NW * 16 - 1) / (DEC2Q_NW * 16);
+    hipLaunchKernelGGL(k_dec2q, dim3((unsigned)qblocks), dim3(DEC2Q_NW * 64), 0, st, proj, mlp, hrfeat, flow, *tab, t,
+                       out, n, h, w, HH, WW, status);
+    return stif_check_launch("stif_dec_stage2");
+  }
   const dim3 g((unsigned)blocks), b(DEC2_NW * 64);
   if (img && f16) hipLaunchKernelGGL((k_dec2<true, 1>), g, b, 0, st, proj, mlp, hrfeat, flow, *tab, im, t, out, n, h, w, HH, WW, status);
   else if (img) hipLaunchKernelGGL((k_dec2<true, 0>), g, b, 0, st, proj, mlp, hrfeat, flow, *tab, im, t, out, n, h, w, HH, WW, status);

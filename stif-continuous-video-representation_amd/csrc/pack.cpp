@@ -445,6 +445,21 @@ void tile_to_f16x3(float* t) {
         split_f16x3_host(x, dst + o, dst + o + 512);
       }
 }
+// fp32 tile [v][lane][4] -> the 16x16x32 split-fp16 tile of k_dec2q (dec_layout.h Q_*) at dst: element
+// (s, e) of lane l = W[16 s + (l & 15)][16 (e >> 2) + 4 (l >> 4) + (e & 3)], read from the fp32 tile where
+// row r, column c sits at lane r + 32 ((c >> 2) & 1), register (c & 3) + 4 (c >> 3)
+void tile_to_q16(const float* src, float* t) {
+  _Float16* dst = reinterpret_cast<_Float16*>(t);
+  for (int s = 0; s < 2; ++s)
+    for (int l = 0; l < 64; ++l)
+      for (int e = 0; e < 8; ++e) {
+        const int row = 16 * s + (l & 15), col = 16 * (e >> 2) + 4 * (l >> 4) + (e & 3);
+        const int r = (col & 3) + 4 * (col >> 3);
+        const double x = src[((r >> 2) * 64 + row + 32 * ((col >> 2) & 1)) * 4 + (r & 3)];
+        const size_t o = ((size_t)(2 * s) * 64 + l) * 8 + e;
+        split_f16x3_host(x, dst + o, dst + o + 512);
+      }
+}
 }  // namespace
 
 extern "C" int stif_pack_dec_mlp(const float* const* f, const float* const* l, const float* const* e, float* d) {
@@ -533,6 +548,10 @@ extern "C" int stif_pack_dec_mlp_ex(const float* const* f, const float* const* l
       for (int k = 0; k < r[1]; ++k)
         if (!tile_f16x3_ok(d + r[0] + k * T))
           return range_fail("stif_pack_dec_mlp_ex: a SIREN weight (times omega_0 for sine layers) is outside the f16x3 range (|w| < 64); pack with flags = 0");
+    // k_dec2q's copies of encode_imnet's tiles, from the fp32 tiles before they are split in place
+    const int qregions[][3] = {{E_W0, Q_W0, 8}, {E_W1, Q_W1, 4}, {E_W2, Q_W2, 16}, {E_W3, Q_W3, 64}};
+    for (const auto& r : qregions)
+      for (int k = 0; k < r[2]; ++k) tile_to_q16(d + r[0] + k * T, d + r[1] + k * T);
     for (const auto& r : regions)
       for (int k = 0; k < r[1]; ++k) tile_to_f16x3(d + r[0] + k * T);
     for (int i = I_L; i < I_END; ++i) d[i] *= 16384.f;

@@ -60,6 +60,9 @@ static_assert(DCNSEP_EXP == 0 || DCNSEP_EXP == 1 || DCNSEP_EXP == 3 || DCNSEP_EX
 // r04_dec1_occ_ab.log) -> 720 us (3 -> 4; C2 11.6 -> 11.1 ms, r04_dec1_occ4_ab.log); all bit-identical
 #define DEC1_OCC 4
 #endif
+#ifndef DEC2_Q16
+#define DEC2_Q16 0         // stage 2 (f16x3, LR-projection inputs) by k_dec2q: 16 pixels per wave, four waves per SIMD
+#endif
 #ifndef DEC2_WPE
 #define DEC2_WPE 2         // waves per SIMD k_dec2 is register-budgeted for (2 workgroups/CU, 80 KB LDS each)
 #endif

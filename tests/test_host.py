@@ -111,6 +111,43 @@ def test_pack_dec_mlp_tile_layout(stif, sd):
     assert np.array_equal(mlp[0:64], (30.0 * arrs["feat_imnet."][0][:, 198].astype(np.float64)).astype(np.float32))
 
 
+def test_pack_dec_mlp_q16_tiles(stif, sd):
+    """The f16x3 decoder packing's 16x16x32 copies of encode_imnet's tiles (dec_layout.h Q_*, read by k_dec2q):
+    tile (ot, kt) as [s][plane][lane][8 halves], lane l holding W[32 ot + 16 s + (l & 15)][32 kt + 16 (e >> 2)
+    + 4 (l >> 4) + (e & 3)] x 2^10 split into fp16 h + l; sine layers in revolutions (omega_0 / 2 pi)."""
+    L = stif._lib
+    lib = L.lib()
+    arrs = {}
+    for p, n in (("feat_imnet.", 3), ("flow_imnet.", 3), ("encode_imnet.", 4)):
+        a = []
+        for i in range(n):
+            a += [sd[f"{p}net.{i}.linear.weight"], sd[f"{p}net.{i}.linear.bias"]]
+        a += [sd[f"{p}net.{n}.weight"], sd[f"{p}net.{n}.bias"]]
+        arrs[p] = [np.ascontiguousarray(x) for x in a]
+    ptr = lambda a: (L._P * len(a))(*[x.ctypes.data for x in a])
+    mlp = np.empty(lib.stif_dec_mlp_floats(), np.float32)
+    L.check(lib.stif_pack_dec_mlp_ex(ptr(arrs["feat_imnet."]), ptr(arrs["flow_imnet."]), ptr(arrs["encode_imnet."]),
+                                     mlp.ctypes.data, L.CONV_F16X3), "pack")
+    T = 1024
+    q_end = mlp.size
+    q_w3 = q_end - 64 * T
+    q_w2 = q_w3 - 16 * T
+    q_w0 = q_w2 - 4 * T - 8 * T
+    rev = 30.0 / (2 * np.pi)
+    lanes = np.arange(64)
+    for base, W, kts, (ot, kt) in ((q_w3, arrs["encode_imnet."][6], 8, (3, 5)), (q_w2, arrs["encode_imnet."][4], 2, (6, 1)),
+                                   (q_w0, arrs["encode_imnet."][0], 4, (1, 3))):
+        t = mlp[base + (ot * kts + kt) * T:base + (ot * kts + kt + 1) * T].view(np.float16).astype(np.float64)
+        t = t.reshape(2, 2, 64, 8)
+        val = (t[:, 0] + t[:, 1]) / 1024.0                       # [s][lane][e]
+        for s_ in range(2):
+            for e in range(8):
+                rows = 32 * ot + 16 * s_ + (lanes & 15)
+                cols = 32 * kt + 16 * (e >> 2) + 4 * (lanes >> 4) + (e & 3)
+                want = rev * W[rows, cols].astype(np.float64)
+                assert np.abs(val[s_, :, e] - want).max() <= 2e-6 * np.abs(want).max() + 1e-12
+
+
 def test_decoder_tables_match_reference_nearest(stif, golden):
     g = golden["ops"]
     for (h, w, hh, ww) in [(16, 20, 40, 50), (24, 32, 60, 80), (135, 240, 337, 600), (32, 32, 128, 128),
