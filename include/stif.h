@@ -327,7 +327,8 @@ int stif_pack_dec_mlp(const float* const* feat, const float* const* flow, const 
 /* flags = STIF_CONV_F16X3: every 32x32 MFMA weight tile as a split-fp16 tile ([m 2][plane h|l][lane 64]
  * [8 halves] of W * 2^10, element e of half-tile m = feature F(8m + e, lane >> 5)) and the image tiles
  * scaled by 2^14, and the sine layers scaled by omega_0 / (2 pi) (revolutions: the stages evaluate
- * v_sin_f32(x - rint(x))), for stif_dec_stage1_ex / stif_dec_stage2_ex with the same flag. */
+ * v_sin_f32(x - rint(x))), for stif_dec_stage1_ex / stif_dec_stage2_ex with the same flag; encode_imnet's
+ * tiles are also stored a second time as 16x16x32 A operands for the 16-pixel stage 2 (dec_layout.h Q_*). */
 int stif_pack_dec_mlp_ex(const float* const* feat, const float* const* flow, const float* const* enc,
                          float* dst, int flags);
 

@@ -61,7 +61,10 @@ static_assert(DCNSEP_EXP == 0 || DCNSEP_EXP == 1 || DCNSEP_EXP == 3 || DCNSEP_EX
 #define DEC1_OCC 4
 #endif
 #ifndef DEC2_Q16
-#define DEC2_Q16 0         // stage 2 (f16x3, LR-projection inputs) by k_dec2q: 16 pixels per wave, four waves per SIMD
+// stage 2 (f16x3, LR-projection inputs) by k_dec2q: 16 pixels per wave, 4-wave workgroups, four per CU (40 KB
+// LDS, 128 VGPRs); C2 stage 2 17.55-17.79 -> 17.32-17.34 ms (r04_dec2q4_ab.log).  0 = k_dec2 (also the
+// fp32 and high-resolution-image stages)
+#define DEC2_Q16 1
 #endif
 #ifndef DEC2_WPE
 #define DEC2_WPE 2         // waves per SIMD k_dec2 is register-budgeted for (2 workgroups/CU, 80 KB LDS each)
