@@ -234,9 +234,9 @@ STIF_DEV f32x4 img_sample(const float* __restrict__ I, const Bilin& b, int hf) {
 // (a few 4-KB tiles: one layer, or one output tile's K-tiles) is LDS-DMA'd while the previous one
 // is being consumed (double-buffered, one barrier per segment), and every wave reads its A
 // operands from LDS -- one tile feeds 16 MFMAs in each wave of the workgroup.
-// waves per workgroup of k_dec1: 4-wave workgroups, 3 per CU (DEC1_OCC: 52 KB LDS and <= 168 VGPRs each):
-// the waves sharing a SIMD come from different workgroups, so one's segment barrier, gather or sin
-// stretch overlaps the others' MFMAs
+// waves per workgroup of k_dec1: 4-wave workgroups, DEC1_OCC per CU -- by default 4 (36 KB LDS, <= 128 VGPRs
+// each; the HRIMG variants stay at 3: 52 KB, <= 168, and MODE 2 at 2: 69 KB): the waves sharing a SIMD come from different
+// workgroups, so one's segment barrier, gather or sin stretch overlaps the others' MFMAs
 constexpr int DEC_NW = DEC1_NW;
 constexpr int DEC2_NW = 4;   // k_dec2: 8 layer-3 accumulator tiles (128 VGPRs) live
 constexpr int SEG = 10;      // max tiles per segment (k_dec2)
@@ -729,17 +729,23 @@ STIF_DEV void tile_q(R32& acc, const float* t, const XQ& x, int lane) {
   }
   __builtin_amdgcn_sched_barrier(0);
 }
-// sin(z * 2^-14 + b) of a register tile whose features start at fb (biases carry omega_0 / 2 pi, pack.cpp)
-STIF_DEV R32 bias_sin_q(const R32& z, const float* __restrict__ b, int q) {
+// this lane's biases of a register tile whose features start at b (they carry omega_0 / 2 pi, pack.cpp)
+STIF_DEV R32 bias_q(const float* __restrict__ b, int q) {
   R32 o;
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const f32x4 bb = ld4(b + 16 * s + 4 * q);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) o.s[s][e] = siren_sin<1>(fmaf(z.s[s][e], ACC_S<1>, bb[e]));
-  }
+  for (int s = 0; s < 2; ++s) o.s[s] = ld4(b + 16 * s + 4 * q);
   return o;
 }
+// sin(z * 2^-14 + b) of a register tile, biases preloaded (bias_q)
+STIF_DEV R32 bias_sin_q(const R32& z, const R32& bb) {
+  R32 o;
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o.s[s][e] = siren_sin<1>(fmaf(z.s[s][e], ACC_S<1>, bb.s[s][e]));
+  return o;
+}
+STIF_DEV R32 bias_sin_q(const R32& z, const float* __restrict__ b, int q) { return bias_sin_q(z, bias_q(b, q)); }
 // bilinear sample of this lane's channels c0 + 32 ot + 16 s + 4 q .. + 3 (ot, s = 0, 1) of an NHWC map
 STIF_DEV void gather_q(R32* dst, const float* __restrict__ base, int stride, int c0, const Bilin& b, int q) {
   const int c = c0 + 4 * q;
@@ -843,6 +849,10 @@ __global__ __launch_bounds__(DEC2Q_NW * 64) __attribute__((amdgpu_waves_per_eu(4
     }
   }
   lds_dma_barrier();
+  // layer-1 biases before the next segment's LDS-DMA: vmcnt counts in issue order, so a bias load issued
+  // after the DMA would wait for the DMA too (as k_dec1 / k_dec2 do)
+  const R32 eb1[2] = {bias_q(mlp + E_B1, q), bias_q(mlp + E_B1 + 32, q)};
+  __builtin_amdgcn_sched_barrier(0);
   // layer-2/3 segment 2 kt + h: h = 0 the W2 rows of tile kt + W3 (ot 0-2, kt), h = 1 W3 (ot 3-7, kt)
   auto seg_l23 = [&](float* dst, int kt, int h) {
     if (h == 0) {
@@ -864,7 +874,7 @@ __global__ __launch_bounds__(DEC2Q_NW * 64) __attribute__((amdgpu_waves_per_eu(4
       acc.s[0] = acc.s[1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) tile_q(acc, B0 + (ot * 2 + kt) * T, xs[kt], lane);
-      x1[ot] = bias_sin_q(acc, mlp + E_B1 + 32 * ot, q);
+      x1[ot] = bias_sin_q(acc, eb1[ot]);
     }
   }
   const XQ x1s[2] = {xq(x1[0]), xq(x1[1])};
@@ -875,12 +885,14 @@ __global__ __launch_bounds__(DEC2Q_NW * 64) __attribute__((amdgpu_waves_per_eu(4
   // segment 2 kt sits in B1, 2 kt + 1 in B0
   auto l23_step = [&](int kt, bool last) {
     lds_dma_barrier();
+    const R32 b2 = bias_q(mlp + E_B2 + kt * 32, q);   // before the DMA (see eb1)
+    __builtin_amdgcn_sched_barrier(0);
     seg_l23(B0, kt, 1);
     R32 acc;
     acc.s[0] = acc.s[1] = f32x4{0.f, 0.f, 0.f, 0.f};
     tile_q(acc, B1, x1s[0], lane);
     tile_q(acc, B1 + T, x1s[1], lane);
-    const XQ h2 = xq(bias_sin_q(acc, mlp + E_B2 + kt * 32, q));
+    const XQ h2 = xq(bias_sin_q(acc, b2));
 #pragma unroll
     for (int ot = 0; ot < 3; ++ot) tile_q(a3[ot], B1 + (2 + ot) * T, h2, lane);
     lds_dma_barrier();

@@ -14,6 +14,11 @@
 #ifndef WINO_OM_SCHED
 #define WINO_OM_SCHED 1    // a scheduling barrier after every k_wino_om B block (keeps the B loads early)
 #endif
+#ifndef WINO_SP
+// f16x3 3x3 convs with in1_mode 0 / 1 and epilogue NONE / LRELU / RELU / RES by the warp-specialized k_wino_sp
+// (wino_sp.hip; bit-identical outputs); 0 = k_wino.  Environment STIF_WINO_SP=0|1 overrides at run time.
+#define WINO_SP 0
+#endif
 #ifndef WINO_EXP
 #define WINO_EXP 0         // probes: 1 no LDS-DMA after the first phase, 2 no B refills, 3 no output exchange
 #endif
@@ -69,3 +74,5 @@ static_assert(DCNSEP_EXP == 0 || DCNSEP_EXP == 1 || DCNSEP_EXP == 3 || DCNSEP_EX
 #ifndef DEC2_WPE
 #define DEC2_WPE 2         // waves per SIMD k_dec2 is register-budgeted for (2 workgroups/CU, 80 KB LDS each)
 #endif
+static_assert(DEC1_OCC >= 2 && DEC1_OCC <= 4, "DEC1_OCC: k_dec1 is laid out for 2, 3 or 4 workgroups per CU");
+static_assert(DEC2_Q16 == 0 || DEC2_Q16 == 1, "DEC2_Q16: 0 (k_dec2) or 1 (k_dec2q)");

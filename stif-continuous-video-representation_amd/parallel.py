@@ -38,7 +38,14 @@ def shard_for_rank(num_frames: int, world: int, rank: int) -> Tuple[int, int]:
     return pair_shards(num_frames, world)[rank]
 
 
-_WARM = set()
+# process-group objects already warmed.  Held by reference and compared by identity: a group destroyed and
+# re-created (destroy_process_group + init_process_group) is a new object and is warmed again, and an id()
+# cannot be reused by a later group while its object is held here.
+_WARM: list = []
+
+
+def _group_object(group):
+    return group if group is not None else dist.distributed_c10d._get_default_group()
 
 
 def warm_group(group=None):
@@ -46,11 +53,13 @@ def warm_group(group=None):
     also one whose shard is empty and that never enters the exchange -- takes part, so a lazily
     initialised NCCL communicator exists before the first ``batch_isend_irecv`` whatever the caller's
     ``init_process_group`` did (no ``device_id`` needed)."""
-    key = id(group) if group is not None else None
-    if key in _WARM or not dist.is_initialized():
+    if not dist.is_initialized():
+        return
+    g = _group_object(group)
+    if any(w is g for w in _WARM):
         return
     dist.barrier(group)
-    _WARM.add(key)
+    _WARM.append(g)
 
 
 def halo_exchange(first_frame_feats: Sequence[torch.Tensor], rank: int, world: int, group=None,

@@ -1,4 +1,4 @@
-"""Full-size decodes pinned to the oracle at sampled pixels (BASELINE configs C2 and C4).
+"""Full-size decodes pinned to the oracle at sampled pixels (BASELINE configs C2, C3 and C4).
 
 The engine's latent at 540x960 (C2, 4x, 3 t) and 1080x1920 (C4, 2.5x -> 2700x4800, 4 t) is decoded
 on the GPU over the whole frame; the oracle's pixel-subset decoder (``decoding_at``: the reference
@@ -7,6 +7,9 @@ the same latent at ~4,096 HR pixels: random ones, the first and last row and col
 flows clamp the warped grid), and -- at 2.5x -- the rows and columns whose nearest LR index is a
 round-half-even tie.  Elementwise |gpu - oracle| <= 1e-4 |oracle| + 1e-6 (north star rtol 1e-4), so
 the full-size decoder is pinned to the reference arithmetic, not only to the other operand mode.
+C3 decodes a whole 9-frame 720p window (8 pairs) and pins its LAST pair: item 7's HRfeat starts
+7 x 2880 x 5120 x 64 x 4 B = 26 GB into the buffer, beyond 2^32 bytes, so the decoder's 64-bit item
+offsets are checked against the oracle too (missing 4).
 The encoder at these sizes is covered by test_gpu_configs (f16x3 vs fp32) and, at sizes the oracle
 runs in seconds, by the reference fixtures.
 """
@@ -61,6 +64,7 @@ def pick_pixels(HH, WW, H, W, n=4096, seed=0):
 CASES = {
     # frames, H, W, output size (None = 4x), times
     "C2": (3, 540, 960, None, [0.25, 0.5, 0.75]),
+    "C3": (9, 720, 1280, None, [0.0, 0.5]),
     "C4": (2, 1080, 1920, (2700, 4800), [0.0, 0.25, 0.5, 0.75]),
 }
 
@@ -71,6 +75,11 @@ def test_full_size_decode_matches_oracle_at_pixels(stif, sd, cfg):
     HH, WW = size or (4 * H, 4 * W)
     m = stif.LunaTokis(64, 6, 8, 5, 40)
     m.load_state_dict(sd, strict=True)
+    if cfg == "C3":
+        # one decode pass over all 8 items (the default dec_chunk_px would split them 2 per pass), so the
+        # HRfeat / flow scratch holds the whole window and item 7 sits 26 GB (> 2^32 B) into it
+        m.dec_chunk_px = (F_ - 1) * HH * WW
+        assert (F_ - 2) * HH * WW * 64 * 4 > 2 ** 32
     fr = synth(0, F_, H, W)
     with torch.no_grad():
         m.gen_feat_window(fr)
@@ -78,7 +87,7 @@ def test_full_size_decode_matches_oracle_at_pixels(stif, sd, cfg):
     py, px, nty, ntx = pick_pixels(HH, WW, H, W)
     if size is not None:
         assert nty > 0 and ntx > 0          # 1080 -> 2700 and 1920 -> 4800 both have ties
-    b = F_ - 2                              # the last pair of the window
+    b = F_ - 2                              # the last pair of the window (C3: item 7, past 2^32 bytes of HRfeat)
     feat = m.feat[b:b + 1].cpu().numpy()    # [1,3,64,H,W], a strided view of the NHWC latent
     x = m.inp[b:b + 1].cpu().numpy()
     st = {}

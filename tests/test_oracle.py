@@ -228,3 +228,30 @@ def test_c1_pin_fixture_is_consistent():
     for i in range(2):
         fr = torch.rand(3, 256, 256, generator=torch.Generator().manual_seed(1234 + i)).numpy()
         assert np.array_equal(g["x"][0, i], fr)
+
+
+def test_chunked_dcn_shim_equals_unchunked_and_oracle():
+    """the C2 / C3 / C4 latent fixtures come from make_golden's row-chunked CPU DCN shim.  Its
+    equality with the unchunked shim (which the model fixtures use) was only printed by `make_golden.py
+    chunk-check`; here it is asserted on that case (offsets up to 6 px, 150 rows in 32-row blocks incl. a
+    partial one and both image edges), and both shims are checked against the oracle's restatement."""
+    import importlib.util
+    import torch
+    here = os.path.dirname(os.path.abspath(__file__))
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(here, "golden", "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    g = torch.Generator().manual_seed(5)
+    B, C, H, W, dg = 1, 16, 150, 40, 2
+    inp = torch.randn(B, C, H, W, generator=g)
+    wt = torch.randn(8, C, 3, 3, generator=g)
+    bs = torch.randn(8, generator=g)
+    off = torch.rand(B, 2 * dg * 9, H, W, generator=g) * 12 - 6
+    m = torch.rand(B, dg * 9, H, W, generator=g)
+    a = mg.dcn_v2_forward_cpu(inp, wt, bs, off, m, 3, 3, 1, 1, 1, 1, 1, 1, dg)
+    b = mg.dcn_v2_forward_cpu_chunked(inp, wt, bs, off, m, 3, 3, 1, 1, 1, 1, 1, 1, dg, rows=32)
+    scale = float(a.abs().max())
+    assert float((a - b).abs().max()) <= 1e-6 * scale
+    ref = O.dcn_v2_forward(inp.numpy().astype(np.float64), wt.numpy().astype(np.float64), bs.numpy().astype(np.float64),
+                           off.numpy(), m.numpy(), 3, 3, 1, 1, 1, 1, 1, 1, dg)
+    assert np.abs(b.numpy() - ref).max() <= 1e-5 * scale

@@ -158,6 +158,48 @@ def _shard_worker(rank, world, port, nframes, outdir):
     dist.destroy_process_group()
 
 
+def _reinit_worker(rank, world, ports, nframes, outdir):
+    """init -> gen_feat_shard -> destroy -> init again -> gen_feat_shard, every rank incl. an empty shard:
+    the re-created default group is a new group and must get its own warm-up barrier."""
+    import stif_pkg
+    P = stif_pkg.load().parallel
+    shards = P.pair_shards(nframes, world)
+    a, b = shards[rank]
+    frames = torch.arange(a, b, dtype=torch.float32).view(-1, 1, 1, 1).repeat(1, 3, 2, 2) if b > a else None
+    calls = []
+    real_barrier = dist.barrier
+
+    def counting_barrier(group=None, **kw):
+        calls.append(1)
+        return real_barrier(group, **kw)
+
+    dist.barrier = counting_barrier
+    try:
+        for port in ports:                 # a fresh rendezvous port per cycle (rank 0's store is torn down)
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+            n0 = len(calls)
+            P.gen_feat_shard(_FakeModel(a), frames, rank, world, shards=shards, exchange=True)
+            P.gen_feat_shard(_FakeModel(a), frames, rank, world, shards=shards, exchange=True)
+            np.save(os.path.join(outdir, f"b{rank}_{len(P._WARM)}.npy"), np.array([len(calls) - n0]))
+            real_barrier()
+            dist.destroy_process_group()
+    finally:
+        dist.barrier = real_barrier
+
+
+def test_warm_group_after_reinit():
+    """warm_group's cache must not treat a re-initialised default group as warmed (an empty-shard
+    rank would then skip the barrier that creates a lazy NCCL communicator, and the first exchange could
+    hang).  Each of the two init/destroy cycles runs exactly one warm-up barrier per rank."""
+    world, nframes = 3, 3      # rank 2 has an empty shard
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_reinit_worker, args=(world, (_free_port(), _free_port()), nframes, d), nprocs=world, join=True)
+        for r in range(world):
+            for k in (1, 2):
+                assert np.load(os.path.join(d, f"b{r}_{k}.npy")).tolist() == [1], (r, k)
+
+
 @pytest.mark.parametrize("nframes,world", [(3, 4), (9, 8)], ids=["empty_shards", "c4_plan"])
 def test_gen_feat_shard_all_ranks(nframes, world):
     """gen_feat_shard called by every rank (bench.py's step): ranks with frames get their window's
