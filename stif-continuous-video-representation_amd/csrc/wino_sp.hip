@@ -6,21 +6,23 @@
 // chain of its transform row (LDS-DMA wait -> halo reads -> input transform -> operand split -> MFMAs ->
 // output-transform exchange) and runs two 4-wave workgroups per CU; its waves are instruction-latency-bound
 // (issue 44 %, MFMA-busy 0.20).  Here one 8-wave workgroup per CU runs
-//   * 4 T-waves (waves 0-3, transform row i = wave): LDS-DMA of the 16-channel halo phases, input transform and
-//     operand split of row i, written to LDS as the ready MFMA A fragments of that row (a 32-KB slot per
-//     16-channel pair: [row i][j][plane][lane][16 B], consecutive lanes, conflict-free);
-//   * 4 M-waves (waves 4-7, row i = wave - 4): A fragments from the slot, B fragments from L2 in k_wino's
-//     register ring, 24 MFMAs per pair, and the output-transform exchange -- written after a tile's last pair
-//     and read back, combined and stored during the next tile's first pair, beside its MFMAs.
+//   * 4 T-waves (waves 0-3, transform row i = wave): staging of the 16-channel halo phases (global loads four
+//     pairs ahead in registers, then ds_write into one of two image buffers), the input transform of row i,
+//     written to LDS in fp32 in the lane order of the MFMA A fragments (a 32-KB slot per 16-channel pair:
+//     [row i][j][chunk][lane][16 B], consecutive lanes, conflict-free), and the output side of the exchange
+//     (read back, combined with bias / residual, activation, stores);
+//   * 4 M-waves (waves 4-7, row i = wave - 4): the A operands from the slot, split to f16 hi/lo beside the
+//     MFMAs, B fragments from L2 in k_wino's register ring, 24 MFMAs per pair, and the input side of the
+//     output-transform exchange after a tile's last pair.
 // One T-wave and one M-wave share each SIMD, so the transform's VALU stream issues beside the other wave's MFMAs.
 // The two roles run one pair apart in lock step: step n = M consumes pair n from slot n & 1 while T transforms
-// pair n + 1 into slot (n + 1) & 1 and DMAs pair n + 2 into staging buffer n & 1; one workgroup barrier per step.
+// pair n + 1 into slot (n + 1) & 1 and writes pair n + 2 into staging buffer n & 1; one workgroup barrier per step.
 //
 // Staging image of a 16-channel phase: [halo row 6][column slot 34][16-B chunk 4], even columns in slots 0-16,
 // odd ones in 17-33 (k_wino's col_slot), no padding: chunk c of slot S sits at position c ^ ((S >> 2) & 3), so
-// the 16 lanes of a ds_read_b128 group (16 consecutive slots, one chunk) hit 16 distinct bank quads.  The LDS-DMA
-// writes 64 consecutive positions per instruction; the swizzle is applied on the source side (lane p fetches
-// the chunk that belongs at position p).
+// the 16 lanes of a ds_read_b128 group (16 consecutive slots, one chunk) hit 16 distinct bank quads.  A staging
+// store writes 64 consecutive positions per wave instruction; the swizzle is applied on the source side (lane p
+// loads the chunk that belongs at position p).
 //
 // LDS: 2 staging buffers (13 KB) + 2 A slots (32 KB) + the exchange (2 x 32 KB) = 154 KB: one workgroup per CU,
 // two waves per SIMD (<= 256 VGPRs).
@@ -31,6 +33,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 namespace {
 
@@ -38,8 +41,8 @@ constexpr int WR = 4;                      // output rows per tile
 constexpr int HC = 34;                     // halo columns
 constexpr int RP = HC * 4;                 // 16-B chunks per staged halo row (136 = 0 mod 8)
 constexpr int IMG = 6 * RP;                // chunks of a staged 16-channel phase (816)
-constexpr int DMA_INS = (IMG + 63) / 64;   // 13 LDS-DMA instructions per phase (the last partly zero-fill)
-constexpr int STG_F = DMA_INS * 256;       // floats per staging buffer (13 KB incl. the tail)
+constexpr int ST_INS = (IMG + 63) / 64;    // 13 wave stores per staged phase (the last partly zero-fill)
+constexpr int STG_F = ST_INS * 256;        // floats per staging buffer (13 KB incl. the tail)
 constexpr int A_F = 8192;                  // floats per A slot: [i 4][j 4][plane 2][lane 64][4]
 constexpr int EX_F = 8192;                 // floats per exchange round (k_wino's [wave][b][32 tiles][32 co])
 constexpr int OFF_STG = 0, OFF_A = 2 * STG_F, OFF_EX = OFF_A + 2 * A_F;
@@ -49,28 +52,63 @@ static_assert(LDS_F * 4 <= 160 * 1024 && RP % 8 == 0, "k_wino_sp LDS map");
 STIF_DEV int col_slot(int c) { return (c & 1) ? 17 + (c >> 1) : (c >> 1); }
 STIF_DEV int slot_col(int s) { return s < 17 ? 2 * s : 2 * (s - 17) + 1; }
 
+// a tile's coordinates and its item's base pointers, all wave-uniform (SGPRs): the kernel-argument pointer
+// arrays are read once per tile by scalar loads -- indexed by a VGPR they became vector loads whose use
+// waited for vmcnt(0), i.e. for every B-operand / staging load in flight
 struct Tile {
   int oy0, ox0, slice, g, n;
+  const float* src0;   // T: the item's in0 / in1 maps
+  const float* src1;
+  float* out;          // M: the item's output, residual, bias and packed weights of its slice
+  const float* res;
+  const float* bias;
+  const float* w;
 };
+STIF_DEV int sgpr(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// a bare workgroup barrier: __syncthreads()'s fence would wait for vmcnt(0), i.e. also for the M-waves'
-// B-operand loads that stay in flight across it.  LDS writes are complete (lgkmcnt) before it, LDS-DMA
-// (T-waves) by the explicit vmcnt wait.
+// a bare workgroup barrier: __syncthreads()'s fence would wait for vmcnt(0), i.e. also for the B-operand and
+// staging loads that stay in flight across it.  LDS writes are complete (lgkmcnt) before it.
 STIF_DEV void bar_lds() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }
-STIF_DEV void bar_dma() {
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
+
+#if WINO_SP_TRACE
+// timing probe (tools/r5/sp_trace.py): per workgroup 0-7, wave and step, the s_memtime after the step's
+// barrier and before the next one; every lane stores to its own address (vector stores)
+__device__ unsigned long long* g_sp_trace;
+constexpr int TR_STEPS = 96;
+// unconditional buffer stores (out-of-range offset past workgroup 7 / step TR_STEPS: dropped), so the
+// compiler's vmcnt bookkeeping sees the same count on every path
+#define SP_STAMP(slot)                                                                                  \
+  do {                                                                                                  \
+    const int sl_ = (slot);                                                                             \
+    const bool ok_ = blockIdx.x < 8 && sl_ < 2 * TR_STEPS;                                              \
+    const unsigned vo_ = ok_ ? (unsigned)(((blockIdx.x * 8 + wv) * 2 * TR_STEPS + sl_) * 64 + lane) * 8u \
+                             : 0x80000000u;                                                             \
+    const unsigned long long tm_ = __builtin_amdgcn_s_memtime();                                        \
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, tm_), \
+                                          trs, vo_, 0, 0);                                              \
+  } while (0)
+#else
+#define SP_STAMP(slot) \
+  do {                 \
+  } while (0)
+#endif
 
 template <int IN1, int EPI>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_wino_sp(stif_conv_args a,
                                                                                         int ntiles) {
+  // 64 input channels (IN1 = 0) or 64 | 64 (IN1 = 1): 4 or 8 16-channel pairs per tile (host-checked), so every
+  // step of a tile is straight-line code with its role known at compile time
+  constexpr int NPR = IN1 ? 8 : 4;
+  constexpr bool RES = EPI == STIF_EPI_RES;
   __shared__ __attribute__((aligned(16))) float smem[LDS_F];
+#if WINO_SP_TRACE
+  const __amdgpu_buffer_rsrc_t trs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)g_sp_trace, (short)0, 8 * 8 * 2 * TR_STEPS * 64 * 8, 0x00020000);
+#endif
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -83,22 +121,28 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
   const int tiles_x = (a.Wo + 31) >> 5;
   const int tiles_y = (a.Ho + WR - 1) / WR;
   const int slices = (a.cout + 63) >> 6;
-  const int H = a.H, W = a.W, C0 = a.C0, C1 = a.C1;
-  const int NC = (C0 >> 3) + (IN1 ? (C1 >> 3) : 0);   // 8-channel chunks
-  const int NPR = NC >> 1;                             // 16-channel pairs per tile (host: C0, C1 % 16 == 0)
+  const int H = a.H, W = a.W;
+  constexpr int NC = 2 * NPR;                 // 8-channel chunks
 
   auto tile_of = [&](int T) {
     Tile t;
-    t.slice = T % slices;
+    T = sgpr(T);
+    t.slice = sgpr(T % slices);
     int r = T / slices;
     const int x = r % tiles_x;
     r /= tiles_x;
     const int y = r % tiles_y;
     r /= tiles_y;
-    t.g = r / a.nitems;
-    t.n = r - t.g * a.nitems;
-    t.oy0 = y * WR;
-    t.ox0 = x * 32;
+    t.g = sgpr(r / a.nitems);
+    t.n = sgpr(r - t.g * a.nitems);
+    t.oy0 = sgpr(y * WR);
+    t.ox0 = sgpr(x * 32);
+    t.src0 = a.in0[t.g] + (size_t)t.n * a.in0_item;
+    t.src1 = IN1 ? a.in1[t.g] + (size_t)t.n * a.in1_item : t.src0;
+    t.out = a.out[t.g] + (size_t)t.n * a.out_item;
+    t.res = RES ? a.res[t.g] + (size_t)t.n * a.res_item : t.src0;
+    t.bias = a.bias[t.g] + t.slice * 64;
+    t.w = a.w[t.g] + (size_t)t.slice * NC * 8192;
     return t;
   };
 
@@ -109,38 +153,49 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
   const int T0 = xcd * per + (blockIdx.x >> 3);
   if (T0 >= tend) return;
   const int ntw = (tend - T0 + nl - 1) / nl;   // tiles of this workgroup
-  const int N = ntw * NPR;                     // pairs of this workgroup
+  const int N = ntw * NPR;                     // pairs (= steps) of this workgroup
+  float* const ex = smem + OFF_EX;
 
   if (is_t) {
-    // =========================================================== T-waves: staging + transform + split
-    // DMA instruction ins = wi + 4 k (k = 0..3, ins < 13): per-lane (halo row, column, source chunk) once
+    // =========================================================== T-waves: staging, transform, split, and the
+    // output side of the exchange
+    if (WINO_SP_TPRIO) __builtin_amdgcn_s_setprio(WINO_SP_TPRIO);
+    // image piece k of this wave (instruction wi + 4 k < 13): per-lane (halo row, column, source chunk) once
     int dr[4], dc[4], dq[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int p = (wi + 4 * k) * 64 + lane;
       const int r = p / RP, rem = p - RP * (p / RP), s = rem >> 2;
-      dr[k] = p < IMG ? r : 1 << 20;   // fails the row range test: zero fill of the tail
+      dr[k] = p < IMG ? r : 1 << 20;   // fails the row range test: zero fill of the tail (and no load at all
+                                       // for the pieces of a fourth instruction that does not exist)
       dc[k] = slot_col(s < HC ? s : 0);
       dq[k] = (rem & 3) ^ ((s >> 2) & 3);
     }
-    auto stage = [&](const Tile& t, int q, int buf) {
-      const bool second = IN1 && 16 * q >= C0;
-      const float* src = (second ? a.in1[t.g] + (size_t)t.n * a.in1_item : a.in0[t.g] + (size_t)t.n * a.in0_item);
-      const int Cs = second ? C1 : C0;
-      const int cbase = second ? 16 * q - C0 : 16 * q;
+    // staging through registers: lane p of load k fetches the 16 B that belong at image position
+    // (wi + 4 k) * 64 + p (out-of-image pixels and the tail read as zeros: the conv padding), four pairs ahead
+    // of their ds_write into the staging image -- an LDS-DMA into one of two image buffers had one step, and
+    // its ~1 us issue-to-landed time set the step
+    auto load_pair = [&](const Tile& t, int q, f32x4 (&dst)[4]) {
+      const bool second = IN1 && q >= 4;
+      const float* src = second ? t.src1 : t.src0;
+      const int cbase = 16 * (second ? q - 4 : q);
       const __amdgpu_buffer_rsrc_t rs =
-          __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, (int)((size_t)H * W * Cs * 4), 0x00020000);
-      const unsigned cs4 = (unsigned)Cs * 4u;
+          __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, (int)((size_t)H * W * 256), 0x00020000);
+      // four loads on every wave (waves 1-3 have three image pieces: their fourth reads out of range, i.e.
+      // nothing), so the per-wave vmcnt bookkeeping is the same on every path
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const int ins = wi + 4 * k;   // wave-uniform
-        if (ins < DMA_INS) {
-          const int y = t.oy0 - 1 + dr[k], x = t.ox0 - 1 + dc[k];
-          const unsigned off = __umul24((unsigned)(y * W + x), cs4) + (unsigned)(cbase + 4 * dq[k]) * 4u;
-          const unsigned voff = (((unsigned)y < (unsigned)H) & ((unsigned)x < (unsigned)W)) ? off : 0x80000000u;
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, smem + OFF_STG + buf * STG_F + ins * 256, 16, voff, 0, 0, 0);
-        }
+        const int y = t.oy0 - 1 + dr[k], x = t.ox0 - 1 + dc[k];
+        const unsigned off = __umul24((unsigned)(y * W + x), 256u) + (unsigned)(cbase + 4 * dq[k]) * 4u;
+        const unsigned voff = (((unsigned)y < (unsigned)H) & ((unsigned)x < (unsigned)W)) ? off : 0x80000000u;
+        dst[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 0));
       }
+    };
+    auto write_pair = [&](const f32x4 (&v)[4], int buf) {
+      float* dst = smem + OFF_STG + buf * STG_F + lane * 4;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (wi + 4 * k < ST_INS) st4(dst + (wi + 4 * k) * 256, v[k]);
     };
     // transform row i of the phase in buffer `buf` (k_wino's xread / xform): rows rA, rB of each 4x4 patch
     const int rA = (wi == 0) ? 0 : (wi == 2 ? 2 : 1);
@@ -155,13 +210,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
       ro[2 * m + 1] = ((2 * tyl + rB) * RP + 4 * S + (hf ^ x)) * 4;
       rdel[m] = ((2 + hf) ^ x) * 4 - (hf ^ x) * 4;
     }
-    auto xread = [&](const float* buf, int s, f32x4* rd) {
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        rd[2 * m] = ld4(buf + ro[2 * m] + s * rdel[m]);
-        rd[2 * m + 1] = ld4(buf + ro[2 * m + 1] + s * rdel[m]);
-      }
-    };
     auto xform = [&](const f32x4* rd, f32x4* v) {
       const f32x4 t0 = rd[0] + sB * rd[1];
       const f32x4 t1 = rd[2] + sB * rd[3];
@@ -174,53 +222,153 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
     };
     auto transform = [&](int stg, int slot) {
       const float* buf = smem + OFF_STG + stg * STG_F;
-      f32x4 rd[8], va[4], vb[4];
-      xread(buf, 0, rd);
-      xform(rd, va);
-      xread(buf, 1, rd);
-      xform(rd, vb);
+      f32x4 rd[2][8], va[4], vb[4];
+#pragma unroll
+      for (int c = 0; c < 2; ++c)   // all 16 reads in flight at once: one LDS latency per step
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          rd[c][2 * m] = ld4(buf + ro[2 * m] + c * rdel[m]);
+          rd[c][2 * m + 1] = ld4(buf + ro[2 * m + 1] + c * rdel[m]);
+        }
+      xform(rd[0], va);
+      xform(rd[1], vb);
       float* dst = smem + OFF_A + slot * A_F + (wi * 8) * 256 + lane * 4;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        f16x8 ah, al;
-        split_f16x3(va[j], vb[j], ah, al);
-        st4(dst + (2 * j) * 256, __builtin_bit_cast(f32x4, ah));
-        st4(dst + (2 * j + 1) * 256, __builtin_bit_cast(f32x4, al));
+        if (WINO_SP_MSPLIT) {
+          // the transformed values in fp32 ([i][j][chunk a|b][lane][4]); the M wave splits them
+          st4(dst + (2 * j) * 256, va[j]);
+          st4(dst + (2 * j + 1) * 256, vb[j]);
+        } else {
+          // the split A fragments ([i][j][plane h|l][lane][8 halves])
+          f16x8 ah, al;
+          split_f16x3(va[j], vb[j], ah, al);
+          st4(dst + (2 * j) * 256, __builtin_bit_cast(f32x4, ah));
+          st4(dst + (2 * j + 1) * 256, __builtin_bit_cast(f32x4, al));
+        }
       }
     };
-    // the tile of the pair being staged (pair n lies in tile n / NPR of this workgroup's list), cached
-    int ks = 0;
-    Tile ts = tile_of(T0);
+
+    // ---- the exchange's output side (k_wino's reader): thread tid = (cout quad c4, column oxl), rows k
+    const int c4 = tid & 7, oxl = (tid >> 3) & 31;
+    const int bb = oxl & 1, txo = oxl >> 1;
+    bool live = false;   // a real exchange is pending (the first tile's first steps have none)
+    auto voff = [&](const Tile& t, int nt, int k, bool on) -> unsigned {
+      const int oy = t.oy0 + k, ox = t.ox0 + oxl;
+      const int co = t.slice * 64 + nt * 32 + c4 * 4;
+      const bool ok = (oy < a.Ho) & (ox < a.Wo) & on;
+      return ok ? (unsigned)(((oy * a.Wo + ox) * a.cout + co) * 4) : 0x80000000u;
+    };
+    const int slab = (int)((size_t)a.Ho * a.Wo * a.cout * 4);
+    f32x4 rv[2][4], bv[2];   // the residual and bias of the tile whose exchange comes next
+    auto load_out = [&](const Tile& t) {
+      bv[0] = ld4(t.bias + c4 * 4);
+      bv[1] = ld4(t.bias + 32 + c4 * 4);
+      if (RES) {
+        const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void*)t.res, (short)0, slab, 0x00020000);
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            rv[nt][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, voff(t, nt, k, true), 0, 0));
+      }
+    };
+    // round nt of tile t's exchange: combine the four rows' P, bias (+ residual), activation, store
+    auto ex_read = [&](const Tile& t, int nt) {
+      const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)t.out, (short)0, slab, 0x00020000);
+      float chk = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float* rbase =
+            ex + nt * EX_F + (bb * 32 + (txo ^ (((txo >> 2) ^ bb) & 1))) * 32 + c4 * 4 + (k >> 1) * 512;
+        const f32x4 p1 = ld4(rbase + 1 * 2048), p2 = ld4(rbase + 2 * 2048);
+        const f32x4 pe = ld4(rbase + ((k & 1) ? 3 : 0) * 2048);
+        f32x4 y = (k & 1) ? (p1 - p2 - pe) : (pe + p1 + p2);
+        y = y * F16X3_UNSCALE + bv[nt];   // exact power of two
+        chk += live ? (y[0] + y[1]) + (y[2] + y[3]) : 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (EPI == STIF_EPI_LRELU) y[e] = lrelu01(y[e]);
+          if (EPI == STIF_EPI_RELU) y[e] = fmaxf(y[e], 0.f);
+        }
+        if (RES) y += rv[nt][k];
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, y),
+                                               ro, voff(t, nt, k, live), 0, 0);
+      }
+      report_range(a.status, not_finite(chk));
+    };
+
+    // tiles: tc = the tile being transformed / exchanged, tl_ = the tile of the pair being loaded (cached)
+    int kl = 0;
+    Tile tld = tile_of(T0);
     auto tile_at = [&](int k) -> const Tile& {
-      if (k != ks) {
-        ks = k;
-        ts = tile_of(T0 + k * nl);
+      if (k != kl) {
+        kl = k;
+        tld = tile_of(T0 + k * nl);
       }
-      return ts;
+      return tld;
     };
-    // step -2: pairs 0 and 1 to the staging buffers
-    stage(ts, 0, 0);
-    if (N > 1) stage(tile_at(1 / NPR), 1 % NPR, 1);
-    bar_dma();
+    // register ring: pair p's staging data in pf[p % 4] from its load (step p - 6) to its write (step p - 2)
+    f32x4 pf[4][4], p0[4], p1[4];
+    // unconditional (past the last pair: the last pair again), so the compiler's vmcnt accounting stays exact
+    auto load_n = [&](int p, f32x4 (&dst)[4]) {
+      p = min(p, N - 1);
+      load_pair(tile_at(p / NPR), p % NPR, dst);
+    };
+    load_n(0, p0);
+    load_n(1, p1);
+#pragma unroll
+    for (int p = 2; p < 6; ++p) load_n(p, pf[p & 3]);
+    // step -2: pairs 0 and 1 into the staging buffers
+    write_pair(p0, 0);
+    if (N > 1) write_pair(p1, 1);
+    bar_lds();
     // step -1: transform pair 0
     transform(0, 0);
-    bar_dma();
-    // step n: stage pair n + 2 (buffer n & 1: pair n's, transformed in step n - 1), transform pair n + 1
-    for (int n = 0; n < N; ++n) {
-      if (n + 2 < N) stage(tile_at((n + 2) / NPR), (n + 2) % NPR, n & 1);
-      if (n + 1 < N) transform((n + 1) & 1, (n + 1) & 1);
-      bar_dma();
+    bar_lds();
+    Tile tc = tile_of(T0), tprev = tc;
+    int n = 0;
+    // step n = k NPR + q: write pair n + 2 (buffer n & 1: pair n's, transformed in step n - 1) from the ring,
+    // load pair n + 6 into the freed slot, transform pair n + 1; q = 0 / 1: rounds 0 / 1 of the previous
+    // tile's exchange (written by the M waves in its last step); q = NPR - 2: this tile's bias / residual
+    auto tstep = [&](auto q_) {
+      constexpr int q = decltype(q_)::value;
+      constexpr int s = (q + 2) & 3;
+      SP_STAMP(2 * n);
+      if (n + 2 < N) write_pair(pf[s], n & 1);
+      load_n(n + 6, pf[s]);
+      if (q == NPR - 2) load_out(tc);
+      if (n + 1 < N && WINO_SP_EXP != 2 && WINO_SP_EXP != 4) transform((n + 1) & 1, (n + 1) & 1);
+      if (q < 2) ex_read(tprev, q);
+      SP_STAMP(2 * n + 1);
+      bar_lds();
+      ++n;
+    };
+    for (int k = 0; k < ntw; ++k) {
+      live = k > 0;
+      tstep(std::integral_constant<int, 0>{});
+      tstep(std::integral_constant<int, 1>{});
+      tstep(std::integral_constant<int, 2>{});
+      tstep(std::integral_constant<int, 3>{});
+      if constexpr (NPR == 8) {
+        tstep(std::integral_constant<int, 4>{});
+        tstep(std::integral_constant<int, 5>{});
+        tstep(std::integral_constant<int, 6>{});
+        tstep(std::integral_constant<int, 7>{});
+      }
+      tprev = tc;
+      tc = tile_of(k + 1 < ntw ? T0 + (k + 1) * nl : T0);
     }
+    // the last tile's exchange (the M waves wrote it before the last barrier)
+    live = true;
+    ex_read(tprev, 0);
+    ex_read(tprev, 1);
     return;
   }
 
-  // ============================================================= M-waves: MFMAs + output transform
-  const int mt = tid - 256;                    // 0..255 over the 4 M-waves (exchange reader)
-  auto wbase = [&](const Tile& t) {
-    return a.w[t.g] + (size_t)t.slice * NC * 8192 + wi * 4096 + lane * 4;
-  };
-  int T = T0;
-  Tile cur = tile_of(T);
+  // ============================================================= M-waves: MFMAs + the exchange's input side
+  auto wbase = [&](const Tile& t) { return t.w + wi * 4096 + lane * 4; };
+  Tile cur = tile_of(T0);
   const float* wsl = wbase(cur);
   f16x8 bh[2][2], bl[2][2];
 #pragma unroll
@@ -232,9 +380,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
     }
   bar_lds();   // step -2
   bar_lds();   // step -1
-
-  // ---- exchange (k_wino's): write P_i of both 32-cout halves, read back (pixel, 4-cout) vectors
-  float* const ex = smem + OFF_EX;
+  // P_i of both 32-cout halves into the exchange (k_wino's layout)
   auto ex_write = [&](f32x16 (&acc)[4][2]) {
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
@@ -250,131 +396,77 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
       }
     }
   };
-  constexpr bool RES = EPI == STIF_EPI_RES;
-  const int c4 = mt & 7, oxl = (mt >> 3) & 31;
-  const int bb = oxl & 1, txo = oxl >> 1;
-  auto voff = [&](const Tile& t, int nt, int k) -> unsigned {
-    const int oy = t.oy0 + k, ox = t.ox0 + oxl;
-    const int co = t.slice * 64 + nt * 32 + c4 * 4;
-    const bool ok = (oy < a.Ho) & (ox < a.Wo) & (co < a.cout);
-    return ok ? (unsigned)(((oy * a.Wo + ox) * a.cout + co) * 4) : 0x80000000u;
-  };
-  auto out_rsrc = [&](const Tile& t) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(a.out[t.g] + (size_t)t.n * a.out_item), (short)0,
-                                             (int)((size_t)a.Ho * a.Wo * a.cout * 4), 0x00020000);
-  };
-  auto res_rsrc = [&](const Tile& t) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(RES ? a.res[t.g] + (size_t)t.n * a.res_item : a.in0[t.g]),
-                                             (short)0, (int)((size_t)a.Ho * a.Wo * a.cout * 4), 0x00020000);
-  };
-  // read round nt of the exchange of tile t, add bias (+ residual), activation, store; returns the range sum
-  auto ex_read = [&](const Tile& t, int nt, const f32x4* rv) -> float {
-    const __amdgpu_buffer_rsrc_t ro = out_rsrc(t);
-    const int cob = t.slice * 64 + nt * 32 + c4 * 4;
-    const f32x4 bv = cob < a.cout ? ld4(a.bias[t.g] + cob) : f32x4{0.f, 0.f, 0.f, 0.f};
-    float chk = 0.f;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float* rbase =
-          ex + nt * EX_F + (bb * 32 + (txo ^ (((txo >> 2) ^ bb) & 1))) * 32 + c4 * 4 + (k >> 1) * 512;
-      const f32x4 p1 = ld4(rbase + 1 * 2048), p2 = ld4(rbase + 2 * 2048);
-      const f32x4 pe = ld4(rbase + ((k & 1) ? 3 : 0) * 2048);
-      f32x4 y = (k & 1) ? (p1 - p2 - pe) : (pe + p1 + p2);
-      y = y * F16X3_UNSCALE + bv;   // exact power of two
-      chk += (cob < a.cout) ? (y[0] + y[1]) + (y[2] + y[3]) : 0.f;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (EPI == STIF_EPI_LRELU) y[e] = lrelu01(y[e]);
-        if (EPI == STIF_EPI_RELU) y[e] = fmaxf(y[e], 0.f);
-      }
-      if (RES) y += rv[k];
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, y), ro,
-                                             voff(t, nt, k), 0, 0);
-    }
-    return chk;
-  };
-  auto load_res = [&](const Tile& t, int nt, f32x4* rv) {
-    if (RES) {
-      const __amdgpu_buffer_rsrc_t rr = res_rsrc(t);
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        rv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, voff(t, nt, k), 0, 0));
-    }
-  };
-
   f32x16 acc[4][2];
-  Tile prv = cur;          // the tile whose exchange is pending (valid when pend)
-  bool pend = false;
-  int k_in = 0;            // tile index of pair n within this workgroup's list
-  Tile nxt = tile_of(ntw > 1 ? T + nl : T);
+  int n = 0;
+  Tile nxt = tile_of(ntw > 1 ? T0 + nl : T0);
   const float* wnx = wbase(nxt);
-  for (int n = 0; n < N; ++n) {
-    const int q = n - k_in * NPR;
+  // one pair: A fragments from the slot, 24 MFMAs, the B ring refilled with the blocks two ahead
+  auto mstep = [&](auto q_) {
+    constexpr int q = decltype(q_)::value;
+    SP_STAMP(2 * n);
     const float* As = smem + OFF_A + (n & 1) * A_F + (wi * 8) * 256 + lane * 4;
-    f32x4 rv[2][4];
     if (q == 0) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int u = 0; u < 2; ++u) acc[j][u] = f32x16{0};
-      if (pend) {
-        load_res(prv, 0, rv[0]);
-        load_res(prv, 1, rv[1]);
-      }
     }
     const float* wq = wsl + (size_t)q * 16384;
     const float* wq1 = q + 1 < NPR ? wq + 16384 : wnx;
-    float chk = 0.f;
+    // WINO_SP_MSPLIT: the split of block j + 1 is issued before block j's MFMAs
+    f16x8 sh[2], sl[2];
+    if (WINO_SP_MSPLIT) split_f16x3(ld4(As), ld4(As + 256), sh[0], sl[0]);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const f16x8 ah = ldh8(As + (2 * j) * 256), al = ldh8(As + (2 * j + 1) * 256);
+      f16x8 ah, al;
+      if (WINO_SP_MSPLIT) {
+        ah = sh[j & 1];
+        al = sl[j & 1];
+        if (j < 3)
+          split_f16x3(ld4(As + (2 * j + 2) * 256), ld4(As + (2 * j + 3) * 256), sh[(j + 1) & 1], sl[(j + 1) & 1]);
+      } else {
+        ah = ldh8(As + (2 * j) * 256);
+        al = ldh8(As + (2 * j + 1) * 256);
+      }
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < 2 && WINO_SP_EXP != 3 && WINO_SP_EXP != 4; ++u) {
         acc[j][u] = mfma16h(ah, bh[j & 1][u], acc[j][u]);
         acc[j][u] = mfma16h(ah, bl[j & 1][u], acc[j][u]);
         acc[j][u] = mfma16h(al, bh[j & 1][u], acc[j][u]);
       }
+      if (WINO_SP_EXP == 3 || WINO_SP_EXP == 4) acc[j][0][0] += (float)ah[0] + (float)al[1];   // keep the reads
       // refill the slot with block j + 2: (pair q, j + 2) or (next pair, j - 2)
       const float* wn = j < 2 ? wq + (j + 2) * 1024 : wq1 + (j - 2) * 1024;
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < 2 && WINO_SP_EXP != 1 && WINO_SP_EXP != 4; ++u) {
         bh[j & 1][u] = ldh8(wn + (u * 2) * 256);
         bl[j & 1][u] = ldh8(wn + (u * 2 + 1) * 256);
       }
       __builtin_amdgcn_sched_barrier(0);
-      // the previous tile's exchange, beside this tile's first MFMAs (its two rounds after blocks 1 and 2)
-      if (q == 0 && pend && (j == 1 || j == 2)) {
-        chk += ex_read(prv, j - 1, rv[j - 1]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    if (q == 0 && pend) {
-      report_range(a.status, not_finite(chk));
-      pend = false;
     }
     if (q == NPR - 1) {
-      // the exchange area is free: the previous tile's rounds were read during this tile's pair 0, at
-      // least one barrier ago (NPR >= 2)
+      // the exchange area is free: the T waves read the previous tile's rounds in steps q = 0, 1
       ex_write(acc);
-      pend = true;
-      prv = cur;
-      ++k_in;
-      T += nl;
       cur = nxt;
       wsl = wnx;
-      nxt = tile_of(k_in + 1 < ntw ? T + nl : T);
-      wnx = wbase(nxt);
     }
+    SP_STAMP(2 * n + 1);
     bar_lds();
-  }
-  // the last tile's exchange (published by the last step's barrier)
-  {
-    f32x4 rv[2][4];
-    load_res(prv, 0, rv[0]);
-    load_res(prv, 1, rv[1]);
-    float chk = ex_read(prv, 0, rv[0]);
-    chk += ex_read(prv, 1, rv[1]);
-    report_range(a.status, not_finite(chk));
+    ++n;
+  };
+  for (int k = 0; k < ntw; ++k) {
+    mstep(std::integral_constant<int, 0>{});
+    mstep(std::integral_constant<int, 1>{});
+    mstep(std::integral_constant<int, 2>{});
+    mstep(std::integral_constant<int, 3>{});
+    if constexpr (NPR == 8) {
+      mstep(std::integral_constant<int, 4>{});
+      mstep(std::integral_constant<int, 5>{});
+      mstep(std::integral_constant<int, 6>{});
+      mstep(std::integral_constant<int, 7>{});
+    }
+    nxt = tile_of(k + 2 < ntw ? T0 + (k + 2) * nl : T0);
+    wnx = wbase(nxt);
   }
 }
 
@@ -398,7 +490,7 @@ int stif_wino_sp_dispatch(const stif_conv_args& a, hipStream_t st) {
   const char* e = getenv("STIF_WINO_SP");
   const bool enabled = e && *e ? (atoi(e) != 0) : (WINO_SP != 0);
   if (!enabled || !(a.flags & STIF_CONV_F16X3) || a.cout % 64) return -1;
-  if (a.in1_mode > 1 || a.C0 % 16 || (a.in1_mode && a.C1 % 16)) return -1;
+  if (a.in1_mode > 1 || a.C0 != 64 || (a.in1_mode && a.C1 != 64)) return -1;   // 4 or 8 pairs per tile
   if ((long long)a.H * a.W * std::max(a.C0, std::max(a.C1, a.cout)) * 4 >= 0x7fffffffLL) return -1;
 #define STIF_SP_CASE(IN1)                                               \
   switch (a.epi) {                                                      \
@@ -412,3 +504,9 @@ int stif_wino_sp_dispatch(const stif_conv_args& a, hipStream_t st) {
   STIF_SP_CASE(1)
 #undef STIF_SP_CASE
 }
+
+#if WINO_SP_TRACE
+extern "C" int stif_wino_sp_trace(void* dev_buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_sp_trace), &dev_buf, sizeof(dev_buf)) == hipSuccess ? 0 : STIF_E_LAUNCH;
+}
+#endif
