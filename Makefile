@@ -13,7 +13,7 @@ HIPFLAGS := --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude -I$(PKG)/csrc -
 # gathers, stride-2 / 1x1 convs, upsample), while the DCN core measured 2-3 % slower and keeps them.
 # Device-only feature: the host pass prints "not a recognized feature for this target (ignoring feature)".
 NOPK := -Xclang -target-feature -Xclang -packed-fp32-ops
-NOPK_SRC := wino wino_sp decoder conv resample
+NOPK_SRC := wino decoder conv resample
 
 all: $(LIB)
 

@@ -14,26 +14,6 @@
 #ifndef WINO_OM_SCHED
 #define WINO_OM_SCHED 1    // a scheduling barrier after every k_wino_om B block (keeps the B loads early)
 #endif
-#ifndef WINO_SP
-// f16x3 3x3 convs with in1_mode 0 / 1 and epilogue NONE / LRELU / RELU / RES by the warp-specialized k_wino_sp
-// (wino_sp.hip; bit-identical outputs); 0 = k_wino.  Environment STIF_WINO_SP=0|1 overrides at run time.
-#define WINO_SP 0
-#endif
-#ifndef WINO_SP_EXP
-// k_wino_sp timing probes (wrong results): 1 no B refills, 2 no transform (T waves only stage), 3 no MFMAs,
-// 4 M waves only read A (no MFMAs, no B) and T waves only stage
-#define WINO_SP_EXP 0
-#endif
-static_assert(WINO_SP_EXP >= 0 && WINO_SP_EXP <= 4, "WINO_SP_EXP: probes 1-4");
-#ifndef WINO_SP_MSPLIT
-#define WINO_SP_MSPLIT 0   // k_wino_sp: operand split on the M waves (1) or the T waves (0)
-#endif
-#ifndef WINO_SP_TPRIO
-#define WINO_SP_TPRIO 0    // k_wino_sp: s_setprio of the T waves
-#endif
-#ifndef WINO_SP_TRACE
-#define WINO_SP_TRACE 0    // k_wino_sp per-step s_memtime trace (timing probe build, tools/r5/sp_trace.py)
-#endif
 #ifndef WINO_EXP
 #define WINO_EXP 0         // probes: 1 no LDS-DMA after the first phase, 2 no B refills, 3 no output exchange
 #endif

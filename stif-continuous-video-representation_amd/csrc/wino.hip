@@ -29,9 +29,6 @@
 
 #include <algorithm>
 
-// wino_sp.hip: k_wino_sp for the shapes it covers, -1 otherwise
-int stif_wino_sp_dispatch(const stif_conv_args& a, hipStream_t st);
-
 namespace {
 
 constexpr int WR = 4;      // output rows per tile
@@ -750,10 +747,6 @@ extern "C" int stif_conv3x3_wino(const stif_conv_args* pa, void* stream) {
   if (a.C0 % (8 * PSUB) || (a.in1_mode && a.C1 % (8 * PSUB)))
     return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: input channel counts must be multiples of 32");
   if (a.epi == STIF_EPI_RES && !a.res[0]) return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: RES needs res");
-  {
-    const int r = stif_wino_sp_dispatch(a, st);   // warp-specialized kernel (wino_sp.hip) where it applies
-    if (r >= 0) return r;
-  }
 #define STIF_WINO_CASE(IN1)                                              \
   switch (a.epi) {                                                       \
     case STIF_EPI_NONE: return launch<IN1, STIF_EPI_NONE>(a, st);        \

@@ -280,83 +280,3 @@ def test_wino_f16x3_range_status_single_element(stif, kind, pos):
         ops.conv2d([dict(layer=layer, in0=nhwc(xx), out=out)], epi=epi, status=st)
         assert int(st.item()) == want, (big, pos)
 
-
-# ---- k_wino_sp (wino_sp.hip): the warp-specialized f16x3 Winograd kernel must reproduce k_wino bit for bit
-# (same packing, MFMA K order and summation order); STIF_WINO_SP selects the kernel per call.
-SP_CASES = {
-    # name: (items, H, W, cin0, cin1, cout, groups)
-    "odd": (3, 13, 37, 64, 0, 64, 1),
-    "tile_exact": (2, 8, 32, 64, 0, 64, 1),
-    "edges": (2, 33, 70, 64, 0, 64, 1),
-    "tiny": (1, 4, 4, 64, 0, 64, 1),
-    "trunk_c0": (18, 128, 128, 64, 0, 64, 1),
-    "cat64": (2, 12, 40, 64, 64, 64, 2),
-    "cat32": (2, 12, 40, 64, 32, 64, 2),
-    "slices": (2, 20, 50, 64, 0, 128, 1),
-    "cout256_cat": (3, 16, 48, 64, 64, 256, 1),
-    "groups8": (1, 16, 32, 64, 0, 64, 8),
-}
-
-
-def _run_wino(stif, monkeypatch, sp, case, epi, seed=0, scale=1.0):
-    L, ops = stif._lib, stif.ops
-    n, H, W, c0, c1, co, g = SP_CASES[case]
-    rng = np.random.default_rng(seed)
-    outs = []
-    entries = []
-    for k in range(g):
-        x0 = torch.from_numpy((rng.standard_normal((n, H, W, c0)) * scale).astype(np.float32)).cuda()
-        x1 = torch.from_numpy(rng.standard_normal((n, H, W, c1)).astype(np.float32)).cuda() if c1 else None
-        w = (rng.standard_normal((co, c0 + c1, 3, 3)) * 0.04).astype(np.float32)
-        b = rng.standard_normal(co).astype(np.float32)
-        r = torch.from_numpy(rng.standard_normal((n, H, W, co)).astype(np.float32)).cuda()
-        out = torch.full((n, H, W, co), float("nan"), device="cuda")
-        outs.append(out)
-        entries.append(dict(layer=ops.pack_conv(w, b, L.PACK_WINO | L.PACK_F16X3), in0=x0, in1=x1, out=out,
-                            res=r if epi == L.EPI_RES else None))
-    monkeypatch.setenv("STIF_WINO_SP", "1" if sp else "0")
-    ops.conv2d(entries, epi=epi, in1_mode=1 if c1 else 0)
-    torch.cuda.synchronize()
-    return outs
-
-
-@pytest.mark.parametrize("epi", ["none", "lrelu", "relu", "res"])
-@pytest.mark.parametrize("case", sorted(SP_CASES))
-def test_wino_sp_bit_identical(stif, monkeypatch, case, epi):
-    L = stif._lib
-    e = dict(none=L.EPI_NONE, lrelu=L.EPI_LRELU, relu=L.EPI_RELU, res=L.EPI_RES)[epi]
-    ref = _run_wino(stif, monkeypatch, False, case, e)
-    got = _run_wino(stif, monkeypatch, True, case, e)
-    for a, b in zip(got, ref):
-        assert torch.isfinite(b).all()
-        assert torch.equal(a, b), (case, epi, float((a - b).abs().max()))
-
-
-def test_wino_sp_residual_in_place_and_oracle(stif, monkeypatch):
-    """k_wino_sp on the model's in-place ResidualBlock update (out == res), against the oracle."""
-    L, ops = stif._lib, stif.ops
-    monkeypatch.setenv("STIF_WINO_SP", "1")
-    x = rnd(2, 64, 16, 64, seed=5)
-    t = rnd(2, 64, 16, 64, seed=6)
-    w = rnd(64, 64, 3, 3, seed=7, scale=0.05)
-    b = rnd(64, seed=8)
-    xd = nhwc(x)
-    ops.conv2d([dict(layer=ops.pack_conv(w, b, L.PACK_WINO | L.PACK_F16X3), in0=nhwc(t), out=xd, res=xd)],
-               epi=L.EPI_RES)
-    assert relmax(to_nchw(xd), x + O.conv2d(t, w, b)) < RTOL
-
-
-def test_wino_sp_reports_range(stif, monkeypatch):
-    """An activation outside the split range makes k_wino_sp's outputs non-finite and sets the status word,
-    as k_wino does (the model then re-runs the call in fp32)."""
-    L, ops = stif._lib, stif.ops
-    monkeypatch.setenv("STIF_WINO_SP", "1")
-    x = torch.zeros(1, 16, 32, 64, device="cuda")
-    x[0, 5, 7, 3] = 1e6
-    w = rnd(64, 64, 3, 3, seed=2, scale=0.05)
-    out = torch.empty(1, 16, 32, 64, device="cuda")
-    st = torch.zeros(1, dtype=torch.int32, device="cuda")
-    ops.conv2d([dict(layer=ops.pack_conv(w, rnd(64, seed=3), L.PACK_WINO | L.PACK_F16X3), in0=x, out=out)],
-               epi=L.EPI_NONE, status=st)
-    torch.cuda.synchronize()
-    assert int(st.item()) == 1
