@@ -262,6 +262,7 @@ class LunaTokis(nn.Module):
         self._meta32 = None
         self._layers_key = None
         self._tables = {}
+        self._consts = {}
 
     def _pack_mlp(self, flags):
         """All SIREN layers (stif_pack_dec_mlp_ex); an out-of-range weight for f16x3 -> fp32 packing."""
@@ -409,6 +410,23 @@ class LunaTokis(nn.Module):
     def _empty(self, *shape):
         return torch.empty(*shape, device=self.device, dtype=torch.float32)
 
+    def _const(self, key, make):
+        """Maps that depend only on the packed weights and a shape (the all-zero initial state, its
+        pyramids, the zero-state L1 DCN output), computed on first use and kept until the layers are
+        re-packed; the key holds the weight buffers' addresses, so the fp32 range re-run's layers get
+        their own entries.  Not cached inside a hipGraph capture (computed in the graph instead)."""
+        if torch.cuda.is_current_stream_capturing():
+            return make()
+        consts = self.__dict__.setdefault("_consts", {})
+        v = consts.get(key)
+        if v is None:
+            v = consts[key] = make()
+        return v
+
+    def _zeros(self, *shape):
+        return self._const(("zeros",) + tuple(shape),
+                           lambda: torch.zeros(*shape, device=self.device, dtype=torch.float32))
+
     def _frame_features(self, frames):
         """conv_first + feature_extraction + pyramid (:318-325) for frames [n,3,H,W] (NCHW)."""
         return _drain(self._frame_features_steps(frames))
@@ -553,41 +571,46 @@ class LunaTokis(nn.Module):
                  epi=L.EPI_LRELU)
             del o1, o2
             self._dcn_sep([(f"{u[0]}L1_dcnpack_{u[1]}", l1off[k], u[2][0], d1[i]) for k, (i, u) in E(live)])
+        # the zero-state units' L1 DCN output is its bias everywhere: a constant map, kept across calls
+        d1z = {}
         for i in zero_l1:
-            d1[i].copy_(L_(units[i], "L1_dcnpack").b.view(1, 1, 1, 64).expand_as(d1[i]))
-        conv_up(lambda i, u, c: dict(layer=L_(u, "L1_fea_conv"), in0=d1[i], in1=c, out=u[4]),
+            b = L_(units[i], "L1_dcnpack").b
+            d1z[i] = self._const(("dcn_bias", b.data_ptr(), n, H, Wd), lambda b=b: b.view(1, 1, 1, 64).expand(
+                n, H, Wd, 64).contiguous())
+        conv_up(lambda i, u, c: dict(layer=L_(u, "L1_fea_conv"), in0=d1z.get(i, d1[i]), in1=c, out=u[4]),
                 l2fea, 1.0, L.EPI_NONE)
 
     def _bilstm(self, X):
-        return _drain(self._bilstm_steps(X))
+        return _drain(self._bilstm_steps([X[0], X[1], X[2]]))
 
-    def _bilstm_steps(self, X):
+    def _bilstm_steps(self, X, feats=None):
         """BiDeformableConvLSTM.forward (:256-266) with DeformableConvLSTM.forward (:192-242) for
-        both directions batched.  X: [3, B, H, W, 64] latent inputs (t-major).  Returns [3,B,H,W,64]."""
-        _, B, H, Wd, _ = X.shape
+        both directions batched.  X: the 3 latent inputs [B, H, W, 64] (t-major; views with one common
+        item stride).  Returns [3,B,H,W,64] (in ``feats`` when given)."""
+        B, H, Wd, _ = X[0].shape
         lay = self.layers
         pf = "ConvBLSTM.forward_net."
         pcds = (pf + "pcd_h.", pf + "pcd_c.")
         hs = self._empty(2, 3, B, H, Wd, 64)            # h of (direction, step)
-        cs = torch.zeros(2, B, H, Wd, 64, device=self.device)
-        zero = torch.zeros(B, H, Wd, 64, device=self.device)
+        cs = self._empty(2, B, H, Wd, 64)               # c of the last step (step 0 reads the zero state)
+        zero = self._zeros(B, H, Wd, 64)                # the initial h and c (convlstm.py:60-63), never written
         # Easy_PCD pyramids (:148-160) of the inputs, once per (pcd, input): the forward direction reads
         # X[t] and the reversed one X[2 - t] with the same weights, so per-step pyramids of the inputs
-        # would compute each of them twice (bit-identical results, half the work)
-        X3 = X.view(3 * B, H, Wd, 64)
-        xp2, xp3 = self._pyramid([(X3, pcds[0]), (X3, pcds[1])])   # [pcd][3B, ...]
+        # would compute each of them twice (bit-identical results, half the work); groups (pcd, t)
+        xp2, xp3 = self._pyramid([(X[t], pcds[p]) for p in range(2) for t in range(3)])
 
         def xpyr(p, level, fr):
-            return (xp2 if level == 2 else xp3)[p, fr * B:(fr + 1) * B]
+            return (xp2 if level == 2 else xp3)[p * 3 + fr]
 
         for t in range(3):
             fr = [t, 2 - t]                               # forward / reversed sequence
             xin = [X[f] for f in fr]
-            state = [[zero if t == 0 else hs[d, t - 1] for d in range(2)], [cs[d] for d in range(2)]]
+            state = [[zero if t == 0 else hs[d, t - 1] for d in range(2)], [zero if t == 0 else cs[d] for d in range(2)]]
             # pyramids of the recurrent states: groups (pcd, dir); at step 0 both directions' states are the
-            # same zeros, so each pcd's pyramid is computed once and shared (groups (pcd, pcd))
+            # same zeros, so each pcd's pyramid depends on its weights only: computed once, kept across calls
             if t == 0:
-                z2, z3 = self._pyramid([(zero, pcds[p]) for p in range(2)])
+                key = ("zero_pyr", lay[pcds[0] + "fea_L2_conv1"].w.data_ptr(), B, H, Wd)
+                z2, z3 = self._const(key, lambda: self._pyramid([(zero, pcds[p]) for p in range(2)]))
                 py2, py3 = [z2[p] for p in range(2) for d in range(2)], [z3[p] for p in range(2) for d in range(2)]
             else:
                 py2, py3 = self._pyramid([(state[p][d], pcds[p]) for p in range(2) for d in range(2)])
@@ -609,7 +632,8 @@ class LunaTokis(nn.Module):
             self._conv([dict(layer=lay[pf + "cell_list.0.conv"], in0=xin[d], in1=T[0, d], res=T[1, d],
                              out=hs[d, t], out2=cs[d]) for d in range(2)], epi=L.EPI_LSTM, in1_mode=1)
             yield
-        feats = self._empty(3, B, H, Wd, 64)
+        if feats is None:
+            feats = self._empty(3, B, H, Wd, 64)
         self._conv([dict(layer=lay["ConvBLSTM.conv_1x1"], in0=hs[0, t], in1=hs[1, 2 - t], out=feats[t])
                     for t in range(3)], in1_mode=1)
         return feats
@@ -619,22 +643,27 @@ class LunaTokis(nn.Module):
         out [3, B, H, W, 64] (generator: yields between stages, see _run_lanes).
         fea1 / fea2: [L1, L2, L3] of the pairs' first / second frames (item = pair)."""
         B, H, Wd, _ = fea1[0].shape
-        X = self._empty(3, B, H, Wd, 64)
-        X[0].copy_(fea1[0])
-        X[2].copy_(fea2[0])
+        X1 = self._empty(B, H, Wd, 64)                  # the fused middle latent input
         Y = self._empty(2, B, H, Wd, 64)
         self._pcd_align([("pcd_align.", 1, fea1, fea2, Y[0]), ("pcd_align.", 2, fea2, fea1, Y[1])])
-        self._conv([dict(layer=self.layers["fusion"], in0=Y[0], in1=Y[1], out=X[1])], in1_mode=1)
+        self._conv([dict(layer=self.layers["fusion"], in0=Y[0], in1=Y[1], out=X1)], in1_mode=1)
         del Y
         yield
-        feats = yield from self._bilstm_steps(X)
-        del X
+        # the inputs X = [fea1 L1, fused, fea2 L1] as views (no copies) when their item strides agree (the
+        # sliding-window path: consecutive frames); the batched pyramid of the inputs needs one stride
+        X = [fea1[0], X1, fea2[0]]
+        if not all(x.stride(0) == X1.stride(0) for x in X):   # (a [1, ...] view counts as contiguous in torch)
+            X = [X1 if x is X1 else self._empty(B, H, Wd, 64).copy_(x) for x in X]
+        # the latents go straight into `out` when it is one contiguous block (one chunk of pairs)
+        feats = yield from self._bilstm_steps(X, out if out.is_contiguous() else None)
+        del X, X1
         trunk = feats.view(3 * B, H, Wd, 64)
         tmp = self._empty(3 * B, H, Wd, 64)
         for i in range(self.back_RBs):
             self._resblock(trunk, tmp, f"recon_trunk.{i}")
             yield
-        out.copy_(feats)
+        if feats is not out:
+            out.copy_(feats)
 
     def _gen_feat_pairs(self, fea1, fea2, out):
         """_gen_feat_core over chunks of about ``chunk_px`` LR pixels of pairs (balanced), so the
