@@ -78,7 +78,10 @@ def kernel_desc(kind, mfma="f32"):
                     F16X3_PEAK_TFLOPS)
         return (f"k_dcn<{kind[1]}, 0>", "fused modulated deformable conv", FP32_PEAK_TFLOPS)
     if f16:
-        return (f"k_{kind[0]}", "SIREN decoder stage, split-fp16 MFMA (peak = fp16 MFMA / 3)", F16X3_PEAK_TFLOPS)
+        # stage 2 of LunaTokis.decoding in f16x3 is k_dec2q (16 pixels per wave); k_dec2 runs the fp32 and the
+        # high-resolution-image variants (decoder.hip, stif_dec_stage2_ex)
+        name = "k_dec2q" if kind[0] == "dec2" else f"k_{kind[0]}"
+        return (name, "SIREN decoder stage, split-fp16 MFMA (peak = fp16 MFMA / 3)", F16X3_PEAK_TFLOPS)
     return (f"k_{kind[0]}", "SIREN decoder stage", FP32_PEAK_TFLOPS)
 
 
@@ -205,7 +208,8 @@ def hot_path_kernels(probe, mfma):
     for k, (nl, ms, fl, nb) in probe.per_kind().items():
         if k[0] not in ("dcn", "dcnsep", "dec1", "dec2") or not ms:
             continue
-        e = {"launches": nl, "avg_us": round(ms / nl * 1e3, 1), "tflops": round(fl / (ms * 1e-3) / 1e12, 1)}
+        e = {"kernel": kernel_desc(k, mfma)[0], "launches": nl, "avg_us": round(ms / nl * 1e3, 1),
+             "tflops": round(fl / (ms * 1e-3) / 1e12, 1)}
         if nb:
             gbps = nb / (ms * 1e-3) / 1e9
             e.update(hbm_gbps_algorithmic=round(gbps, 1), hbm_frac=round(gbps / HBM_PEAK_GBPS, 3))
