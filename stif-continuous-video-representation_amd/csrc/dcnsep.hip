@@ -272,8 +272,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_
   // gate; global fallback outside the tile
   auto sample = [&](const float* st, int pa, int tap, float dy, float dx, float mk, f32x4& a0, f32x4& a1) {
     const int ky = tap / 3, kx = tap - 3 * ky;
+#if DCNSEP_EXP == 6   // timing probe: sampling positions without the learned offsets (regular LDS addresses)
+    const float h_im = (float)(oy - 1 + ky) + 0.25f + 0.f * dy;
+    const float w_im = (float)(ox - 1 + kx) + 0.25f + 0.f * dx;
+#else
     const float h_im = (float)(oy - 1 + ky) + dy;
     const float w_im = (float)(ox - 1 + kx) + dx;
+#endif
     const bool valid = pix_ok & (h_im > -1.f) & (w_im > -1.f) & (h_im < (float)H) & (w_im < (float)W);
     const float fh = floorf(h_im), fw = floorf(w_im);
     const float lh = h_im - fh, lw = w_im - fw, hh = 1.f - lh, hw = 1.f - lw;

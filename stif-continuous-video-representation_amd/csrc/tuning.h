@@ -43,10 +43,10 @@
 #define DCNSEP_WPE 2       // waves per SIMD the kernel is register-budgeted for
 #endif
 #ifndef DCNSEP_EXP
-#define DCNSEP_EXP 0       // probes: 1 no phase 1, 3 no phase 2, 5 no per-pair restaging
+#define DCNSEP_EXP 0       // probes: 1 no phase 1, 3 no phase 2, 5 no per-pair restaging, 6 offset-free sampling
 #endif
-static_assert(DCNSEP_EXP == 0 || DCNSEP_EXP == 1 || DCNSEP_EXP == 3 || DCNSEP_EXP == 5,
-              "DCNSEP_EXP: only probes 1, 3 and 5 exist (a probe number without code would build the product kernel)");
+static_assert(DCNSEP_EXP == 0 || DCNSEP_EXP == 1 || DCNSEP_EXP == 3 || DCNSEP_EXP == 5 || DCNSEP_EXP == 6,
+              "DCNSEP_EXP: only probes 1, 3, 5 and 6 exist (a probe number without code would build the product kernel)");
 
 // ---- k_dec1 / k_dec2 (decoder.hip)
 #ifndef DEC1_NW
