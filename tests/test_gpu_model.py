@@ -298,3 +298,31 @@ def test_decoder_stage2_flags_nonfinite_flow(stif, sd, golden):
             ops.dec_stage2(proj, mlp, hrf, f, tab, t, out, flags=m._dec_flags, status=st)
             assert int(st.item()) == int(poison)
             assert bool(torch.isfinite(out).all())      # the clamp keeps the pixel finite: only the flag tells
+
+
+def test_cached_constants_follow_the_weights(stif):
+    """The encoder caches weight-only constants across calls (the zero-state pyramids and L1 DCN maps,
+    LunaTokis._const).  Loading other weights into the same module must not reuse them: the second run equals
+    a fresh module's bit for bit, and a repeated call equals the first."""
+    dev = torch.device("cuda", 0)
+    fr = torch.rand(3, 3, 32, 48, generator=torch.Generator().manual_seed(3)).to(dev)
+    tq = [torch.tensor([[0.5]])]
+
+    def run(m):
+        with torch.no_grad():
+            m.gen_feat_window(fr)
+            out = m.decoding(tq)[0]
+        torch.cuda.synchronize()
+        return m._feat.clone(), out.clone()
+
+    m = stif.LunaTokis(64, 6, 8, 5, 40, device=dev)
+    m.load_state_dict(stif.weights.make_state_dict(0), strict=True)
+    a0 = run(m)
+    assert torch.equal(run(m)[1], a0[1])               # second call on the cached constants
+    m.load_state_dict(stif.weights.make_state_dict(1), strict=True)
+    b = run(m)
+    fresh = stif.LunaTokis(64, 6, 8, 5, 40, device=dev)
+    fresh.load_state_dict(stif.weights.make_state_dict(1), strict=True)
+    ref = run(fresh)
+    assert torch.equal(b[0], ref[0]) and torch.equal(b[1], ref[1])
+    assert not torch.equal(b[1], a0[1])
