@@ -392,7 +392,8 @@ def run_config(stif, sd, cfg, args, world, rank, device, dist, mfma, trace_dom=T
     a, b = shards[rank]
     total_pairs = total_frames - 1
     HH, WW = int(round(H * scale)), int(round(W * scale))
-    model = stif.LunaTokis(64, 6, 8, 5, 40, device=device, mfma=mfma, lanes=args.lanes,
+    model = stif.LunaTokis(64, 6, 8, 5, 40, device=device, mfma=mfma, lanes=args.lanes, trunk_lanes=args.trunk_lanes,
+                           dec_lanes=args.dec_lanes, lstm_lanes=args.lstm_lanes,
                            range_check=getattr(args, "range_check", "rerun"), fused_dcn=bool(args.fused_dcn))
     model.load_state_dict(sd, strict=True)
     frames = synth_frames(a, b - a, H, W, device) if b > a else None
@@ -488,6 +489,12 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="N>1 process group: nccl (= RCCL over xGMI, one GPU per rank) or gloo (host-staged halo; "
                          "ranks may share a GPU -- the multi-rank GPU test on a one-GPU box)")
+    ap.add_argument("--trunk-lanes", type=int, default=2,
+                    help="HIP streams the recon trunk's items are split over (LunaTokis trunk_lanes)")
+    ap.add_argument("--lstm-lanes", type=int, default=1,
+                    help="streams for the BiConvLSTM's two directions (LunaTokis lstm_lanes: 1 or 2)")
+    ap.add_argument("--dec-lanes", type=int, default=None,
+                    help="HIP streams decoding's pairs are split over (LunaTokis dec_lanes; default: --lanes)")
     ap.add_argument("--lanes", type=int, default=1,
                     help="concurrent HIP streams per rank, each a contiguous range of the pairs (LunaTokis lanes)")
     args = ap.parse_args()

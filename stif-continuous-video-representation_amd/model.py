@@ -62,7 +62,7 @@ class LunaTokis(nn.Module):
 
     def __init__(self, nf=64, nframes=3, groups=8, front_RBs=5, back_RBs=10, device="cuda", winograd=True,
                  mfma="f16x3", range_check="rerun", chunk_px=2 ** 21, lanes=1, dec_chunk_px=2 ** 25,
-                 fused_dcn=True):
+                 fused_dcn=True, trunk_lanes=2, dec_lanes=None, lstm_lanes=1):
         super().__init__()
         if nf != 64 or groups != 8:
             raise ValueError("the gfx950 kernels implement nf=64, groups=8 (the shipped STIF configuration)")
@@ -120,6 +120,20 @@ class LunaTokis(nn.Module):
         if int(lanes) < 1:
             raise ValueError("lanes must be >= 1")
         self.lanes = int(lanes)
+        # the recon trunk's items (3 latents per pair, independent chains of 80 convs) split over
+        # `trunk_lanes` streams, block by block round-robin, so one half's tail waves overlap the other's.
+        # At C0 (18 items = 2,304 tiles = 4.5 per persistent workgroup) 2 streams measured -0.1 to -0.5 ms
+        # per step against 1, 3 streams +0.2 ms; splitting the 7-frame feature_extraction stack the same
+        # way measured slower (profiles/r05_trunk_lanes_ab.log)
+        if int(trunk_lanes) < 1:
+            raise ValueError("trunk_lanes must be >= 1")
+        self.trunk_lanes = int(trunk_lanes)
+        # the BiConvLSTM's two directions on two streams (lstm_lanes=2)
+        self.lstm_lanes = int(lstm_lanes)
+        # decoding's pair ranges on their own streams (None: follow `lanes`)
+        if dec_lanes is not None and int(dec_lanes) < 1:
+            raise ValueError("dec_lanes must be >= 1")
+        self.dec_lanes = None if dec_lanes is None else int(dec_lanes)
         self._lane_streams = {}
         self._active = False
 
@@ -421,6 +435,8 @@ class LunaTokis(nn.Module):
         v = consts.get(key)
         if v is None:
             v = consts[key] = make()
+            if self.device.type == "cuda":   # once: other streams (lanes) read it without an event
+                torch.cuda.current_stream(self.device).synchronize()
         return v
 
     def _zeros(self, *shape):
@@ -436,21 +452,19 @@ class LunaTokis(nn.Module):
         l1 = self._empty(n, H, Wd, 64)
         ops.conv_first(frames, self.layers["conv_first"].w, self.layers["conv_first"].b, l1)
         tmp = self._empty(n, H, Wd, 64)
-        for i in range(self.front_RBs):
-            self._resblock(l1, tmp, f"feature_extraction.{i}")
-            yield
+        yield from self._resblocks(l1, tmp, [f"feature_extraction.{i}" for i in range(self.front_RBs)])
         l2, l3 = self._pyramid([(l1, "")])
         return l1, l2[0], l3[0]
 
     # ------------------------------------------------------------------ lanes
-    def _streams(self, k):
+    def _streams(self, k, pool="lanes"):
         dev = self.device
-        ss = self._lane_streams.setdefault(str(dev), [])
+        ss = self._lane_streams.setdefault((pool, str(dev)), [])
         while len(ss) < k:
             ss.append(torch.cuda.Stream(device=dev))
         return ss[:k]
 
-    def _run_lanes(self, n, make):
+    def _run_lanes(self, n, make, lanes=None, pool="lanes"):
         """Items [0, n) in up to ``self.lanes`` contiguous ranges; ``make(c0, c1)`` is a generator
         issuing one range's launches (each ``yield`` a point where another lane may issue).  Each
         range runs on its own stream, forked from and joined back into the current one, and the
@@ -458,14 +472,14 @@ class LunaTokis(nn.Module):
         kernels of one lane fill the last waves and the dispatch gaps of the others.  Every kernel
         computes each item independently of the batch it is launched in, so the results are
         bit-identical for any lane count."""
-        k = max(1, min(self.lanes, n))
+        k = max(1, min(self.lanes if lanes is None else lanes, n))
         per = -(-n // k)
         ranges = [(c0, min(n, c0 + per)) for c0 in range(0, n, per)]
         if len(ranges) == 1:
             _drain(make(0, n))
             return
         main = torch.cuda.current_stream()
-        streams = self._streams(len(ranges))
+        streams = self._streams(len(ranges), pool)
         for s in streams:
             s.wait_stream(main)
         live = [(s, make(c0, c1)) for s, (c0, c1) in zip(streams, ranges)]
@@ -480,6 +494,32 @@ class LunaTokis(nn.Module):
                         pass
             live = nxt
         for s in streams:
+            main.wait_stream(s)
+
+    def _resblocks(self, x, tmp, names, lanes=1):
+        """A stack of ResidualBlock_noBN on x [n, H, W, 64] in place (generator, one yield per block).
+        The items are independent chains, so with ``lanes`` > 1 they are split into that many
+        contiguous ranges on their own streams, issued block by block round-robin: one range's tail
+        waves and dispatch gaps overlap the other's work.  Bit-identical for any split."""
+        n = x.shape[0]
+        k = max(1, min(lanes, n))
+        if k == 1:
+            for name in names:
+                self._resblock(x, tmp, name)
+                yield
+            return
+        per = -(-n // k)
+        ranges = [(c0, min(n, c0 + per)) for c0 in range(0, n, per)]
+        main = torch.cuda.current_stream()
+        ss = self._streams(len(ranges), pool="trunk")
+        for s in ss:
+            s.wait_stream(main)
+        for name in names:
+            for s, (c0, c1) in zip(ss, ranges):
+                with torch.cuda.stream(s):
+                    self._resblock(x[c0:c1], tmp[c0:c1], name)
+            yield
+        for s in ss:
             main.wait_stream(s)
 
     def _resblock(self, x, tmp, name):
@@ -602,36 +642,57 @@ class LunaTokis(nn.Module):
         def xpyr(p, level, fr):
             return (xp2 if level == 2 else xp3)[p * 3 + fr]
 
-        for t in range(3):
+        # the step-0 state pyramids (zeros) once per pcd, depending on the weights only: kept across calls
+        zkey = ("zero_pyr", lay[pcds[0] + "fea_L2_conv1"].w.data_ptr(), B, H, Wd)
+        z2, z3 = self._const(zkey, lambda: self._pyramid([(zero, pcds[p]) for p in range(2)]))
+
+        def step(t, ds):
+            """Step t of the directions ds (0 forward, 1 reversed): state pyramids, PCD alignments,
+            Easy_PCD fusion and the ConvLSTM cell, each one launch over (pcd, direction) groups."""
             fr = [t, 2 - t]                               # forward / reversed sequence
             xin = [X[f] for f in fr]
-            state = [[zero if t == 0 else hs[d, t - 1] for d in range(2)], [zero if t == 0 else cs[d] for d in range(2)]]
-            # pyramids of the recurrent states: groups (pcd, dir); at step 0 both directions' states are the
-            # same zeros, so each pcd's pyramid depends on its weights only: computed once, kept across calls
+            pd = [(p, d) for p in range(2) for d in ds]
+            st = {(p, d): zero if t == 0 else (hs[d, t - 1] if p == 0 else cs[d]) for p, d in pd}
             if t == 0:
-                key = ("zero_pyr", lay[pcds[0] + "fea_L2_conv1"].w.data_ptr(), B, H, Wd)
-                z2, z3 = self._const(key, lambda: self._pyramid([(zero, pcds[p]) for p in range(2)]))
-                py2, py3 = [z2[p] for p in range(2) for d in range(2)], [z3[p] for p in range(2) for d in range(2)]
+                pyr = {(p, d): (z2[p], z3[p]) for p, d in pd}
             else:
-                py2, py3 = self._pyramid([(state[p][d], pcds[p]) for p in range(2) for d in range(2)])
-            Y = self._empty(2, 2, 2, B, H, Wd, 64)       # (pcd, dir, align direction)
+                a2, a3 = self._pyramid([(st[p, d], pcds[p]) for p, d in pd])
+                pyr = {k: (a2[i], a3[i]) for i, k in enumerate(pd)}
+            nd = len(ds)
+            Y = self._empty(2, nd, 2, B, H, Wd, 64)      # (pcd, dir, align direction)
             units = []
             for p in range(2):
-                for d in range(2):
-                    gi = p * 2 + d
+                for j, d in enumerate(ds):
                     f1 = [xin[d], xpyr(p, 2, fr[d]), xpyr(p, 3, fr[d])]
-                    f2 = [state[p][d], py2[gi], py3[gi]]
-                    units.append((pcds[p] + "pcd_align.", 1, f1, f2, Y[p, d, 0]))
-                    units.append((pcds[p] + "pcd_align.", 2, f2, f1, Y[p, d, 1]))
+                    f2 = [st[p, d], *pyr[p, d]]
+                    units.append((pcds[p] + "pcd_align.", 1, f1, f2, Y[p, j, 0]))
+                    units.append((pcds[p] + "pcd_align.", 2, f2, f1, Y[p, j, 1]))
             # step 0: the reversed alignments (odd units) sample the all-zero initial state at L1
-            self._pcd_align(units, zero_l1=range(1, 8, 2) if t == 0 else ())
-            T = self._empty(2, 2, B, H, Wd, 64)          # Easy_PCD.fusion outputs: (pcd, dir)
-            self._conv([dict(layer=lay[pcds[p] + "fusion"], in0=Y[p, d, 0], in1=Y[p, d, 1], out=T[p, d])
-                        for p in range(2) for d in range(2)], in1_mode=1)
+            self._pcd_align(units, zero_l1=range(1, len(units), 2) if t == 0 else ())
+            T = self._empty(2, nd, B, H, Wd, 64)         # Easy_PCD.fusion outputs: (pcd, dir)
+            self._conv([dict(layer=lay[pcds[p] + "fusion"], in0=Y[p, j, 0], in1=Y[p, j, 1], out=T[p, j])
+                        for p in range(2) for j in range(nd)], in1_mode=1)
             # ConvLSTMCell (convlstm.py:42-58): combined = cat(x, h~); c_next = f*c~ + i*g
-            self._conv([dict(layer=lay[pf + "cell_list.0.conv"], in0=xin[d], in1=T[0, d], res=T[1, d],
-                             out=hs[d, t], out2=cs[d]) for d in range(2)], epi=L.EPI_LSTM, in1_mode=1)
-            yield
+            self._conv([dict(layer=lay[pf + "cell_list.0.conv"], in0=xin[d], in1=T[0, j], res=T[1, j],
+                             out=hs[d, t], out2=cs[d]) for j, d in enumerate(ds)], epi=L.EPI_LSTM, in1_mode=1)
+
+        if self.lstm_lanes < 2:
+            for t in range(3):
+                step(t, (0, 1))
+                yield
+        else:
+            # the two directions are independent recurrences: one stream each, step by step round-robin
+            main = torch.cuda.current_stream()
+            ss = self._streams(2, pool="lstm")
+            for s in ss:
+                s.wait_stream(main)
+            for t in range(3):
+                for s, d in zip(ss, (0, 1)):
+                    with torch.cuda.stream(s):
+                        step(t, (d,))
+                yield
+            for s in ss:
+                main.wait_stream(s)
         if feats is None:
             feats = self._empty(3, B, H, Wd, 64)
         self._conv([dict(layer=lay["ConvBLSTM.conv_1x1"], in0=hs[0, t], in1=hs[1, 2 - t], out=feats[t])
@@ -659,9 +720,7 @@ class LunaTokis(nn.Module):
         del X, X1
         trunk = feats.view(3 * B, H, Wd, 64)
         tmp = self._empty(3 * B, H, Wd, 64)
-        for i in range(self.back_RBs):
-            self._resblock(trunk, tmp, f"recon_trunk.{i}")
-            yield
+        yield from self._resblocks(trunk, tmp, [f"recon_trunk.{i}" for i in range(self.back_RBs)], self.trunk_lanes)
         if feats is not out:
             out.copy_(feats)
 
@@ -838,7 +897,7 @@ class LunaTokis(nn.Module):
                 yield
                 yield from self._decode_steps(proj, [t[a:b] for t in tvs], HH, WW, tab, [o[a:b] for o in outs])
                 del proj
-        self._run_lanes(B, lane)
+        self._run_lanes(B, lane, self.dec_lanes, pool="dec")
         return outs
 
     def decoding_test(self, times=None, scale=None):
