@@ -128,7 +128,11 @@ class LunaTokis(nn.Module):
         if int(trunk_lanes) < 1:
             raise ValueError("trunk_lanes must be >= 1")
         self.trunk_lanes = int(trunk_lanes)
-        # the BiConvLSTM's two directions on two streams (lstm_lanes=2)
+        # the BiConvLSTM's two directions on two streams (lstm_lanes=2): bit-identical, but measured
+        # +0.9 ms per C0 step (17.2 vs 16.3 ms, profiles/r05_trunk_lanes_ab.log) -- half-size PCD launches
+        # of two chains competing for the CUs; default 1
+        if int(lstm_lanes) not in (1, 2):
+            raise ValueError("lstm_lanes must be 1 or 2")
         self.lstm_lanes = int(lstm_lanes)
         # decoding's pair ranges on their own streams (None: follow `lanes`)
         if dec_lanes is not None and int(dec_lanes) < 1:
