@@ -393,7 +393,7 @@ def run_config(stif, sd, cfg, args, world, rank, device, dist, mfma, trace_dom=T
     total_pairs = total_frames - 1
     HH, WW = int(round(H * scale)), int(round(W * scale))
     model = stif.LunaTokis(64, 6, 8, 5, 40, device=device, mfma=mfma, lanes=args.lanes, trunk_lanes=args.trunk_lanes,
-                           dec_lanes=args.dec_lanes, lstm_lanes=args.lstm_lanes,
+                           dec_lanes=args.dec_lanes, lstm_lanes=args.lstm_lanes, pcd_streams=args.pcd_streams,
                            range_check=getattr(args, "range_check", "rerun"), fused_dcn=bool(args.fused_dcn))
     model.load_state_dict(sd, strict=True)
     frames = synth_frames(a, b - a, H, W, device) if b > a else None
@@ -491,6 +491,10 @@ def main():
                          "ranks may share a GPU -- the multi-rank GPU test on a one-GPU box)")
     ap.add_argument("--trunk-lanes", type=int, default=2,
                     help="HIP streams the recon trunk's items are split over (LunaTokis trunk_lanes)")
+    ap.add_argument("--pcd-streams", type=int, default=1,
+                    help="PCD alignment: 2 = the DCN / feature branch on a second stream (LunaTokis pcd_streams)")
+    ap.add_argument("--dynamic-tiles", type=int, default=0,
+                    help="persistent Winograd conv: 1 = dynamic per-XCD tile counters, 0 = static schedule")
     ap.add_argument("--lstm-lanes", type=int, default=1,
                     help="streams for the BiConvLSTM's two directions (LunaTokis lstm_lanes: 1 or 2)")
     ap.add_argument("--dec-lanes", type=int, default=None,
@@ -521,6 +525,7 @@ def main():
 
     import stif_pkg
     stif = stif_pkg.load()
+    stif.ops.DYNAMIC_TILES = bool(args.dynamic_tiles)
     sd = stif.weights.make_state_dict(seed=0)
     nframes, H, W, scale, times, scaling = CONFIGS[args.config]
     elapsed, probe, timer, model, frames, tq, out_pix = run_config(stif, sd, args.config, args, world, rank, device,

@@ -74,6 +74,12 @@ typedef struct {
   int* status;             /* optional device word (NULL = none): with STIF_CONV_F16X3, set to 1 when an output
                               element is not finite before its activation -- the signature of an activation
                               outside the split-fp16 operand range (see STIF_CONV_F16X3) */
+  int* sched;              /* optional device block of 8 ints, zero when first used (stif_conv3x3_wino, STIF_CONV_F16X3
+                              launches; ignored otherwise): per-XCD tile counters of the persistent kernel's dynamic
+                              schedule.  The library keeps each block's running totals on the host, so the launches
+                              that use one block must run in issue order (one stream) and the block must not be
+                              freed and re-allocated while the library is loaded.  NULL = static schedule.
+                              Outputs are identical either way. */
 } stif_conv_args;
 
 /* stif_conv_args.flags: fp32 products on the fp16 MFMA pipe by 3-term operand splitting (x = h + l,

@@ -31,7 +31,7 @@ class ConvArgs(C.Structure):
         ("H", C.c_int), ("W", C.c_int), ("C0", C.c_int),
         ("C1", C.c_int), ("in1_mode", C.c_int), ("in1_scale", C.c_float),
         ("Ho", C.c_int), ("Wo", C.c_int), ("cout", C.c_int), ("ks", C.c_int), ("stride", C.c_int),
-        ("epi", C.c_int), ("flags", C.c_int), ("status", _P),
+        ("epi", C.c_int), ("flags", C.c_int), ("status", _P), ("sched", _P),
     ]
 
 

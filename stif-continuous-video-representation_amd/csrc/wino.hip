@@ -28,6 +28,9 @@
 #include "tuning.h"
 
 #include <algorithm>
+#include <array>
+#include <mutex>
+#include <unordered_map>
 
 namespace {
 
@@ -98,8 +101,15 @@ struct Tile {
 // phase of the next tile and the last chunk prefetches the next tile's first B operands, so a
 // workgroup's MFMA stream only pauses at the per-phase barriers and the short epilogue exchange.
 // Wave i = transform row i for both 32-cout halves (2 waves per SIMD, ~250 VGPRs).
+// dynamic schedule: the value each XCD counter holds before the launch (the host keeps the counters'
+// running totals, so nothing resets them at the end of a launch)
+struct SchedBase {
+  unsigned b[8];
+};
+
 template <int IN1, int EPI, int F16>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_wino(stif_conv_args a, int ntiles) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_wino(stif_conv_args a, int ntiles,
+                                                                                      SchedBase sb) {
   __shared__ __attribute__((aligned(16))) float smem[2 * BUF_F + (IN1 == 2 ? SCR_F : 0)];
   float* const scr = smem + 2 * BUF_F;                       // IN1 = 2: coarse patch of the next phase
   const int tid = threadIdx.x;
@@ -228,13 +238,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   };
 
   // XCD-aware persistent schedule: workgroup b is dispatched to XCD b % 8, and XCD x owns the
-  // contiguous tile range [x * per, (x + 1) * per), its workgroups striding through it -- tiles
-  // that share input (cout slices, halo rows) run at the same time under the same L2
+  // contiguous tile range [x * per, (x + 1) * per) -- tiles that share input (cout slices, halo rows)
+  // run at the same time under the same L2.  Static (a.sched == nullptr): the XCD's workgroups stride
+  // through it.  Dynamic (a.sched: this stream's 8 counters): the first two tiles are static, the rest
+  // are taken from the XCD's counter (relative to its value before the launch, sb), one workgroup-wide
+  // atomic fetched a tile ahead -- a workgroup that started late (another stream's kernel held the CU)
+  // takes fewer tiles instead of finishing late.  Outputs do not depend on it.
   const int xcd = blockIdx.x & 7, nl = gridDim.x >> 3;   // host: grid is a multiple of 8
   const int per = (ntiles + 7) >> 3;
   const int tend = min((xcd + 1) * per, ntiles);
+  // (the fp32-operand variants -- the range re-run -- keep the static schedule: no registers to spare)
+  int* const sched = a.sched;
+  const bool dyn = F16 && sched != nullptr;
+  __shared__ int tslot[2];                                // fetched tile indices, by tile parity
   int T = xcd * per + (blockIdx.x >> 3);
-  if (T >= tend) return;
+  int Tn = T + nl;                                        // the next tile (static for the first two)
+  const int dbase = xcd * per + 2 * nl;                   // dynamic tile d = dbase + counter value
+  int par = 0;
+  if (T < tend) {
   Tile cur = tile_of(T);
   const float* wsl = wbase(cur);
   f32x4 bw[4][2];
@@ -260,10 +281,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   lds_dma_barrier();
 
   for (;;) {
-    const int Tn = T + nl;
     const bool has_next = Tn < tend;
     const Tile nxt = tile_of(has_next ? Tn : T);
     const float* wnx = wbase(nxt);
+    // dynamic: the tile after next, consumed at the next tile's top (written to tslot after phase 0's
+    // barrier, when every wave has read the previous value)
+    const bool fetch = dyn && has_next;
+    int fetched = 0;
+    if (fetch && wi == 0 && lane == 0)
+      fetched = (int)((unsigned)__hip_atomic_fetch_add(sched + xcd, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
+                      sb.b[xcd]);
+    auto publish = [&](int p) {
+      if (p == 0 && fetch && wi == 0 && lane == 0) tslot[par] = fetched;
+    };
+    auto advance = [&]() {
+      T = Tn;
+      cur = nxt;
+      wsl = wnx;
+      Tn = dyn ? dbase + tslot[par] : Tn + nl;
+      par ^= 1;
+    };
 
     f32x16 acc[4][2];
 #pragma unroll
@@ -319,6 +356,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         // them -- has landed
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         __syncthreads();
+        publish(p);
         if (IN1 == 2 && p + 1 < NP && up_phase(p + 1)) {
           expand(cur, (gp + 1) & 1);
           __syncthreads();
@@ -357,6 +395,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       // them -- has landed; those 8 stay in flight across the barrier
       asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       __syncthreads();
+      publish(p);
       if (IN1 == 2 && p + 1 < NP && up_phase(p + 1)) {
         expand(cur, (gp + 1) & 1);
         __syncthreads();
@@ -379,10 +418,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 #pragma unroll
       for (int r = 0; r < 16; ++r) tot += sm[r];
       a.out[cur.g][(size_t)cur.n * a.out_item + ((size_t)(cur.oy0 * a.Wo + cur.ox0) * a.cout) + tid] = tot;
+      __syncthreads();
       if (!has_next) break;
-      T = Tn;
-      cur = nxt;
-      wsl = wnx;
+      advance();
       continue;
     }
     f32x16 yv[2][2];   // [local half][b]
@@ -476,9 +514,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     if (F16) report_range(a.status, not_finite(chk));   // a non-finite output makes the sum non-finite
     __syncthreads();   // exchange buffer free for the next tile's staging
     if (!has_next) break;
-    T = Tn;
-    cur = nxt;
-    wsl = wnx;
+    advance();
+  }
   }
 }
 
@@ -703,6 +740,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   }
 }
 
+// Host side of the dynamic schedule: the running totals of every counter block, by address.  Per launch the
+// increments of XCD x's counter are exact: every dynamic tile is fetched once (D = count - 2 nl valid
+// values), and every workgroup that fetches at all (its second static tile exists: F = count - nl, at most
+// nl of them) stops after its one failing fetch -- so sb is the counter's value before the launch.
+// Launches sharing a block run one after another (one stream), so the totals are exact in order.
+std::mutex g_sched_mu;
+std::unordered_map<const int*, std::array<unsigned, 8>> g_sched;
+
+void sched_advance(const int* key, int ntiles, int grid, SchedBase& sb) {
+  const int nl = grid >> 3, per = (ntiles + 7) >> 3;
+  std::lock_guard<std::mutex> lk(g_sched_mu);
+  std::array<unsigned, 8>& tot = g_sched[key];   // a new block starts at zero (the caller zeroed it)
+  for (int x = 0; x < 8; ++x) {
+    sb.b[x] = tot[x];
+    const int count = std::max(0, std::min((x + 1) * per, ntiles) - x * per);
+    const int dyn_tiles = std::max(0, count - 2 * nl);
+    const int fetchers = std::max(0, std::min(nl, count - nl));
+    tot[x] += (unsigned)(dyn_tiles + fetchers);
+  }
+}
+
 template <int IN1, int EPI>
 int launch(const stif_conv_args& a, hipStream_t st) {
   const long long tiles =
@@ -717,10 +775,12 @@ int launch(const stif_conv_args& a, hipStream_t st) {
     return stif_check_launch("stif_conv3x3_wino");
   }
   const int grid = 8 * (int)std::min<long long>((tiles + 7) / 8, (long long)WG_PER_CU * stif_num_cus() / 8);
+  SchedBase sb{};
+  if (a.sched && (a.flags & STIF_CONV_F16X3)) sched_advance(a.sched, (int)tiles, grid, sb);
   if (a.flags & STIF_CONV_F16X3)
-    hipLaunchKernelGGL((k_wino<IN1, EPI, 1>), dim3(grid), dim3(256), 0, st, a, (int)tiles);
+    hipLaunchKernelGGL((k_wino<IN1, EPI, 1>), dim3(grid), dim3(256), 0, st, a, (int)tiles, sb);
   else
-    hipLaunchKernelGGL((k_wino<IN1, EPI, 0>), dim3(grid), dim3(256), 0, st, a, (int)tiles);
+    hipLaunchKernelGGL((k_wino<IN1, EPI, 0>), dim3(grid), dim3(256), 0, st, a, (int)tiles, sb);
   return stif_check_launch("stif_conv3x3_wino");
 }
 

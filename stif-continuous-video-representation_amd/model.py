@@ -17,6 +17,7 @@ the reconstruction trunk.  Per-frame encoder features are computed once per fram
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import warnings
 from collections import OrderedDict
@@ -62,7 +63,7 @@ class LunaTokis(nn.Module):
 
     def __init__(self, nf=64, nframes=3, groups=8, front_RBs=5, back_RBs=10, device="cuda", winograd=True,
                  mfma="f16x3", range_check="rerun", chunk_px=2 ** 21, lanes=1, dec_chunk_px=2 ** 25,
-                 fused_dcn=True, trunk_lanes=2, dec_lanes=None, lstm_lanes=1):
+                 fused_dcn=True, trunk_lanes=2, dec_lanes=None, lstm_lanes=1, pcd_streams=1):
         super().__init__()
         if nf != 64 or groups != 8:
             raise ValueError("the gfx950 kernels implement nf=64, groups=8 (the shipped STIF configuration)")
@@ -134,6 +135,11 @@ class LunaTokis(nn.Module):
         if int(lstm_lanes) not in (1, 2):
             raise ValueError("lstm_lanes must be 1 or 2")
         self.lstm_lanes = int(lstm_lanes)
+        # PCD alignment: the DCN / feature branch on a second stream (_pcd_align); bit-identical, measured
+        # equal to one stream at C0 with either tile schedule (profiles/r05_dynamic_tiles_ab.log); default 1
+        if int(pcd_streams) not in (1, 2):
+            raise ValueError("pcd_streams must be 1 or 2")
+        self.pcd_streams = int(pcd_streams)
         # decoding's pair ranges on their own streams (None: follow `lanes`)
         if dec_lanes is not None and int(dec_lanes) < 1:
             raise ValueError("dec_lanes must be >= 1")
@@ -572,6 +578,18 @@ class LunaTokis(nn.Module):
 
         conv = self._conv
         E = enumerate
+        # pcd_streams = 2: the DCN / feature branch (L3 DCN; L2 DCN + fea conv; L1 DCN + fea conv) on a
+        # side stream, each part forked when its offsets are ready, so it overlaps the offset convs of the
+        # next level (which depend on the offsets only) -- the under-filled L3 launches and the tails of
+        # every launch get work beside them
+        main = torch.cuda.current_stream()
+        side = self._streams(1, pool="pcd")[0] if self.pcd_streams > 1 else None
+
+        def branch():
+            if side is None:
+                return contextlib.nullcontext()
+            side.wait_stream(main)
+            return torch.cuda.stream(side)
 
         def conv_up(make, coarse, scale, epi):
             """conv on cat(x, scale * up2(coarse)) for every unit, the x2 upsample fused into the
@@ -585,7 +603,9 @@ class LunaTokis(nn.Module):
         l3off = buf(2)
         conv([dict(layer=L_(u, "L3_offset_conv2"), in0=o[i], out=l3off[i]) for i, u in E(units)], epi=L.EPI_LRELU)
         l3fea = buf(2)
-        self._dcn_sep([(f"{u[0]}L3_dcnpack_{u[1]}", l3off[i], u[2][2], l3fea[i]) for i, u in E(units)], L.EPI_LRELU)
+        with branch():
+            self._dcn_sep([(f"{u[0]}L3_dcnpack_{u[1]}", l3off[i], u[2][2], l3fea[i]) for i, u in E(units)],
+                          L.EPI_LRELU)
         # ---- L2
         o1 = buf(1)
         conv([dict(layer=L_(u, "L2_offset_conv1"), in0=u[2][1], in1=u[3][1], out=o1[i]) for i, u in E(units)],
@@ -596,10 +616,11 @@ class LunaTokis(nn.Module):
         l2off = buf(1)
         conv([dict(layer=L_(u, "L2_offset_conv3"), in0=o2[i], out=l2off[i]) for i, u in E(units)], epi=L.EPI_LRELU)
         d2 = buf(1)
-        self._dcn_sep([(f"{u[0]}L2_dcnpack_{u[1]}", l2off[i], u[2][1], d2[i]) for i, u in E(units)])
         l2fea = buf(1)
-        conv_up(lambda i, u, c: dict(layer=L_(u, "L2_fea_conv"), in0=d2[i], in1=c, out=l2fea[i]),
-                l3fea, 1.0, L.EPI_LRELU)
+        with branch():
+            self._dcn_sep([(f"{u[0]}L2_dcnpack_{u[1]}", l2off[i], u[2][1], d2[i]) for i, u in E(units)])
+            conv_up(lambda i, u, c: dict(layer=L_(u, "L2_fea_conv"), in0=d2[i], in1=c, out=l2fea[i]),
+                    l3fea, 1.0, L.EPI_LRELU)
         # ---- L1 (offset branch and DCN for the units whose fa L1 is not all zeros; k = their index)
         live = [(i, u) for i, u in E(units) if i not in zero_l1]
         d1 = buf(0)
@@ -614,15 +635,19 @@ class LunaTokis(nn.Module):
             conv([dict(layer=L_(u, "L1_offset_conv3"), in0=o2[k], out=l1off[k]) for k, (i, u) in E(live)],
                  epi=L.EPI_LRELU)
             del o1, o2
-            self._dcn_sep([(f"{u[0]}L1_dcnpack_{u[1]}", l1off[k], u[2][0], d1[i]) for k, (i, u) in E(live)])
+            with branch():
+                self._dcn_sep([(f"{u[0]}L1_dcnpack_{u[1]}", l1off[k], u[2][0], d1[i]) for k, (i, u) in E(live)])
         # the zero-state units' L1 DCN output is its bias everywhere: a constant map, kept across calls
         d1z = {}
         for i in zero_l1:
             b = L_(units[i], "L1_dcnpack").b
             d1z[i] = self._const(("dcn_bias", b.data_ptr(), n, H, Wd), lambda b=b: b.view(1, 1, 1, 64).expand(
                 n, H, Wd, 64).contiguous())
-        conv_up(lambda i, u, c: dict(layer=L_(u, "L1_fea_conv"), in0=d1z.get(i, d1[i]), in1=c, out=u[4]),
-                l2fea, 1.0, L.EPI_NONE)
+        with branch():
+            conv_up(lambda i, u, c: dict(layer=L_(u, "L1_fea_conv"), in0=d1z.get(i, d1[i]), in1=c, out=u[4]),
+                    l2fea, 1.0, L.EPI_NONE)
+        if side is not None:
+            main.wait_stream(side)   # before any buffer of this call can be freed and reused on main
 
     def _bilstm(self, X):
         return _drain(self._bilstm_steps([X[0], X[1], X[2]]))

@@ -20,6 +20,25 @@ from .coords import TABLE_ORDER, dec_tables
 # the launch stream): an object with begin(kind: tuple, flops: float) and end().
 TRACE = None
 
+# Dynamic tile scheduling of the persistent Winograd conv (stif_conv_args.sched): one block of counters
+# per (device, stream), zeroed once and kept for the process (the library tracks each block's running
+# totals) -- launches on one stream run in issue order, launches on different streams never share one.
+# Default off: at C0 the dynamic schedule measured 0.1-0.3 ms per step slower than the static one alone,
+# and equal to it with the PCD DCN branch on a second stream (profiles/r05_dynamic_tiles_ab.log).
+DYNAMIC_TILES = False
+_SCHED = {}
+
+
+def _sched_buf():
+    if not DYNAMIC_TILES or torch.cuda.is_current_stream_capturing():
+        return None
+    s = torch.cuda.current_stream()
+    key = (s.device.index, s.cuda_stream)
+    b = _SCHED.get(key)
+    if b is None:
+        b = _SCHED[key] = torch.zeros(16, dtype=torch.int32, device=s.device)   # stream-ordered before use
+    return b
+
 
 def _vp(t: Optional[torch.Tensor]):
     return None if t is None else t.data_ptr()
@@ -134,6 +153,7 @@ def conv2d(groups, *, epi=L.EPI_NONE, in1_mode=0, in1_scale=1.0, stride=None, st
         raise ValueError("conv2d: groups mix Winograd / direct or f32 / f16x3 packings")
     a.flags = L.CONV_F16X3 if lay.mode & L.PACK_F16X3 else 0
     a.status = _vp(status)
+    a.sched = _vp(_sched_buf()) if wino else None
     tr = TRACE
     if tr is not None:
         # algorithmic (direct-convolution) FLOPs, whichever algorithm runs

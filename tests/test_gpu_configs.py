@@ -175,28 +175,30 @@ def test_chunked_window_is_bit_identical(models):
 
 def test_lanes_are_bit_identical(models):
     """Lanes (concurrent streams over pair ranges, LunaTokis(lanes=)), trunk lanes (the recon trunk's
-    items over streams, trunk_lanes=), decoder lanes (dec_lanes=) and the BiConvLSTM directions on two
-    streams (lstm_lanes=2) do not change a bit: the window path
+    items over streams, trunk_lanes=), decoder lanes (dec_lanes=), the BiConvLSTM directions on two
+    streams (lstm_lanes=2) and the PCD DCN branch on a side stream (pcd_streams=2) do not change a bit:
+    the window path
     (shared boundary frames encoded per lane), the gen_feat(x) path and decoding, against one stream
     everywhere (4 lanes over 5 pairs: ranges 2, 2, 1; trunk 15 items as 8 + 7 or 5 + 5 + 5)."""
     m = models["f16x3"]
     fr = synth(20, 6, 64, 96)
     x = torch.stack([fr[:-1], fr[1:]], 1)
-    keep = (m.lanes, m.trunk_lanes, m.dec_lanes, m.lstm_lanes)
+    keep = (m.lanes, m.trunk_lanes, m.dec_lanes, m.lstm_lanes, m.pcd_streams)
     res = {}
-    combos = [(1, 1, None, 1), (2, 1, None, 1), (4, 1, None, 1), (1, 2, None, 1), (1, 3, None, 1), (2, 2, None, 1),
-              (1, 2, 2, 1), (1, 1, None, 2), (2, 2, None, 2)]
+    combos = [(1, 1, None, 1, 1), (2, 1, None, 1, 1), (4, 1, None, 1, 1), (1, 2, None, 1, 1), (1, 3, None, 1, 1),
+              (2, 2, None, 1, 1), (1, 2, 2, 1, 1), (1, 1, None, 2, 1), (2, 2, None, 2, 1), (1, 2, None, 1, 2),
+              (2, 2, None, 2, 2)]
     with torch.no_grad():
         try:
             for k in combos:
-                m.lanes, m.trunk_lanes, m.dec_lanes, m.lstm_lanes = k
+                m.lanes, m.trunk_lanes, m.dec_lanes, m.lstm_lanes, m.pcd_streams = k
                 m.gen_feat_window(fr)
                 f = m.feat.clone()
                 d = [o.clone() for o in m.decoding([0.25, 0.5])]
                 g = m(x, [0.75])[0].clone()
                 res[k] = (f, d, g)
         finally:
-            m.lanes, m.trunk_lanes, m.dec_lanes, m.lstm_lanes = keep
+            m.lanes, m.trunk_lanes, m.dec_lanes, m.lstm_lanes, m.pcd_streams = keep
     ref = res[combos[0]]
     for k in combos[1:]:
         assert torch.equal(res[k][0], ref[0]), k

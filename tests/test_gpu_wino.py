@@ -280,3 +280,45 @@ def test_wino_f16x3_range_status_single_element(stif, kind, pos):
         ops.conv2d([dict(layer=layer, in0=nhwc(xx), out=out)], epi=epi, status=st)
         assert int(st.item()) == want, (big, pos)
 
+
+
+def test_wino_dynamic_schedule_bit_identical(stif):
+    """Dynamic per-XCD tile scheduling (stif_conv_args.sched, ops.DYNAMIC_TILES) changes only which
+    workgroup computes a tile: outputs bit-identical to the static schedule, for launches with one to many
+    tiles per workgroup, back to back on one stream (each launch's counter bases come from the host's
+    running totals) and interleaved on two streams with their own counters."""
+    L, ops = stif._lib, stif.ops
+    layer = ops.pack_conv(rnd(64, 64, 3, 3, seed=21, scale=0.05), rnd(64, seed=22), L.PACK_WINO | L.PACK_F16X3)
+    shapes = [(18, 64, 64), (1, 8, 32), (5, 70, 33), (24, 128, 128)]    # 576 / 1 / 95 / 24,576 tiles
+    xs = [torch.from_numpy(rnd(n, h, w, 64, seed=30 + i)).cuda() for i, (n, h, w) in enumerate(shapes)]
+
+    def run_all(outs):
+        for x, o in zip(xs, outs):
+            ops.conv2d([dict(layer=layer, in0=x, out=o, res=x)], epi=L.EPI_RES)
+
+    keep = ops.DYNAMIC_TILES
+    try:
+        ops.DYNAMIC_TILES = False
+        ref = [torch.empty_like(x) for x in xs]
+        run_all(ref)
+        ops.DYNAMIC_TILES = True
+        for _ in range(2):
+            got = [torch.full_like(x, float("nan")) for x in xs]
+            run_all(got)
+            torch.cuda.synchronize()
+            assert all(torch.equal(a, b) for a, b in zip(got, ref))
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        g1 = [torch.full_like(x, float("nan")) for x in xs]
+        g2 = [torch.full_like(x, float("nan")) for x in xs]
+        for s in (s1, s2):
+            s.wait_stream(torch.cuda.current_stream())
+        for k in range(len(xs)):
+            for s, g in ((s1, g1), (s2, g2)):
+                with torch.cuda.stream(s):
+                    ops.conv2d([dict(layer=layer, in0=xs[k], out=g[k], res=xs[k])], epi=L.EPI_RES)
+        torch.cuda.synchronize()
+        assert all(torch.equal(a, b) for a, b in zip(g1, ref))
+        assert all(torch.equal(a, b) for a, b in zip(g2, ref))
+        assert any(int(b.sum()) > 0 for b in ops._SCHED.values())   # the counters were used
+    finally:
+        ops.DYNAMIC_TILES = keep

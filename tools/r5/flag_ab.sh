@@ -6,9 +6,9 @@ O=$R/gpurun_out/r5
 mkdir -p $O
 cd $R
 for rep in $(seq ${REPS:-3}); do
-  for v in A B C; do
+  for v in A B C D; do
     eval "f=\$FLAGS_$v"
-    [ -z "$f" ] && [ "$v" = C ] && continue
+    [ -z "$f" ] && continue
     timeout -k 10 300 python -u bench.py --no-extras --no-cpu-baseline --steps 20 $f > $O/fab.json 2> $O/fab.err \
       || { tail -30 $O/fab.err; exit 1; }
     python - "$f" <<'PY'
