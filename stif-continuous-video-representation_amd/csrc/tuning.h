@@ -14,8 +14,13 @@
 #ifndef WINO_OM_SCHED
 #define WINO_OM_SCHED 1    // a scheduling barrier after every k_wino_om B block (keeps the B loads early)
 #endif
+#ifndef WINO_UPQ
+#define WINO_UPQ 1         // fused x2 upsample expanded by 2 x 2 quads (0: per pixel, k_up2's expression)
+#endif
+static_assert(WINO_UPQ == 0 || WINO_UPQ == 1, "WINO_UPQ");
 #ifndef WINO_EXP
-#define WINO_EXP 0         // probes: 1 no LDS-DMA after the first phase, 2 no B refills, 3 no output exchange
+#define WINO_EXP 0         // probes: 1 no LDS-DMA after the first phase, 2 no B refills, 3 no output exchange,
+                           // 4 no x2-upsample expansion (in1_mode 2)
 #endif
 
 // ---- k_dcn (dcn.hip): the DCN core of the two-kernel path and the _ext drop-in at the STIF shape

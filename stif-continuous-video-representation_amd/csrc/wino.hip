@@ -180,33 +180,69 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, (int)((size_t)H * W * Cs * 4), 0x00020000);
     stage_image(rs, smem + buf * BUF_F, t.oy0 - 1, t.ox0 - 1, H, W, Cs, cbase, wi, 4, lpx, lck);
   };
-  // IN1 = 2: the staged coarse patch -> the phase image of the tile's 6 x 34 halo (zero outside the map)
+  // IN1 = 2: the staged coarse patch -> the phase image of the tile's 6 x 34 halo (zero outside the map).
+  // The halo rows / columns pair up over the coarse patch (oy0 and ox0 are even): halo rows 2 qr, 2 qr + 1
+  // (map rows 2 k + 1, 2 k + 2 with k = cy0 + qr) both interpolate coarse rows k, k + 1, with weights
+  // (0.75, 0.25) and (0.25, 0.75) -- the values F.interpolate's source coordinates give away from the
+  // borders -- and the same for columns.  So a thread takes a 2 x 2 quad of halo pixels for one 16-B
+  // channel chunk: 4 coarse reads and 8 lerps for 4 outputs (the per-pixel form needs 16 reads and 12).
+  // Quads that touch a map border (clamped source coordinates, or pixels outside the map) take the
+  // per-pixel k_up2 expression.  The scale s (2 or 1 in the model) is folded into the row weights.
+  auto expand_px = [&](const Tile& t, int r, int c, int ch) {   // k_up2's expression for one pixel
+    const int cy0 = (t.oy0 >> 1) - 1, cx0 = (t.ox0 >> 1) - 1;
+    const int Y = t.oy0 - 1 + r, X = t.ox0 - 1 + c;
+    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (((unsigned)Y < (unsigned)H) & ((unsigned)X < (unsigned)W)) {
+      const float sy = fmaxf(0.5f * ((float)Y + 0.5f) - 0.5f, 0.f);
+      const float sx = fmaxf(0.5f * ((float)X + 0.5f) - 0.5f, 0.f);
+      const int y0 = min((int)sy, h1 - 1), x0 = min((int)sx, w1 - 1);
+      const int y1 = y0 + (y0 < h1 - 1 ? 1 : 0), x1 = x0 + (x0 < w1 - 1 ? 1 : 0);
+      const float ly1 = sy - (float)y0, lx1 = sx - (float)x0;
+      const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
+      const float* s0 = scr + ((y0 - cy0) * UP_C) * 32 + ch * 4;
+      const float* s1 = scr + ((y1 - cy0) * UP_C) * 32 + ch * 4;
+      const f32x4 v00 = ld4(s0 + (x0 - cx0) * 32), v01 = ld4(s0 + (x1 - cx0) * 32);
+      const f32x4 v10 = ld4(s1 + (x0 - cx0) * 32), v11 = ld4(s1 + (x1 - cx0) * 32);
+      v = (ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11)) * a.in1_scale;
+    }
+    return v;
+  };
   auto expand = [&](const Tile& t, int buf) {
     float* dst = smem + buf * BUF_F;
     const int cy0 = (t.oy0 >> 1) - 1, cx0 = (t.ox0 >> 1) - 1;
     const float sc = a.in1_scale;
-    for (int f = tid; f < HR * HC * 8; f += 256) {
-      const int ch = f & 7, pc = f >> 3, r = pc / HC, c = pc - HC * (pc / HC);
-      const int Y = t.oy0 - 1 + r, X = t.ox0 - 1 + c;
-      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (((unsigned)Y < (unsigned)H) & ((unsigned)X < (unsigned)W)) {
-        // k_up2 (resample.hip): align_corners=False source coordinates, clamped at 0
-        const float sy = fmaxf(0.5f * ((float)Y + 0.5f) - 0.5f, 0.f);
-        const float sx = fmaxf(0.5f * ((float)X + 0.5f) - 0.5f, 0.f);
-        const int y0 = min((int)sy, h1 - 1), x0 = min((int)sx, w1 - 1);
-        const int y1 = y0 + (y0 < h1 - 1 ? 1 : 0), x1 = x0 + (x0 < w1 - 1 ? 1 : 0);
-        const float ly1 = sy - (float)y0, lx1 = sx - (float)x0;
-        const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
-        const float* s0 = scr + ((y0 - cy0) * UP_C) * 32 + ch * 4;
-        const float* s1 = scr + ((y1 - cy0) * UP_C) * 32 + ch * 4;
-        const f32x4 v00 = ld4(s0 + (x0 - cx0) * 32), v01 = ld4(s0 + (x1 - cx0) * 32);
-        const f32x4 v10 = ld4(s1 + (x0 - cx0) * 32), v11 = ld4(s1 + (x1 - cx0) * 32);
-        v = (ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11)) * sc;
+    const float w3 = 0.75f * sc, w1 = 0.25f * sc;
+    if (WINO_UPQ == 0) {   // per-pixel form (A/B reference)
+      for (int f = tid; f < HR * HC * 8; f += 256) {
+        const int ch = f & 7, pc = f >> 3, r = pc / HC, c = pc - HC * (pc / HC);
+        st4(dst + (r * OM_RP + col_slot(c) * PITCH + ch) * 4, expand_px(t, r, c, ch));
       }
-      st4(dst + (r * OM_RP + col_slot(c) * PITCH + ch) * 4, v);
+      return;
+    }
+    for (int f = tid; f < 3 * 17 * 8; f += 256) {
+      const int ch = f & 7, q = f >> 3, qr = q / 17, qc = q - 17 * (q / 17);
+      const int k = cy0 + qr, m = cx0 + qc;   // coarse rows k, k + 1 and columns m, m + 1
+      float* d0 = dst + ((2 * qr) * OM_RP + col_slot(2 * qc) * PITCH + ch) * 4;
+      float* d1 = dst + ((2 * qr) * OM_RP + col_slot(2 * qc + 1) * PITCH + ch) * 4;
+      if (((unsigned)k < (unsigned)(h1 - 1)) & ((unsigned)m < (unsigned)(w1 - 1))) {
+        const float* s0 = scr + ((qr * UP_C + qc) * 8 + ch) * 4;
+        const f32x4 v00 = ld4(s0), v01 = ld4(s0 + 32), v10 = ld4(s0 + UP_C * 32), v11 = ld4(s0 + UP_C * 32 + 32);
+        // columns: b = 0 (map column 2 m + 1) weights (0.75, 0.25), b = 1 (2 m + 2) (0.25, 0.75)
+        const f32x4 t00 = 0.75f * v00 + 0.25f * v01, t01 = 0.25f * v00 + 0.75f * v01;
+        const f32x4 t10 = 0.75f * v10 + 0.25f * v11, t11 = 0.25f * v10 + 0.75f * v11;
+        st4(d0, w3 * t00 + w1 * t10);
+        st4(d1, w3 * t01 + w1 * t11);
+        st4(d0 + OM_RP * 4, w1 * t00 + w3 * t10);
+        st4(d1 + OM_RP * 4, w1 * t01 + w3 * t11);
+      } else {
+        st4(d0, expand_px(t, 2 * qr, 2 * qc, ch));
+        st4(d1, expand_px(t, 2 * qr, 2 * qc + 1, ch));
+        st4(d0 + OM_RP * 4, expand_px(t, 2 * qr + 1, 2 * qc, ch));
+        st4(d1 + OM_RP * 4, expand_px(t, 2 * qr + 1, 2 * qc + 1, ch));
+      }
     }
   };
-  auto up_phase = [&](int p) { return IN1 == 2 && p * PSUB >= NC0; };
+  auto up_phase = [&](int p) { return IN1 == 2 && WINO_EXP != 4 && p * PSUB >= NC0; };
 
   // rows of the 4x4 patch feeding transform row i: (B^T d)_i = d[rA] + sB * d[rB]
   const int rA = (wi == 0) ? 0 : (wi == 2 ? 2 : 1);
