@@ -110,9 +110,17 @@ __host__ __device__ __forceinline__ float stif_sin_poly(float x) {
   const float v = (qi & 1) ? pc : ps;
   return (qi & 2) ? -v : v;
 }
+// The hardware sine reduces its argument itself, exactly: v_sin_f32 of x and of x - rint(x) have the same
+// maximum error against sin(2 pi x) -- 1.1-1.3e-7 in every band from |x| <= 0.5 to |x| <= 1e7 revolutions, 6-34 %
+// of results one ulp apart (tools/r5/vsin_reduce.hip, profiles/r05_sin_raw.log) -- so the f16x3 decoder skips the
+// two-instruction reduction (DEC_SIN_RAW = 1).
+#ifndef DEC_SIN_RAW
+#define DEC_SIN_RAW 1
+#endif
 template <int F16>
 STIF_DEV float siren_sin(float x) {
-  if constexpr (F16) return stif_sin_rev(x);
+  if constexpr (F16 && DEC_SIN_RAW) return __builtin_amdgcn_sinf(x);
+  else if constexpr (F16) return stif_sin_rev(x);
   else return stif_sin_poly(x);
 }
 
