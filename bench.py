@@ -108,9 +108,11 @@ class KernelTimer:
     kinds = None
 
     def begin(self, kind, flops, nbytes=0.0):
+        base = tuple(kind)
         if self.main is not None and torch.cuda.current_stream() != self.main:
-            kind = tuple(kind) + ("lane",)
-        if self.kind is None or kind == self.kind:
+            kind = base + ("lane",)
+        # a named kind is timed on whichever stream it is launched (the events record on that stream)
+        if self.kind is None or kind == self.kind or base == tuple(self.kind):
             self.seen += 1
             if (self.seen - 1) % self.every:
                 return
@@ -141,8 +143,12 @@ class KernelTimer:
         return agg
 
     def dominant(self):
-        """the launch kind with the largest total time (launches on the main stream)"""
-        return max(((k, v) for k, v in self.per_kind().items() if k[-1] != "lane"), key=lambda kv: kv[1][1])[0]
+        """the launch kind with the largest total time (launches on the main stream; run_config probes a
+        single-stream step, so every launch is there; with none, any stream; ("none",) for an empty probe)"""
+        agg = self.per_kind()
+        main = {k: v for k, v in agg.items() if k[-1] != "lane"} or {k[:-1] if k[-1] == "lane" else k: v
+                                                                    for k, v in agg.items()}
+        return max(main.items(), key=lambda kv: kv[1][1])[0] if main else ("none",)
 
     def report(self):
         """per-kind launches / avg us / TFLOP/s (all-kinds mode); kinds tagged 'lane' ran on a side stream
@@ -192,7 +198,7 @@ def roofline(kname, kdesc, dom, peak_tflops, achieved_tflops, avg_ms, avg_flops,
 
 def kernel_table(probe, mfma, top=4):
     """The `top` launch kinds of one step by total time (HIP events on the launch stream, one untimed
-    step): launches, avg us, share of the step's main-stream kernel time, and each kind's roofline fraction on the
+    step, single-stream): launches, avg us, share of the step's kernel time, and each kind's roofline fraction on the
     bound its intensity picks (roofline())."""
     # launches on the model's side streams (the trunk lanes) overlap each other, so their event intervals
     # are not kernel times: left out here (their kernel times are in the rocprof summary)
@@ -291,7 +297,7 @@ CPU_SAMPLE = 96   # LR crop of the CPU-baseline sample (FLOP per output pixel do
 
 def _oracle_timed(threads=None):
     """time the numpy oracle on the sample pair (frames 0-1 of the window cropped to CPU_SAMPLE^2,
-    4x, t = 0.5); threads=None: every host BLAS thread"""
+    4x, t = 0.5); threads=None: the process's BLAS pool as configured"""
     from oracle import stif_oracle as O
     sd = __import__("stif_pkg").load().weights.make_state_dict(seed=0)
     x = np.ascontiguousarray(synth_frames(0, 2, 128, 128, "cpu")[:, :, :CPU_SAMPLE, :CPU_SAMPLE].numpy()[None])
@@ -315,7 +321,8 @@ def _pinned_child():
 
 def cpu_baseline():
     """The numpy oracle (fp32) on a bounded sample of the same workload -- one pair of the window
-    cropped to CPU_SAMPLE x CPU_SAMPLE LR pixels, 4x, t = 0.5 -- on all host BLAS threads, and again
+    cropped to CPU_SAMPLE x CPU_SAMPLE LR pixels, 4x, t = 0.5 -- on the process's BLAS pool (its thread
+    count stated as `cores`, next to the host's CPU count and the process affinity), and again
     in a child process pinned to 8 cores (the survey container's count, where the reference's own torch
     CPU path was timed).  The child is a fresh interpreter that never touches the GPU."""
     import subprocess
@@ -330,9 +337,16 @@ def cpu_baseline():
         print(f"pinned CPU baseline failed: {e}", file=sys.stderr)
     sample = (f"1 pair (frames 0-1) of the window cropped to {CPU_SAMPLE}x{CPU_SAMPLE} -> {4 * CPU_SAMPLE}x"
               f"{4 * CPU_SAMPLE}, t=0.5, numpy fp32 restatement (oracle/stif_oracle.py)")
-    rec = {"value": round(mpix / dt, 6), "unit": "Mpix/s", "cores": _threads(), "kind": "port",
-           "sample": f"{sample}, {dt:.1f} s on all host threads", "cpu_model": cpu_model(),
-           "host_cpus": os.cpu_count(),
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    nthr = _threads()
+    rec = {"value": round(mpix / dt, 6), "unit": "Mpix/s", "cores": nthr, "kind": "port",
+           "sample": f"{sample}, {dt:.1f} s on {nthr} BLAS threads",
+           "threads_note": "the BLAS pool the process was given (OMP_NUM_THREADS: the GPU box's per-GPU CPU share, "
+                           "16, which the pool's rules say to leave as set), not every CPU of the host",
+           "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "affinity_cpus": affinity,
            "pinned_8_cores": None if pinned is None else {
                "value": round(mpix / pinned, 6), "unit": "Mpix/s", "cores": 8, "seconds": round(pinned, 2),
                "how": "child process, sched_setaffinity CPUs 0-7 (as taskset -c 0-7), 8 BLAS threads"},
@@ -418,11 +432,25 @@ def run_config(stif, sd, cfg, args, world, rank, device, dist, mfma, trace_dom=T
             return None
         return model.decoding(tq, None if scale == 4.0 else (HH, WW))
 
+    # the kernel-table probe (the last warm-up step) runs every launch on one stream: outputs are bit-identical
+    # for any lane setting, and HIP-event intervals of launches overlapping on side streams are not kernel times
+    knobs = ("lanes", "trunk_lanes", "dec_lanes", "lstm_lanes", "pcd_streams")
     with torch.no_grad():
         probe = KernelTimer(None)
         for i in range(max(1, args.warmup)):
-            stif.ops.TRACE = probe if (trace_dom and i == max(1, args.warmup) - 1) else None
             step()
+        if trace_dom:   # one more untimed step, single-stream, traced
+            keep = {k: getattr(model, k) for k in knobs}
+            for k in knobs:
+                setattr(model, k, 1)
+            stif.ops.TRACE = probe
+            try:
+                step()
+            finally:
+                stif.ops.TRACE = None
+                for k, v in keep.items():
+                    setattr(model, k, v)
+            step()   # and the timed configuration once more, so the timed region starts warm
         stif.ops.TRACE = None
         torch.cuda.synchronize()
         timer = KernelTimer(probe.dominant() if (trace_dom and probe.rec) else ("none",), every=args.time_every)

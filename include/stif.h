@@ -74,12 +74,14 @@ typedef struct {
   int* status;             /* optional device word (NULL = none): with STIF_CONV_F16X3, set to 1 when an output
                               element is not finite before its activation -- the signature of an activation
                               outside the split-fp16 operand range (see STIF_CONV_F16X3) */
-  int* sched;              /* optional device block of 8 ints, zero when first used (stif_conv3x3_wino, STIF_CONV_F16X3
-                              launches; ignored otherwise): per-XCD tile counters of the persistent kernel's dynamic
+  int* sched;              /* device block of 8 ints, zero when first used, read only with flags & STIF_CONV_DYNAMIC
+                              (stif_conv3x3_wino, STIF_CONV_F16X3 launches; ignored otherwise, and ignored while the
+                              stream is capturing a graph): per-XCD tile counters of the persistent kernel's dynamic
                               schedule.  The library keeps each block's running totals on the host, so the launches
                               that use one block must run in issue order (one stream) and the block must not be
-                              freed and re-allocated while the library is loaded.  NULL = static schedule.
-                              Outputs are identical either way. */
+                              freed and re-allocated while the library is loaded.  Outputs are identical either way.
+                              Zero-initialise the whole struct: fields added at its end keep their old meaning
+                              only when zero. */
 } stif_conv_args;
 
 /* stif_conv_args.flags: fp32 products on the fp16 MFMA pipe by 3-term operand splitting (x = h + l,
@@ -89,6 +91,9 @@ typedef struct {
  * outside it, and an activation outside it turns the outputs it feeds into NaN/inf, which the
  * kernels report through the `status` word (the host then re-runs the call in fp32). */
 #define STIF_CONV_F16X3 1
+/* stif_conv_args.flags: take the persistent Winograd conv's tiles from the per-XCD counters in `sched`
+ * (dynamic schedule) instead of the static stride; without this bit `sched` is never read. */
+#define STIF_CONV_DYNAMIC 2
 
 int stif_conv2d_nhwc(const stif_conv_args* args, void* stream);
 

@@ -16,6 +16,7 @@ EPI_NONE, EPI_LRELU, EPI_RELU, EPI_RES, EPI_OFFMASK, EPI_LSTM = range(6)
 PACK_PLAIN, PACK_OFFMASK, PACK_LSTM, PACK_WINO, PACK_WINO_OFFMASK, PACK_WINO_LSTM, PACK_DCNSEP, PACK_DCNPAIR = range(8)
 PACK_F16X3 = 16          # OR'ed into a PACK_WINO* mode (stif.h STIF_PACK_F16X3)
 CONV_F16X3 = 1           # stif_conv_args.flags
+CONV_DYNAMIC = 2         # stif_conv_args.flags: dynamic tile schedule (sched counters)
 DEC_REVOLUTIONS = 2      # stif_pack_dec_proj_ex lr_image bit (stif.h STIF_DEC_REVOLUTIONS)
 
 _P = C.c_void_p

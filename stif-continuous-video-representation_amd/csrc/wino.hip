@@ -797,6 +797,13 @@ void sched_advance(const int* key, int ntiles, int grid, SchedBase& sb) {
   }
 }
 
+// a launch that failed after sched_advance: restore the totals it started from
+void sched_undo(const int* key, const SchedBase& sb) {
+  std::lock_guard<std::mutex> lk(g_sched_mu);
+  std::array<unsigned, 8>& tot = g_sched[key];
+  for (int x = 0; x < 8; ++x) tot[x] = sb.b[x];
+}
+
 template <int IN1, int EPI>
 int launch(const stif_conv_args& a, hipStream_t st) {
   const long long tiles =
@@ -812,12 +819,21 @@ int launch(const stif_conv_args& a, hipStream_t st) {
   }
   const int grid = 8 * (int)std::min<long long>((tiles + 7) / 8, (long long)WG_PER_CU * stif_num_cus() / 8);
   SchedBase sb{};
-  if (a.sched && (a.flags & STIF_CONV_F16X3)) sched_advance(a.sched, (int)tiles, grid, sb);
+  // the dynamic schedule only on request (flag bit and block), and never inside a graph capture: a replayed
+  // launch would find the counters past the bases the host recorded for it
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  const bool dyn = a.sched && (a.flags & STIF_CONV_DYNAMIC) && (a.flags & STIF_CONV_F16X3) &&
+                   hipStreamIsCapturing(st, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone;
+  stif_conv_args ka = a;
+  if (!dyn) ka.sched = nullptr;
+  if (dyn) sched_advance(a.sched, (int)tiles, grid, sb);
   if (a.flags & STIF_CONV_F16X3)
-    hipLaunchKernelGGL((k_wino<IN1, EPI, 1>), dim3(grid), dim3(256), 0, st, a, (int)tiles, sb);
+    hipLaunchKernelGGL((k_wino<IN1, EPI, 1>), dim3(grid), dim3(256), 0, st, ka, (int)tiles, sb);
   else
-    hipLaunchKernelGGL((k_wino<IN1, EPI, 0>), dim3(grid), dim3(256), 0, st, a, (int)tiles, sb);
-  return stif_check_launch("stif_conv3x3_wino");
+    hipLaunchKernelGGL((k_wino<IN1, EPI, 0>), dim3(grid), dim3(256), 0, st, ka, (int)tiles, sb);
+  const int rc = stif_check_launch("stif_conv3x3_wino");
+  if (rc != STIF_OK && dyn) sched_undo(a.sched, sb);   // the kernel never ran: the counters did not move
+  return rc;
 }
 
 }  // namespace

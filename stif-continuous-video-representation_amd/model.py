@@ -20,6 +20,7 @@ from __future__ import annotations
 import contextlib
 import math
 import warnings
+import threading
 from collections import OrderedDict
 
 import numpy as np
@@ -30,6 +31,8 @@ from . import _lib as L
 from . import ops
 from . import weights as W
 from .coords import ensemble_weights
+
+_CONST_LOCK = threading.Lock()   # _const's dict is shared by DataParallel replicas (replicate() threads)
 
 
 def _np(v):
@@ -63,7 +66,7 @@ class LunaTokis(nn.Module):
 
     def __init__(self, nf=64, nframes=3, groups=8, front_RBs=5, back_RBs=10, device="cuda", winograd=True,
                  mfma="f16x3", range_check="rerun", chunk_px=2 ** 21, lanes=1, dec_chunk_px=2 ** 25,
-                 fused_dcn=True, trunk_lanes=2, dec_lanes=None, lstm_lanes=1, pcd_streams=1):
+                 fused_dcn=True, trunk_lanes=2, dec_lanes=None, lstm_lanes=1, pcd_streams=1, const_shapes=2):
         super().__init__()
         if nf != 64 or groups != 8:
             raise ValueError("the gfx950 kernels implement nf=64, groups=8 (the shipped STIF configuration)")
@@ -146,6 +149,10 @@ class LunaTokis(nn.Module):
         self.dec_lanes = None if dec_lanes is None else int(dec_lanes)
         self._lane_streams = {}
         self._active = False
+        # weight-only constant maps (_const) are kept for this many (items, H, W) shapes per device
+        if int(const_shapes) < 1:
+            raise ValueError("const_shapes must be >= 1")
+        self.const_shapes = int(const_shapes)
 
     # ------------------------------------------------------------------ nn.Module API
     @property
@@ -161,7 +168,13 @@ class LunaTokis(nn.Module):
         device, dtype, _, _ = torch._C._nn._parse_to(*args, **kwargs)
         if dtype is not None and dtype != torch.float32:
             raise NotImplementedError("LunaTokis (stif_amd) computes in fp32 (operand modes: mfma='f32'|'f16x3')")
-        return super().to(*args, **kwargs)
+        out = super().to(*args, **kwargs)
+        with _CONST_LOCK:   # the constant maps of the device the module left are not used again
+            consts = self.__dict__.get("_consts")
+            if consts:
+                for g in [g for g in consts if g[0] != str(self.device)]:
+                    del consts[g]
+        return out
 
     def half(self):
         raise NotImplementedError("LunaTokis (stif_amd) computes in fp32")
@@ -286,7 +299,7 @@ class LunaTokis(nn.Module):
         self._meta32 = None
         self._layers_key = None
         self._tables = {}
-        self._consts = {}
+        self._consts = OrderedDict()
 
     def _pack_mlp(self, flags):
         """All SIREN layers (stif_pack_dec_mlp_ex); an out-of-range weight for f16x3 -> fp32 packing."""
@@ -434,23 +447,42 @@ class LunaTokis(nn.Module):
     def _empty(self, *shape):
         return torch.empty(*shape, device=self.device, dtype=torch.float32)
 
-    def _const(self, key, make):
+    def _const(self, key, shape, make):
         """Maps that depend only on the packed weights and a shape (the all-zero initial state, its
         pyramids, the zero-state L1 DCN output), computed on first use and kept until the layers are
-        re-packed; the key holds the weight buffers' addresses, so the fp32 range re-run's layers get
-        their own entries.  Not cached inside a hipGraph capture (computed in the graph instead)."""
-        if torch.cuda.is_current_stream_capturing():
+        re-packed.  Entries are grouped by (device, shape): the key holds the weight buffers' addresses
+        (so the fp32 range re-run's layers get their own entries) and the device is part of every
+        group, so DataParallel replicas -- which share this dict through replicate()'s shallow
+        __dict__ copy -- and a module moved by .to() never receive another device's tensors.  At most
+        ``const_shapes`` groups per device are kept (least recently used evicted): one C0 group is
+        ~0.1 GB, a 720p / 1080p group ~1.7 / 2 GB, so a serving process that sees many resolutions
+        holds at most two of them.  Not cached inside a hipGraph capture (computed in the graph)."""
+        if self.device.type == "cuda" and torch.cuda.is_current_stream_capturing():
             return make()
-        consts = self.__dict__.setdefault("_consts", {})
-        v = consts.get(key)
-        if v is None:
-            v = consts[key] = make()
-            if self.device.type == "cuda":   # once: other streams (lanes) read it without an event
-                torch.cuda.current_stream(self.device).synchronize()
+        dev = str(self.device)
+        grp = (dev,) + tuple(int(s) for s in shape)
+        with _CONST_LOCK:
+            consts = self.__dict__.get("_consts")
+            if not isinstance(consts, OrderedDict):
+                consts = self.__dict__["_consts"] = OrderedDict()
+            ent = consts.get(grp)
+            if ent is not None and key in ent:
+                consts.move_to_end(grp)
+                return ent[key]
+        v = make()
+        if self.device.type == "cuda":   # once: other streams (lanes) read it without an event
+            torch.cuda.current_stream(self.device).synchronize()
+        with _CONST_LOCK:
+            consts.setdefault(grp, {})[key] = v
+            consts.move_to_end(grp)
+            mine = [g for g in consts if g[0] == dev]
+            for g in mine[:max(0, len(mine) - max(1, self.const_shapes))]:
+                del consts[g]
         return v
 
     def _zeros(self, *shape):
-        return self._const(("zeros",) + tuple(shape),
+        # grouped with the other maps of the same (items, H, W)
+        return self._const(("zeros",) + tuple(shape), shape[:3],
                            lambda: torch.zeros(*shape, device=self.device, dtype=torch.float32))
 
     def _frame_features(self, frames):
@@ -641,7 +673,7 @@ class LunaTokis(nn.Module):
         d1z = {}
         for i in zero_l1:
             b = L_(units[i], "L1_dcnpack").b
-            d1z[i] = self._const(("dcn_bias", b.data_ptr(), n, H, Wd), lambda b=b: b.view(1, 1, 1, 64).expand(
+            d1z[i] = self._const(("dcn_bias", b.data_ptr()), (n, H, Wd), lambda b=b: b.view(1, 1, 1, 64).expand(
                 n, H, Wd, 64).contiguous())
         with branch():
             conv_up(lambda i, u, c: dict(layer=L_(u, "L1_fea_conv"), in0=d1z.get(i, d1[i]), in1=c, out=u[4]),
@@ -672,8 +704,8 @@ class LunaTokis(nn.Module):
             return (xp2 if level == 2 else xp3)[p * 3 + fr]
 
         # the step-0 state pyramids (zeros) once per pcd, depending on the weights only: kept across calls
-        zkey = ("zero_pyr", lay[pcds[0] + "fea_L2_conv1"].w.data_ptr(), B, H, Wd)
-        z2, z3 = self._const(zkey, lambda: self._pyramid([(zero, pcds[p]) for p in range(2)]))
+        zkey = ("zero_pyr", lay[pcds[0] + "fea_L2_conv1"].w.data_ptr())
+        z2, z3 = self._const(zkey, (B, H, Wd), lambda: self._pyramid([(zero, pcds[p]) for p in range(2)]))
 
         def step(t, ds):
             """Step t of the directions ds (0 forward, 1 reversed): state pyramids, PCD alignments,

@@ -153,7 +153,10 @@ def conv2d(groups, *, epi=L.EPI_NONE, in1_mode=0, in1_scale=1.0, stride=None, st
         raise ValueError("conv2d: groups mix Winograd / direct or f32 / f16x3 packings")
     a.flags = L.CONV_F16X3 if lay.mode & L.PACK_F16X3 else 0
     a.status = _vp(status)
-    a.sched = _vp(_sched_buf()) if wino else None
+    sched = _sched_buf() if wino else None
+    a.sched = _vp(sched)
+    if sched is not None:
+        a.flags |= L.CONV_DYNAMIC
     tr = TRACE
     if tr is not None:
         # algorithmic (direct-convolution) FLOPs, whichever algorithm runs

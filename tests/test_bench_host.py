@@ -59,3 +59,16 @@ def test_gratings_ground_truth_is_the_pattern(bench):
     gt = bench.gratings_gt(3, 1.0, 16, 24, 16, 24)
     assert np.allclose(gt, fr[1], atol=1e-6)
     assert 0.0 <= fr.min() and fr.max() <= 1.0
+
+
+def test_dominant_kind_is_robust_to_side_streams(bench):
+    """KernelTimer.dominant (advisor r5): main-stream kinds first; a probe whose launches all ran on side
+    streams still names a kernel (tag stripped); an empty probe gives ("none",) instead of raising."""
+    t = bench.KernelTimer.__new__(bench.KernelTimer)
+    t.per_kind = lambda: {("wino", 3): [2, 5.0, 1.0, 1.0], ("dcnsep", 0, "lane"): [1, 9.0, 1.0, 1.0],
+                          ("dec2",): [1, 3.0, 1.0, 1.0]}
+    assert t.dominant() == ("wino", 3)
+    t.per_kind = lambda: {("wino", 3, "lane"): [2, 5.0, 1.0, 1.0], ("dcnsep", 0, "lane"): [1, 9.0, 1.0, 1.0]}
+    assert t.dominant() == ("dcnsep", 0)
+    t.per_kind = lambda: {}
+    assert t.dominant() == ("none",)

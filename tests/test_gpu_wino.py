@@ -320,5 +320,20 @@ def test_wino_dynamic_schedule_bit_identical(stif):
         assert all(torch.equal(a, b) for a, b in zip(g1, ref))
         assert all(torch.equal(a, b) for a, b in zip(g2, ref))
         assert any(int(b.sum()) > 0 for b in ops._SCHED.values())   # the counters were used
+        # a block passed without the STIF_CONV_DYNAMIC flag bit is never read or written (advisor r5: a caller
+        # that leaves the trailing field uninitialised must not get the dynamic schedule)
+        s3 = torch.cuda.Stream()
+        s3.wait_stream(torch.cuda.current_stream())
+        keep_flag = L.CONV_DYNAMIC
+        L.CONV_DYNAMIC = 0
+        try:
+            with torch.cuda.stream(s3):
+                g3 = [torch.full_like(x, float("nan")) for x in xs]
+                run_all(g3)
+        finally:
+            L.CONV_DYNAMIC = keep_flag
+        torch.cuda.synchronize()
+        assert all(torch.equal(a, b) for a, b in zip(g3, ref))
+        assert int(ops._SCHED[(s3.device.index, s3.cuda_stream)].abs().sum()) == 0
     finally:
         ops.DYNAMIC_TILES = keep

@@ -80,3 +80,39 @@ def test_model_packs_out_of_range_layers_in_fp32(stif, sd):
     assert lay["recon_trunk.7.conv2"].mode == L.PACK_WINO
     assert lay["recon_trunk.7.conv1"].mode == L.PACK_WINO | L.PACK_F16X3
     assert m._dec_flags == 0 and m._meta["dec.mlp"][1] == 0
+
+
+def test_const_cache_is_device_scoped_and_bounded(stif, cpu_model):
+    """_const (the weight-only constant maps): entries are grouped by (device, shape), at most
+    const_shapes groups per device are kept (least recently used evicted), a replica sharing the dict
+    on another device never receives this device's tensors, and .to() drops the groups of the device
+    the module left (advisor r5)."""
+    import copy
+    m = cpu_model
+    m._consts.clear()
+    calls = []
+
+    def mk(tag):
+        calls.append(tag)
+        return torch.full((1,), float(len(calls)))
+
+    a = m._const(("k", 1), (2, 8, 8), lambda: mk("a"))
+    assert m._const(("k", 1), (2, 8, 8), lambda: mk("x")) is a and calls == ["a"]
+    m._const(("k", 1), (2, 16, 16), lambda: mk("b"))
+    m._const(("k", 1), (2, 8, 8), lambda: mk("y"))          # hit: (2, 8, 8) becomes most recent
+    m._const(("k", 1), (2, 32, 32), lambda: mk("c"))        # third shape: evicts (2, 16, 16)
+    assert calls == ["a", "b", "c"] and list(m._consts) == [("cpu", 2, 8, 8), ("cpu", 2, 32, 32)]
+    assert m._zeros(2, 8, 8, 64).shape == (2, 8, 8, 64) and ("zeros", 2, 8, 8, 64) in m._consts[("cpu", 2, 8, 8)]
+    # a replica whose device differs (DataParallel shares __dict__ entries shallowly): its own group
+    class OnMeta(type(m)):
+        device = property(lambda self: torch.device("meta"))
+
+    rep = copy.copy(m)
+    rep.__class__ = OnMeta
+    assert rep._consts is m._consts
+    r = rep._const(("k", 1), (2, 8, 8), lambda: mk("rep"))
+    assert r is not a and calls[-1] == "rep" and ("meta", 2, 8, 8) in m._consts
+    m.to("cpu")                                                # leaving "meta"-device entries behind
+    assert all(g[0] == "cpu" for g in m._consts)
+    with pytest.raises(ValueError):
+        stif.LunaTokis(64, 6, 8, 5, 40, device="cpu", const_shapes=0)
