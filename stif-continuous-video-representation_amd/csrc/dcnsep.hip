@@ -90,6 +90,10 @@ STIF_DEV void wait_vm(int n) {
 template <int EPI>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_WPE))) void k_dcn_sep(stif_dcn_sep_args a) {
   __shared__ __attribute__((aligned(16))) float smem[LDS_F];
+#if DCNSEP_SOLO   // diagnostic: 48 KB of unused LDS, so only one workgroup fits on a CU
+  __shared__ float solo_pad[12288];
+  if (a.H < 0) reinterpret_cast<volatile float*>(solo_pad)[threadIdx.x] = 0.f;
+#endif
   const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, hf = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = a.H, W = a.W;
@@ -200,6 +204,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_
       // the next two steps too.  Every LDS read of the step that frees a ring slot has returned (its
       // MFMAs consumed it), and LDS-DMA visibility is the vmcnt wait above.
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#if DCNSEP_P1_SAFE   // diagnostic: every phase-1 step behind a full drain (vmcnt(0) lgkmcnt(0)) and __syncthreads
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+#endif
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       // the first weight fragments right after the barrier; this step's data fragment was read and split
@@ -224,7 +232,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_
         om[q] = mfma16h(wh[q & 1], dl, om[q]);
         om[q] = mfma16h(wl[q & 1], dh, om[q]);
         if (q == 0) {
-          if (t < 7 || c < 3) stage_w(k + 2, (t + 2) % RING);
+          if ((t < 7 || c < 3) && DCNSEP_EXP != 7) stage_w(k + 2, (t + 2) % RING);
           if (t == 1) {
             if (c < 3) stage_data(c + 1, smem + (((c + 1) & 1) ? OFF_D1 : OFF_D0));
             else if (PAIR_AHEAD) stage_pair(0, smem + OFF_XT, smem + OFF_XW);   // D0 is free: chunk 2 is done
@@ -320,6 +328,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_
       acc1[r] = b1;
     }
   }
+#if DCNSEP_TP_CHECK
+  int tp_bad = 0, tp_badw = 0, tp_first = -1, tp_tap = 0;
+#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // pair 0 staged (NW 8) and the om biases loaded
   __syncthreads();                                    // phase-1 buffers free
 #pragma unroll
@@ -347,6 +358,128 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_
     }
     const float* st = smem + ((PAIR_AHEAD && (pa & 1)) ? OFF_YT : OFF_XT);
     const float* sw = smem + ((PAIR_AHEAD && (pa & 1)) ? OFF_YW : OFF_XW);
+#if DCNSEP_TAPPIPE
+    // diagnostic variant (round-5 review item 4): tap t + 1's eight corner reads issued before tap t's blend
+    struct Samp {
+      f32x4 v[8];
+      float w1, w2, w3, w4;
+      int h_low, w_low;
+      bool fb;
+      bool it;
+    };
+    auto prep = [&](int tap, float dy, float dx, float mk, Samp& o) {
+      const int ky = tap / 3, kx = tap - 3 * ky;
+      const float h_im = (float)(oy - 1 + ky) + dy;
+      const float w_im = (float)(ox - 1 + kx) + dx;
+      const bool valid = pix_ok & (h_im > -1.f) & (w_im > -1.f) & (h_im < (float)H) & (w_im < (float)W);
+      const float fh = floorf(h_im), fw = floorf(w_im);
+      const float lh = h_im - fh, lw = w_im - fw, hh = 1.f - lh, hw = 1.f - lw;
+      o.h_low = (int)fh;
+      o.w_low = (int)fw;
+      const int r0 = o.h_low - ty0, c0 = o.w_low - tx0;
+      const bool in_tile = ((unsigned)r0 < (unsigned)(TR - 1)) & ((unsigned)c0 < (unsigned)(TC - 1));
+      const float m = valid ? mk : 0.f;
+      const float hm = hh * m, lm = lh * m;
+      o.w1 = hm * hw;
+      o.w2 = hm * lw;
+      o.w3 = lm * hw;
+      o.w4 = lm * lw;
+      o.fb = DCNSEP_TP_NOFB ? false : (valid & !in_tile);
+      o.it = in_tile;
+      const float* p0 = st + (((in_tile ? r0 : 0) * 4 + 2 * hf) * TP + (in_tile ? c0 : 0)) * 4;
+      const float* p1 = p0 + 4 * TP * 4;
+      o.v[0] = ld4(p0);
+      o.v[1] = ld4(p0 + 4);
+      o.v[2] = ld4(p1);
+      o.v[3] = ld4(p1 + 4);
+      o.v[4] = ld4(p0 + TP * 4);
+      o.v[5] = ld4(p0 + TP * 4 + 4);
+      o.v[6] = ld4(p1 + TP * 4);
+      o.v[7] = ld4(p1 + TP * 4 + 4);
+    };
+    auto finish = [&](const Samp& o, f32x4& a0, f32x4& a1) {
+#if DCNSEP_TP_CHECK
+      // diagnostic guard: every staged corner this lane read from LDS against the input map in HBM
+      if (o.it) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int y = o.h_low + ((k >> 1) & 1), x = o.w_low + (k & 1), qd = 2 * hf + (k >> 2);
+          const bool inimg = ((unsigned)y < (unsigned)H) & ((unsigned)x < (unsigned)W);
+          const f32x4 g = inimg ? ld4(in + ((size_t)y * W + x) * 64 + pa * 16 + qd * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (__builtin_bit_cast(unsigned, g[e]) != __builtin_bit_cast(unsigned, o.v[k][e])) {
+              ++tp_bad;
+              if (tp_first < 0) tp_first = (pa * 16 + tp_tap) * 8 + k;
+            }
+        }
+      }
+#endif
+      a0 = o.w1 * o.v[0] + o.w2 * o.v[1] + o.w3 * o.v[2] + o.w4 * o.v[3];
+      a1 = o.w1 * o.v[4] + o.w2 * o.v[5] + o.w3 * o.v[6] + o.w4 * o.v[7];
+      if (__builtin_amdgcn_ballot_w64(o.fb)) {
+        if (o.fb) {
+          const int h_low = o.h_low, w_low = o.w_low, h_high = h_low + 1, w_high = w_low + 1, co = pa * 16 + hf * 8;
+          const bool b1 = h_low >= 0 && w_low >= 0, b2 = h_low >= 0 && w_high <= W - 1;
+          const bool b3 = h_high <= H - 1 && w_low >= 0, b4 = h_high <= H - 1 && w_high <= W - 1;
+          const float* q1 = in + ((size_t)h_low * W + w_low) * 64 + co;
+          const float* q2 = in + ((size_t)h_low * W + w_high) * 64 + co;
+          const float* q3 = in + ((size_t)h_high * W + w_low) * 64 + co;
+          const float* q4 = in + ((size_t)h_high * W + w_high) * 64 + co;
+          const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+          a0 = o.w1 * (b1 ? ld4(q1) : z) + o.w2 * (b2 ? ld4(q2) : z) + o.w3 * (b3 ? ld4(q3) : z) +
+               o.w4 * (b4 ? ld4(q4) : z);
+          a1 = o.w1 * (b1 ? ld4(q1 + 4) : z) + o.w2 * (b2 ? ld4(q2 + 4) : z) + o.w3 * (b3 ? ld4(q3 + 4) : z) +
+               o.w4 * (b4 ? ld4(q4 + 4) : z);
+        }
+      }
+    };
+    Samp cur, nxt;
+    {
+      const int s = 27 * pa;
+      prep(0, om[s / 16][s % 16], om[(s + 1) / 16][(s + 1) % 16], om[(s + 2) / 16][(s + 2) % 16], cur);
+    }
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const float* wp = sw + t * 1024 + lane * 4;
+      const f16x8 bh0 = ldh8(wp), bl0 = ldh8(wp + 256), bh1 = ldh8(wp + 512), bl1 = ldh8(wp + 768);
+      if (t < 8) {
+        const int s = 27 * pa + 3 * (t + 1);
+        prep(t + 1, om[s / 16][s % 16], om[(s + 1) / 16][(s + 1) % 16], om[(s + 2) / 16][(s + 2) % 16], nxt);
+      }
+      if (DCNSEP_TP_WAIT) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      f32x4 a0, a1;
+#if DCNSEP_TP_CHECK
+      tp_tap = t;
+      {   // the B fragments of this tap against the packed weights in HBM
+        const float* gw = wt + (size_t)pa * WP_F + t * 1024 + lane * 4;
+        const f16x8 g0 = ldh8(gw), g1 = ldh8(gw + 256), g2 = ldh8(gw + 512), g3 = ldh8(gw + 768);
+        typedef unsigned u32x4c __attribute__((ext_vector_type(4)));
+        const u32x4c d = __builtin_bit_cast(u32x4c, g0) ^ __builtin_bit_cast(u32x4c, bh0);
+        const u32x4c d1 = __builtin_bit_cast(u32x4c, g1) ^ __builtin_bit_cast(u32x4c, bl0);
+        const u32x4c d2 = __builtin_bit_cast(u32x4c, g2) ^ __builtin_bit_cast(u32x4c, bh1);
+        const u32x4c d3 = __builtin_bit_cast(u32x4c, g3) ^ __builtin_bit_cast(u32x4c, bl1);
+        if ((d[0] | d[1] | d[2] | d[3] | d1[0] | d1[1] | d1[2] | d1[3] | d2[0] | d2[1] | d2[2] | d2[3] | d3[0] | d3[1] |
+             d3[2] | d3[3]) != 0u) {
+          tp_badw++;
+          if (tp_first < 0) tp_first = 100000 + pa * 16 + t;
+        }
+      }
+#endif
+      finish(cur, a0, a1);
+      f16x8 ah, al;
+      split_f16x3(a0, a1, ah, al);
+      acc0 = mfma16h(ah, bh0, acc0);
+      acc1 = mfma16h(ah, bh1, acc1);
+      acc0 = mfma16h(ah, bl0, acc0);
+      acc1 = mfma16h(ah, bl1, acc1);
+      acc0 = mfma16h(al, bh0, acc0);
+      acc1 = mfma16h(al, bh1, acc1);
+      __builtin_amdgcn_sched_barrier(0);
+      if (t < 8) cur = nxt;
+    }
+#else
     // a tap-level software pipeline (tap t + 1's corner reads issued before tap t's blend, one more
     // sample set live) measured 4 % faster in the C0 step but made the outputs depend on the launch's
     // timing at two waves per SIMD; not kept
@@ -367,8 +500,17 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_
       acc1 = mfma16h(al, bh1, acc1);
       __builtin_amdgcn_sched_barrier(0);   // one tap's operands live at a time (VGPR budget)
     }
+#endif
     if (PAIR_AHEAD) lds_dma_barrier();
   }
+#if DCNSEP_TP_CHECK
+  if (__builtin_amdgcn_ballot_w64(tp_bad > 0 || tp_badw > 0) && blockIdx.x % 53 == 0) {
+    const unsigned long long m = __builtin_amdgcn_ballot_w64(tp_bad > 0 || tp_badw > 0);
+    if (lane == __builtin_ctzll(m))
+      printf("TPCHECK block %d wave %d tile (%d,%d) g %d n %d H %d: lanes %d, corner mismatches %d, weight mismatches %d, "
+             "first %d\n", (int)blockIdx.x, wv, oy0, ox0, g, n, H, __builtin_popcountll(m), tp_bad, tp_badw, tp_first);
+  }
+#endif
   if (!PAIR_AHEAD) __syncthreads();   // the epilogue blocks overwrite the pair buffer
   // epilogue through a per-wave LDS block -> coalesced 16-B stores (k_dcn's)
   float* out = a.out[g] + (size_t)n * a.out_item;

@@ -39,6 +39,18 @@ STIF_DEV void split_f16x3(f32x4 x0, f32x4 x1, f16x8& h, f16x8& l) {
   // is exact in fp32, so l equals fp16(x * 2^4 - float(h)) bit for bit, at 4 VALU ops per pair
   // instead of ~7 (the compiler's lowering of the plain expression scales, converts h back to fp32
   // and subtracts separately)
+#if STIF_SPLIT_C
+  // plain-expression form (diagnostic): the compiler sees the VALU ops, so its hazard recognizer covers them
+  const f32x4 s0 = x0 * F16X3_SCALE_A, s1 = x1 * F16X3_SCALE_A;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float v = e < 4 ? s0[e] : s1[e - 4];
+    const _Float16 hh = (_Float16)v;
+    h[e] = hh;
+    l[e] = (_Float16)(v - (float)hh);
+  }
+  return;
+#endif
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   u32x4 hv, lv;
 #pragma unroll
@@ -46,10 +58,17 @@ STIF_DEV void split_f16x3(f32x4 x0, f32x4 x1, f16x8& h, f16x8& l) {
     const float x = e < 2 ? x0[2 * e] : x1[2 * e - 4];
     const float y = e < 2 ? x0[2 * e + 1] : x1[2 * e - 3];
     unsigned hp, lp;
-    asm("v_fma_mixlo_f16 %0, %2, %4, 0\n\t"
+    asm(
+#if STIF_SPLIT_NOP_PRE
+        "s_nop 7\n\ts_nop 7\n\t"
+#endif
+        "v_fma_mixlo_f16 %0, %2, %4, 0\n\t"
         "v_fma_mixhi_f16 %0, %3, %4, 0\n\t"
         "v_fma_mixlo_f16 %1, %2, %4, -%0 op_sel_hi:[0,0,1]\n\t"
         "v_fma_mixhi_f16 %1, %3, %4, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+#if STIF_SPLIT_NOP
+        "\n\ts_nop 4"
+#endif
         : "=&v"(hp), "=&v"(lp)
         : "v"(x), "v"(y), "s"(F16X3_SCALE_A));
     hv[e] = hp;

@@ -47,11 +47,31 @@ static_assert(WINO_UPQ == 0 || WINO_UPQ == 1, "WINO_UPQ");
 #ifndef DCNSEP_WPE
 #define DCNSEP_WPE 2       // waves per SIMD the kernel is register-budgeted for
 #endif
-#ifndef DCNSEP_EXP
-#define DCNSEP_EXP 0       // probes: 1 no phase 1, 3 no phase 2, 5 no per-pair restaging, 6 offset-free sampling
+#ifndef DCNSEP_TAPPIPE
+#define DCNSEP_TAPPIPE 0   // diagnostic: phase-2 tap t + 1's corner reads before tap t's blend (review r5 item 4)
 #endif
-static_assert(DCNSEP_EXP == 0 || DCNSEP_EXP == 1 || DCNSEP_EXP == 3 || DCNSEP_EXP == 5 || DCNSEP_EXP == 6,
-              "DCNSEP_EXP: only probes 1, 3, 5 and 6 exist (a probe number without code would build the product kernel)");
+#ifndef DCNSEP_TP_NOFB
+#define DCNSEP_TP_NOFB 0   // diagnostic (TAPPIPE): no global-load fallback (wrong results past the margin)
+#endif
+#ifndef DCNSEP_TP_CHECK
+#define DCNSEP_TP_CHECK 0  // diagnostic (TAPPIPE): every staged corner / B fragment read checked against HBM (printf)
+#endif
+#ifndef DCNSEP_P1_SAFE
+#define DCNSEP_P1_SAFE 0   // diagnostic: phase-1 steps behind full drains and __syncthreads
+#endif
+#ifndef DCNSEP_SOLO
+#define DCNSEP_SOLO 0      // diagnostic: 48 KB of padding LDS (one workgroup per CU)
+#endif
+#ifndef DCNSEP_TP_WAIT
+#define DCNSEP_TP_WAIT 0   // diagnostic (TAPPIPE): tap t + 1's corner reads drained before tap t's blend
+#endif
+#ifndef DCNSEP_EXP
+#define DCNSEP_EXP 0       // probes: 1 no phase 1, 3 no phase 2, 5 no per-pair restaging, 6 offset-free sampling,
+                           // 7 phase-1 weights DMA'd for the first two steps only (stale after)
+#endif
+static_assert(DCNSEP_EXP == 0 || DCNSEP_EXP == 1 || DCNSEP_EXP == 3 || DCNSEP_EXP == 5 || DCNSEP_EXP == 6 ||
+                  DCNSEP_EXP == 7,
+              "DCNSEP_EXP: only probes 1, 3, 5, 6 and 7 exist (a probe number without code would build the product kernel)");
 
 // ---- k_dec1 / k_dec2 (decoder.hip)
 #ifndef DEC1_NW

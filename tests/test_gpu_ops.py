@@ -594,3 +594,26 @@ def test_dcn_sep_fused_reports_range(ops, L, which):
     ops.dcn_sep([dict(om_layer=om, layer=core, fea=fi, inp=xi, out=out)], status=st)
     assert int(st.item()) == 1, which
 
+
+
+@pytest.mark.parametrize("shape", [(3, 37, 53, 8), (5, 61, 29, 3), (1, 130, 97, 2), (4, 17, 250, 5)])
+def test_dcn_sep_fused_launches_deterministic_odd_shapes(ops, L, shape):
+    """Round-5 review item 4: launch groups of 2-8 weight sets with odd H / W (partial tiles in both directions,
+    several workgroups per CU and so two per CU sharing it) and 1-5 items; every launch re-run three times into
+    fresh NaN buffers reproduces its output bit for bit.  (The tap-pipelined diagnostic variant, DCNSEP_TAPPIPE=1,
+    fails this whenever two workgroups share a CU -- DESIGN.md section 3d.)"""
+    B, H, W, G = shape
+    groups = []
+    for i in range(G):
+        sdx = _dcnsep_weights(200 + 7 * i, 1.0 + 0.7 * i)
+        om, core = _dcnsep_layers(ops, L, sdx)
+        groups.append(dict(om_layer=om, layer=core, fea=torch.from_numpy(rnd(B, H, W, 64, seed=300 + i)).cuda(),
+                           inp=torch.from_numpy(rnd(B, H, W, 64, seed=400 + i)).cuda(),
+                           out=torch.full((B, H, W, 64), float("nan"), device="cuda")))
+    ops.dcn_sep(groups, epi=L.EPI_LRELU)
+    ref = [g["out"].clone() for g in groups]
+    assert all(bool(torch.isfinite(r).all()) for r in ref)
+    for _ in range(3):
+        g2 = [dict(g, out=torch.full_like(g["out"], float("nan"))) for g in groups]
+        ops.dcn_sep(g2, epi=L.EPI_LRELU)
+        assert all(torch.equal(a["out"], b) for a, b in zip(g2, ref))
