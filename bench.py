@@ -521,6 +521,8 @@ def main():
     ap.add_argument("--mfma", default="f16x3", choices=["f32", "f16x3"],
                     help="operand mode of the contractions (model.LunaTokis mfma=)")
     ap.add_argument("--kernel-report", action="store_true", help="time every launch kind (stderr)")
+    ap.add_argument("--range-check", default="rerun", choices=["rerun", "raise", "off"],
+                    help="LunaTokis range_check (timing probes with wrong results use 'off')")
     ap.add_argument("--time-every", type=int, default=1,
                     help="HIP-event-time every N-th launch of the dominant kernel in the timed region")
     ap.add_argument("--fused-dcn", type=int, default=1, choices=[0, 1],

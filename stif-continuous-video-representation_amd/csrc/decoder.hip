@@ -246,6 +246,9 @@ constexpr int SEG1 = 8;      // max tiles per segment (k_dec1)
 // tile (flat global_load_lds would keep a 64-bit VGPR address per hoisted tile live).
 template <int NW>
 STIF_DEV void dma_tiles(float* dst, __amdgpu_buffer_rsrc_t rm, int src, int ntiles, int wv, int lane) {
+#if DEC_EXP == 1   // timing probe: no weight streaming (the MLPs run on whatever the LDS holds)
+  return;
+#endif
   if ((ntiles * 4) % NW == 0) {
     // the same number of pieces per wave, known at compile time: the compiler counts them in vmcnt, so
     // waiting for a load issued before the DMA does not wait for the DMA
@@ -318,8 +321,12 @@ template <int MODE, bool HRIMG>
 constexpr int OCC1 = MODE == 2 ? 2 : (HRIMG && DEC1_OCC > 3) ? 3 : DEC1_OCC;
 template <int MODE, bool HRIMG>
 constexpr int S1 = OCC1<MODE, HRIMG> == 4 ? 4 : OCC1<MODE, HRIMG> == 3 ? 6 : SEG1;
+// waves per workgroup: DEC1_NW for the four-per-SIMD variants (8: two 8-wave workgroups per CU stream each weight
+// segment for 256 pixels instead of 128), 4 for the others
+template <int MODE, bool HRIMG>
+constexpr int NW1 = OCC1<MODE, HRIMG> == 4 ? DEC1_NW : 4;
 template <int MODE, bool HRIMG, int F16>
-__global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(OCC1<MODE, HRIMG>))) void k_dec1(const float* __restrict__ proj, const float* __restrict__ mlp,
+__global__ __launch_bounds__((NW1<MODE, HRIMG> * 64)) __attribute__((amdgpu_waves_per_eu(OCC1<MODE, HRIMG>))) void k_dec1(const float* __restrict__ proj, const float* __restrict__ mlp,
                                                      stif_dec_tables tb, stif_dec_image im,
                                                      const float* __restrict__ tq, float* __restrict__ hrfeat,
                                                      float* __restrict__ flow, int n, int h, int w, int HH,
@@ -327,6 +334,7 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(OCC
   // two segment buffers of SEG1 tiles + the flow's last layer (plain [4][256], resident)
   constexpr bool OCC3 = S1<MODE, HRIMG> != SEG1;             // 3 or 4 workgroups per CU
   constexpr bool OCC4 = OCC1<MODE, HRIMG> == 4;
+  constexpr int DEC_NW = NW1<MODE, HRIMG>;
   __shared__ __attribute__((aligned(16))) float wbuf[2 * S1<MODE, HRIMG> * T + T];
   const int lane = threadIdx.x & 63, hf = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
@@ -369,10 +377,14 @@ __global__ __launch_bounds__(DEC_NW * 64) __attribute__((amdgpu_waves_per_eu(OCC
         for (int e = 0; e < 4; ++e) x0[ot][4 * v + e] = siren_sin<F16>(z[e]);
       }
   }
-  auto seg_feat23 = [&](float* dst, int kt) {   // W2 rows kt (2 tiles), W3 (0, kt), (1, kt)
-    dma_tiles<DEC_NW>(dst, rm, F_W2 + kt * 2 * T, 2, wv, lane);
-    dma_tiles<DEC_NW>(dst + 2 * T, rm, F_W3 + kt * T, 1, wv, lane);
-    dma_tiles<DEC_NW>(dst + 3 * T, rm, F_W3 + (8 + kt) * T, 1, wv, lane);
+  auto seg_feat23 = [&](float* dst, int kt) {   // W2 rows kt (2 tiles), W3 (0, kt), (1, kt): 16 pieces, as one
+    // loop with the same count on every wave (exact vmcnt bookkeeping for 4- and 8-wave workgroups)
+#pragma unroll
+    for (int r = 0; r < 16 / DEC_NW; ++r) {
+      const int i = wv + r * DEC_NW, j = i >> 2;
+      const int src = (j < 2 ? F_W2 + (kt * 2 + j) * T : F_W3 + ((j - 2) * 8 + kt) * T) + (i & 3) * 256;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rm, dst + j * T + (i & 3) * 256, 16, lane * 16, src * 4, 0, 0);
+    }
   };
   lds_dma_barrier();
   const Bias32 fb1[2] = {bias_ld(mlp + F_B1, hf), bias_ld(mlp + F_B1 + 32, hf)};   // before the DMA
@@ -702,11 +714,23 @@ __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DE
 // tile is two 16x16 accumulators: lane (p, q) holds features 16 s + 4 q + i (s = 0, 1; i = 0..3) of pixel
 // p -- which is also the B-operand order of the next layer's K (dec_layout.h Q_*), so features stay in
 // registers between layers as in k_dec2.  The layer-3 state halves (8 tiles x 8 floats = 64 VGPRs): 128 VGPRs,
-// and 4-wave 64-pixel workgroups streaming the weights in 5-tile segments (2 x 20 KB of LDS) run FOUR
-// workgroups per CU -- more independent workgroups, the occupancy that paid in k_dec1 (2 -> 3 -> 4).
+// four waves per SIMD.
+// Weight streaming (round 6): every workgroup streams the whole 372-KB weight set through its LDS, so the
+// stream is paid once per workgroup -- with 4-wave 64-pixel workgroups it cost more than half the kernel (a
+// probe without it, DEC_EXP = 1: C0 stage 2 1,160 -> 480 us, profiles/r06_dec_probe.log).  Workgroups are
+// DEC2Q_NW waves (8: 128 pixels, two per CU; 16: 256 pixels, one per CU) and a segment is the layer-2 / -3
+// weights of DEC2Q_KTS whole layer-2 tiles kt (W2 rows kt + W3 column kt: 10 tiles each), double-buffered in
+// 2 x 40 KB (KTS 1) or 2 x 80 KB (KTS 2): the weight bytes per pixel halve / quarter and one barrier per kt
+// (or per two) replaces two.  Every wave issues the same number of LDS-DMA pieces per segment (5), so the
+// compiler's vmcnt bookkeeping stays exact.
 // Gathers: each lane fetches its own quarter of a 64-channel block (16 corner loads in flight).
-constexpr int DEC2Q_NW = 4;
-constexpr int SEGQ = 5;   // tiles per segment
+constexpr int DEC2Q_NWV = DEC2Q_NW;
+constexpr int KTS = DEC2Q_KTS;            // layer-2 tiles per segment
+constexpr int SEGQ = 10 * KTS;            // tiles per segment
+static_assert(40 * KTS % DEC2Q_NWV == 0 && 32 % DEC2Q_NWV == 0 && 16 % DEC2Q_NWV == 0 && 8 % KTS == 0,
+              "k_dec2q: every wave issues the same number of LDS-DMA pieces");
+static_assert((DEC2Q_NWV == 8 || DEC2Q_NWV == 16) && 2 * SEGQ * T * 4 * (16 / DEC2Q_NWV) <= 160 * 1024,
+              "k_dec2q: 16 waves per CU (four per SIMD) in 8- or 16-wave workgroups, their LDS within 160 KB");
 struct R32 {
   f32x4 s[2];
 };
@@ -769,25 +793,31 @@ STIF_DEV void gather_q(R32* dst, const float* __restrict__ base, int stride, int
   }
 }
 
-__global__ __launch_bounds__(DEC2Q_NW * 64) __attribute__((amdgpu_waves_per_eu(4))) void k_dec2q(
+__global__ __launch_bounds__(DEC2Q_NWV * 64) __attribute__((amdgpu_waves_per_eu(4))) void k_dec2q(
     const float* __restrict__ proj, const float* __restrict__ mlp, const float* __restrict__ hrfeat,
     const float* __restrict__ flow, stif_dec_tables tb, const float* __restrict__ tq, float* __restrict__ out, int n,
     int h, int w, int HH, int WW, int* status) {
   __shared__ __attribute__((aligned(16))) float wbuf[2 * SEGQ * T];
   const int lane = threadIdx.x & 63, q = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  constexpr int NW = DEC2Q_NWV;
   float* const B0 = wbuf;
   float* const B1 = wbuf + SEGQ * T;
   const __amdgpu_buffer_rsrc_t rm = mlp_rsrc(mlp);
-  // segments: [L0 kt 0-1: 4 tiles] [L0 kt 2-3: 4] [L1: 4], per layer-2 tile kt [W2 rows kt (2) + W3 column kt,
-  // ot 0-2 (3)] [W3 column kt, ot 3-7 (5)], then [W4 rows + B3]
-  auto seg_l0 = [&](float* dst, int k0) {   // W0 tiles (ot, k0), (ot, k0 + 1): tile index 4 ot + kt
-    dma_tiles<DEC2Q_NW>(dst, rm, Q_W0 + k0 * T, 2, wv, lane);
-    dma_tiles<DEC2Q_NW>(dst + 2 * T, rm, Q_W0 + (4 + k0) * T, 2, wv, lane);
+  // segments: [L0: 8 tiles] in B0, [L1: 4 tiles] in B1, then per segment s the tiles of kt = KTS s .. KTS s + KTS - 1
+  // ([W2 rows kt (2) | W3 column kt, ot 0-7 (8)] each) alternating B0 / B1, then [W4 rows + B3]
+  dma_tiles<NW>(B0, rm, Q_W0, 8, wv, lane);   // tile index 4 ot + kt
+  auto seg_l23 = [&](float* dst, int sg) {
+#pragma unroll
+    for (int r = 0; r < 40 * KTS / NW; ++r) {
+      const int i = wv + r * NW;                // piece i: tile j = i / 4 of the segment, quarter i % 4
+      const int j = i >> 2, k = j / 10, jj = j - 10 * k, kt = sg * KTS + k;
+      const int src = (jj < 2 ? Q_W2 + (kt * 2 + jj) * T : Q_W3 + ((jj - 2) * 8 + kt) * T) + (i & 3) * 256;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rm, dst + j * T + (i & 3) * 256, 16, lane * 16, src * 4, 0, 0);
+    }
   };
-  seg_l0(B0, 0);
   const long long total = (long long)n * HH * WW;
-  const long long pix = ((long long)xcd_block(blockIdx.x, gridDim.x) * DEC2Q_NW + wv) * 16 + (lane & 15);
+  const long long pix = ((long long)xcd_block(blockIdx.x, gridDim.x) * NW + wv) * 16 + (lane & 15);
   const bool valid = pix < total;
   const long long pc = valid ? pix : total - 1;
   const int item = (int)(pc / ((long long)HH * WW));
@@ -824,47 +854,34 @@ __global__ __launch_bounds__(DEC2Q_NW * 64) __attribute__((amdgpu_waves_per_eu(4
       }
     asm volatile("" ::: "memory");
     gather_q(g, HRF, 64, 0, bilin(g1x, g1y, WW, HH), q);   // q_feat1 -> W0 columns 0..63
-    lds_dma_barrier();
-    seg_l0(B1, 2);
+    lds_dma_barrier();                                      // layer 0 landed in B0
+    dma_tiles<NW>(B1, rm, Q_W1, 4, wv, lane);
     {
       const XQ qs[2] = {xq(g[0]), xq(g[1])};
 #pragma unroll
       for (int ot = 0; ot < 2; ++ot)
 #pragma unroll
-        for (int kt = 0; kt < 2; ++kt) tile_q(z[ot], B0 + (ot * 2 + kt) * T, qs[kt], lane);
+        for (int kt = 0; kt < 2; ++kt) tile_q(z[ot], B0 + (ot * 4 + kt) * T, qs[kt], lane);
     }
     asm volatile("" ::: "memory");
     gather_q(g, HRF, 64, 0, bilin(g2x, g2y, WW, HH), q);   // q_feat2 -> W0 columns 64..127
-    lds_dma_barrier();
-    dma_tiles<DEC2Q_NW>(B0, rm, Q_W1, 4, wv, lane);
     const XQ qs[2] = {xq(g[0]), xq(g[1])};
 #pragma unroll
     for (int ot = 0; ot < 2; ++ot) {
 #pragma unroll
-      for (int kt = 2; kt < 4; ++kt) tile_q(z[ot], B1 + (ot * 2 + kt - 2) * T, qs[kt - 2], lane);
+      for (int kt = 2; kt < 4; ++kt) tile_q(z[ot], B0 + (ot * 4 + kt) * T, qs[kt - 2], lane);
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int e = 0; e < 4; ++e) x0[ot].s[s][e] = siren_sin<1>(z[ot].s[s][e] * ACC_S<1>);
     }
   }
-  lds_dma_barrier();
+  lds_dma_barrier();   // layer 1 landed in B1; every wave is done with layer 0's B0
   // layer-1 biases before the next segment's LDS-DMA: vmcnt counts in issue order, so a bias load issued
   // after the DMA would wait for the DMA too (as k_dec1 / k_dec2 do)
   const R32 eb1[2] = {bias_q(mlp + E_B1, q), bias_q(mlp + E_B1 + 32, q)};
   __builtin_amdgcn_sched_barrier(0);
-  // layer-2/3 segment 2 kt + h: h = 0 the W2 rows of tile kt + W3 (ot 0-2, kt), h = 1 W3 (ot 3-7, kt)
-  auto seg_l23 = [&](float* dst, int kt, int h) {
-    if (h == 0) {
-      dma_tiles<DEC2Q_NW>(dst, rm, Q_W2 + kt * 2 * T, 2, wv, lane);
-#pragma unroll
-      for (int ot = 0; ot < 3; ++ot) dma_tiles<DEC2Q_NW>(dst + (2 + ot) * T, rm, Q_W3 + (ot * 8 + kt) * T, 1, wv, lane);
-    } else {
-#pragma unroll
-      for (int ot = 3; ot < 8; ++ot) dma_tiles<DEC2Q_NW>(dst + (ot - 3) * T, rm, Q_W3 + (ot * 8 + kt) * T, 1, wv, lane);
-    }
-  };
-  seg_l23(B1, 0, 0);
+  seg_l23(B0, 0);
   R32 x1[2];
   {
     const XQ xs[2] = {xq(x0[0]), xq(x0[1])};
@@ -873,7 +890,7 @@ __global__ __launch_bounds__(DEC2Q_NW * 64) __attribute__((amdgpu_waves_per_eu(4
       R32 acc;
       acc.s[0] = acc.s[1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) tile_q(acc, B0 + (ot * 2 + kt) * T, xs[kt], lane);
+      for (int kt = 0; kt < 2; ++kt) tile_q(acc, B1 + (ot * 2 + kt) * T, xs[kt], lane);
       x1[ot] = bias_sin_q(acc, eb1[ot]);
     }
   }
@@ -882,32 +899,36 @@ __global__ __launch_bounds__(DEC2Q_NW * 64) __attribute__((amdgpu_waves_per_eu(4
   R32 a3[8];
 #pragma unroll
   for (int ot = 0; ot < 8; ++ot) a3[ot].s[0] = a3[ot].s[1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // segment 2 kt sits in B1, 2 kt + 1 in B0
-  auto l23_step = [&](int kt, bool last) {
-    lds_dma_barrier();
-    const R32 b2 = bias_q(mlp + E_B2 + kt * 32, q);   // before the DMA (see eb1)
+  constexpr int NSEG = 8 / KTS;
+  auto l23_step = [&](int sg, bool last) {
+    lds_dma_barrier();   // segment sg landed; every wave is done with the other buffer
+    R32 b2[KTS];
+#pragma unroll
+    for (int k = 0; k < KTS; ++k) b2[k] = bias_q(mlp + E_B2 + (sg * KTS + k) * 32, q);   // before the DMA
     __builtin_amdgcn_sched_barrier(0);
-    seg_l23(B0, kt, 1);
-    R32 acc;
-    acc.s[0] = acc.s[1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    tile_q(acc, B1, x1s[0], lane);
-    tile_q(acc, B1 + T, x1s[1], lane);
-    const XQ h2 = xq(bias_sin_q(acc, b2));
+    float* cur = (sg & 1) ? B1 : B0;
+    float* nxt = (sg & 1) ? B0 : B1;
+    if (!last) seg_l23(nxt, sg + 1);
+    else dma_tiles<NW>(nxt, rm, E_W4V, 1, wv, lane);
 #pragma unroll
-    for (int ot = 0; ot < 3; ++ot) tile_q(a3[ot], B1 + (2 + ot) * T, h2, lane);
-    lds_dma_barrier();
-    if (!last) seg_l23(B1, kt + 1, 0);
-    else dma_tiles<DEC2Q_NW>(B1, rm, E_W4V, 1, wv, lane);
+    for (int k = 0; k < KTS; ++k) {
+      const float* sk = cur + k * 10 * T;
+      R32 acc;
+      acc.s[0] = acc.s[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      tile_q(acc, sk, x1s[0], lane);
+      tile_q(acc, sk + T, x1s[1], lane);
+      const XQ h2 = xq(bias_sin_q(acc, b2[k]));
 #pragma unroll
-    for (int ot = 3; ot < 8; ++ot) tile_q(a3[ot], B0 + (ot - 3) * T, h2, lane);
+      for (int ot = 0; ot < 8; ++ot) tile_q(a3[ot], sk + (2 + ot) * T, h2, lane);
+    }
   };
 #pragma unroll 1
-  for (int kt = 0; kt < 7; ++kt) l23_step(kt, false);
-  l23_step(7, true);
+  for (int sg = 0; sg < NSEG - 1; ++sg) l23_step(sg, false);
+  l23_step(NSEG - 1, true);
   // layer 3 sine streamed into layer 4 (256 -> 3, VALU dot products over this lane's 64 features); W4 rows
-  // and the layer-3 biases in B1 (k_dec2's tile)
+  // and the layer-3 biases in the buffer the last segment did not use (k_dec2's tile)
   lds_dma_barrier();
-  float* const B4 = B1;
+  float* const B4 = ((NSEG - 1) & 1) ? B0 : B1;
   float o4[3] = {0.f, 0.f, 0.f};
 #pragma unroll
   for (int kt = 0; kt < 8; ++kt) {
@@ -1005,14 +1026,16 @@ bool image_ok(const stif_dec_image* im) {
 }
 
 template <int MODE, bool HRIMG>
-void launch_dec1(bool f16, long long blocks, hipStream_t st, const float* proj, const float* mlp,
+void launch_dec1(bool f16, long long total, hipStream_t st, const float* proj, const float* mlp,
                  const stif_dec_tables& tb, const stif_dec_image& im, const float* t, float* hrfeat, float* flow, int n,
                  int h, int w, int HH, int WW) {
+  constexpr int nw = NW1<MODE, HRIMG>;
+  const long long blocks = (total + nw * 32 - 1) / (nw * 32);
   if (f16)
-    hipLaunchKernelGGL((k_dec1<MODE, HRIMG, 1>), dim3((unsigned)blocks), dim3(DEC_NW * 64), 0, st, proj, mlp, tb, im,
+    hipLaunchKernelGGL((k_dec1<MODE, HRIMG, 1>), dim3((unsigned)blocks), dim3(nw * 64), 0, st, proj, mlp, tb, im,
                        t, hrfeat, flow, n, h, w, HH, WW);
   else
-    hipLaunchKernelGGL((k_dec1<MODE, HRIMG, 0>), dim3((unsigned)blocks), dim3(DEC_NW * 64), 0, st, proj, mlp, tb, im,
+    hipLaunchKernelGGL((k_dec1<MODE, HRIMG, 0>), dim3((unsigned)blocks), dim3(nw * 64), 0, st, proj, mlp, tb, im,
                        t, hrfeat, flow, n, h, w, HH, WW);
 }
 
@@ -1027,17 +1050,16 @@ extern "C" int stif_dec_stage1_ex(const float* proj, const float* mlp, const sti
       HH < 2 || WW < 2 || (!tab->hr_y) != (!tab->hr_x))
     return stif_fail(STIF_E_INVALID, "stif_dec_stage1: bad arguments");
   const long long total = (long long)n * HH * WW;
-  const long long blocks = (total + DEC_NW * 32 - 1) / (DEC_NW * 32);
   hipStream_t st = (hipStream_t)stream;
   const stif_dec_image im = img ? *img : stif_dec_image{};
   if (tab->hr_y) {   // remapped HRfeat operand: the whole HRfeat map first, then the flow stage
-    launch_dec1<1, false>(f16, blocks, st, proj, mlp, *tab, im, t, hrfeat, flow, n, h, w, HH, WW);
-    if (img) launch_dec1<2, true>(f16, blocks, st, proj, mlp, *tab, im, t, hrfeat, flow, n, h, w, HH, WW);
-    else launch_dec1<2, false>(f16, blocks, st, proj, mlp, *tab, im, t, hrfeat, flow, n, h, w, HH, WW);
+    launch_dec1<1, false>(f16, total, st, proj, mlp, *tab, im, t, hrfeat, flow, n, h, w, HH, WW);
+    if (img) launch_dec1<2, true>(f16, total, st, proj, mlp, *tab, im, t, hrfeat, flow, n, h, w, HH, WW);
+    else launch_dec1<2, false>(f16, total, st, proj, mlp, *tab, im, t, hrfeat, flow, n, h, w, HH, WW);
   } else if (img) {
-    launch_dec1<0, true>(f16, blocks, st, proj, mlp, *tab, im, t, hrfeat, flow, n, h, w, HH, WW);
+    launch_dec1<0, true>(f16, total, st, proj, mlp, *tab, im, t, hrfeat, flow, n, h, w, HH, WW);
   } else {
-    launch_dec1<0, false>(f16, blocks, st, proj, mlp, *tab, im, t, hrfeat, flow, n, h, w, HH, WW);
+    launch_dec1<0, false>(f16, total, st, proj, mlp, *tab, im, t, hrfeat, flow, n, h, w, HH, WW);
   }
   return stif_check_launch("stif_dec_stage1");
 }
@@ -1060,8 +1082,8 @@ extern "C" int stif_dec_stage2_ex(const float* proj, const float* mlp, const flo
   const stif_dec_image im = img ? *img : stif_dec_image{};
   hipStream_t st = (hipStream_t)stream;
   if (DEC2_Q16 && f16 && !img) {
-    const long long qblocks = (total + DEC2Q_NW * 16 - 1) / (DEC2Q_NW * 16);
-    hipLaunchKernelGGL(k_dec2q, dim3((unsigned)qblocks), dim3(DEC2Q_NW * 64), 0, st, proj, mlp, hrfeat, flow, *tab, t,
+    const long long qblocks = (total + DEC2Q_NWV * 16 - 1) / (DEC2Q_NWV * 16);
+    hipLaunchKernelGGL(k_dec2q, dim3((unsigned)qblocks), dim3(DEC2Q_NWV * 64), 0, st, proj, mlp, hrfeat, flow, *tab, t,
                        out, n, h, w, HH, WW, status);
     return stif_check_launch("stif_dec_stage2");
   }

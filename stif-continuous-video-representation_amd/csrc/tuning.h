@@ -20,7 +20,8 @@
 static_assert(WINO_UPQ == 0 || WINO_UPQ == 1, "WINO_UPQ");
 #ifndef WINO_EXP
 #define WINO_EXP 0         // probes: 1 no LDS-DMA after the first phase, 2 no B refills, 3 no output exchange,
-                           // 4 no x2-upsample expansion (in1_mode 2)
+                           // 4 no x2-upsample expansion (in1_mode 2), 5 RELU-epilogue convs store nothing,
+                           // 6 k_wino_om stores nothing (out-of-range store offsets)
 #endif
 
 // ---- k_dcn (dcn.hip): the DCN core of the two-kernel path and the _ext drop-in at the STIF shape
@@ -75,8 +76,9 @@ static_assert(DCNSEP_EXP == 0 || DCNSEP_EXP == 1 || DCNSEP_EXP == 3 || DCNSEP_EX
 
 // ---- k_dec1 / k_dec2 (decoder.hip)
 #ifndef DEC1_NW
-// waves per k_dec1 workgroup (~240 VGPRs: 2 waves/SIMD); 4-wave workgroups, 2 per CU (80 KB LDS each):
-// the two waves sharing a SIMD come from different workgroups (4 vs 8 within noise, r01_knob_sweep.log)
+// k_dec1 waves per workgroup for its four-waves-per-SIMD variants (MODE 0 / 1, no high-resolution image): 4 = four
+// 4-wave workgroups per CU.  8 (two 8-wave workgroups, each streaming the MLP weights for 256 pixels instead of 128)
+// measured slower: C0 stage 1 686-715 -> 768-784 us, C2 10.9 -> 11.7 ms (profiles/r06_dec_ab.log)
 #define DEC1_NW 4
 #endif
 #ifndef DEC1_OCC
@@ -91,8 +93,18 @@ static_assert(DCNSEP_EXP == 0 || DCNSEP_EXP == 1 || DCNSEP_EXP == 3 || DCNSEP_EX
 // fp32 and high-resolution-image stages)
 #define DEC2_Q16 1
 #endif
+#ifndef DEC2Q_NW
+#define DEC2Q_NW 8         // k_dec2q waves per workgroup (8: two 80-KB workgroups per CU; 16: one 160-KB workgroup)
+#endif
+#ifndef DEC2Q_KTS
+#define DEC2Q_KTS (DEC2Q_NW == 16 ? 2 : 1)   // layer-2 tiles per streamed weight segment
+#endif
 #ifndef DEC2_WPE
 #define DEC2_WPE 2         // waves per SIMD k_dec2 is register-budgeted for (2 workgroups/CU, 80 KB LDS each)
 #endif
 static_assert(DEC1_OCC >= 2 && DEC1_OCC <= 4, "DEC1_OCC: k_dec1 is laid out for 2, 3 or 4 workgroups per CU");
 static_assert(DEC2_Q16 == 0 || DEC2_Q16 == 1, "DEC2_Q16: 0 (k_dec2) or 1 (k_dec2q)");
+#ifndef DEC_EXP
+#define DEC_EXP 0          // probe: 1 no MLP weight streaming into LDS (wrong results)
+#endif
+static_assert(DEC_EXP == 0 || DEC_EXP == 1, "DEC_EXP");

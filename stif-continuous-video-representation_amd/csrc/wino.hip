@@ -544,7 +544,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, cn), ro2, voff(nt, k), 0, 0);
           continue;
         }
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, y), ro, voff(nt, k), 0, 0);
+        if (WINO_EXP != 5 || EPI != STIF_EPI_RELU)   // probe 5: the ResidualBlock's conv1 stores nothing
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, y), ro,
+                                                 voff(nt, k), 0, 0);
       }
     }
     if (F16) report_range(a.status, not_finite(chk));   // a non-finite output makes the sum non-finite
@@ -701,7 +703,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       for (int e = 0; e < 4; ++e)
         if (EPI == STIF_EPI_OFFMASK) y[e] = (m3 + e) % 3 == 2 ? sigmoid_fast(y[e]) : y[e];
       const int oy = t.oy0 + k;
-      const bool ok = (oy < a.Ho) & (ox < a.Wo) & cok;
+      const bool ok = (oy < a.Ho) & (ox < a.Wo) & cok & (WINO_EXP != 6);   // probe 6: k_wino_om stores nothing
       const unsigned vo = ok ? (unsigned)(((oy * a.Wo + ox) * a.cout + cob) * 4) : 0x80000000u;
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, y), ro,
                                              vo, 0, 0);
