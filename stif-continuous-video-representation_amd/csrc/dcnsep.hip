@@ -128,7 +128,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_
       const int y = oy0 - 1 + row, x = ox0 - 1 + col;
       const bool ok = (s < D_SLOTS) & (sub < 4) & ((unsigned)y < (unsigned)H) & ((unsigned)x < (unsigned)W);
       const unsigned voff = ok ? (unsigned)((((size_t)y * W + x) * 64 + 16 * c + 4 * sub) * 4) : 0x80000000u;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rfea, dst + i * 256, 16, voff, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rfea, dst + i * 256, 16, voff, 0, 0, DCNSEP_NT);
     }
   };
   // the packed weights of step k (the instructions past the step's 14 KB load zeros)
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_
         const bool ok = (i < T_INST) & (e < T_EL) & ((unsigned)y < (unsigned)H) & ((unsigned)x < (unsigned)W);
         const unsigned voff = ok ? (unsigned)((((size_t)y * W + x) * 64 + pa * 16 + q * 4) * 4) : 0x80000000u;
         float* dst = i < T_INST ? st + i * 256 : sw + (i - T_INST) * 256;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, dst, 16, voff, 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, dst, 16, voff, 0, 0, DCNSEP_NT);   // tile (pad pieces load nothing)
       }
     }
   };
@@ -504,7 +504,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_
     if (PAIR_AHEAD) lds_dma_barrier();
   }
 #if DCNSEP_TP_CHECK
-  if (__builtin_amdgcn_ballot_w64(tp_bad > 0 || tp_badw > 0) && blockIdx.x % 53 == 0) {
+  if (__builtin_amdgcn_ballot_w64(tp_bad > 0 || tp_badw > 0)) {
     const unsigned long long m = __builtin_amdgcn_ballot_w64(tp_bad > 0 || tp_badw > 0);
     if (lane == __builtin_ctzll(m))
       printf("TPCHECK block %d wave %d tile (%d,%d) g %d n %d H %d: lanes %d, corner mismatches %d, weight mismatches %d, "

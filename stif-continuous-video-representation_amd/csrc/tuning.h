@@ -18,6 +18,9 @@
 #define WINO_UPQ 1         // fused x2 upsample expanded by 2 x 2 quads (0: per pixel, k_up2's expression)
 #endif
 static_assert(WINO_UPQ == 0 || WINO_UPQ == 1, "WINO_UPQ");
+#ifndef WINO_NT
+#define WINO_NT 0          // cache-policy bits (aux) of the input-halo LDS-DMA (2 = nt)
+#endif
 #ifndef WINO_EXP
 #define WINO_EXP 0         // probes: 1 no LDS-DMA after the first phase, 2 no B refills, 3 no output exchange,
                            // 4 no x2-upsample expansion (in1_mode 2), 5 RELU-epilogue convs store nothing,
@@ -65,6 +68,9 @@ static_assert(WINO_UPQ == 0 || WINO_UPQ == 1, "WINO_UPQ");
 #endif
 #ifndef DCNSEP_TP_WAIT
 #define DCNSEP_TP_WAIT 0   // diagnostic (TAPPIPE): tap t + 1's corner reads drained before tap t's blend
+#endif
+#ifndef DCNSEP_NT
+#define DCNSEP_NT 0        // cache-policy bits (aux) of the feature / input tile LDS-DMA (2 = nt)
 #endif
 #ifndef DCNSEP_EXP
 #define DCNSEP_EXP 0       // probes: 1 no phase 1, 3 no phase 2, 5 no per-pair restaging, 6 offset-free sampling,

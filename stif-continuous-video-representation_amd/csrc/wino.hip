@@ -77,7 +77,7 @@ STIF_DEV void stage_image(__amdgpu_buffer_rsrc_t rs, float* dst, int iy0, int ix
     const unsigned off = __umul24((unsigned)(y * W + x), cs4) + cb;
     // select, not branch: every lane's offset is computed, out-of-range ones replaced
     const unsigned voff = (((unsigned)y < (unsigned)H) & ((unsigned)x < (unsigned)W)) ? off : 0x80000000u;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, dst + (r * OM_RP + 63 * m) * 4, 16, voff, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, dst + (r * OM_RP + 63 * m) * 4, 16, voff, 0, 0, WINO_NT);
   }
 }
 
