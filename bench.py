@@ -648,7 +648,9 @@ def main():
         if args.mfma == "f16x3":
             runs.append((args.config, "f16x3", "off"))
         runs += [(c, args.mfma, "rerun") for c in ("c1", "c2", "c3", "c4") if c != args.config]
-        reps = {"c0": (3, 1), "c1": (3, 1), "c2": (2, 1), "c3": (1, 1), "c4": (1, 1)}
+        # the other operand mode / the range-sync-free line of the metric's own config over 10 steps (review r5: the
+        # 3-step fp32 line moved by a few % between runs); the large configs keep 1-3 steps (seconds each)
+        reps = {"c0": (10, 2), "c1": (3, 1), "c2": (2, 1), "c3": (1, 1), "c4": (1, 1)}
         for cfg, mf, rc in runs:
             a2 = argparse.Namespace(**vars(args))
             a2.steps, a2.warmup = reps[cfg]
