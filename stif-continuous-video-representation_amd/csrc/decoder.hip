@@ -262,6 +262,18 @@ STIF_DEV void dma_tiles(float* dst, __amdgpu_buffer_rsrc_t rm, int src, int ntil
   }
 }
 
+// the segment barrier of the weight stream (lds_dma_barrier); probe DEC_EXP 2 skips its vmcnt(0) wait, i.e. the
+// time the waves spend waiting for segments still in flight (wrong results)
+STIF_DEV void dec_barrier() {
+#if DEC_EXP == 2
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+#else
+  lds_dma_barrier();
+#endif
+}
+
 STIF_DEV __amdgpu_buffer_rsrc_t mlp_rsrc(const float* mlp) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)mlp, (short)0, (int)(MLP_FLOATS * 4), 0x00020000);
 }
@@ -386,7 +398,7 @@ __global__ __launch_bounds__((NW1<MODE, HRIMG> * 64)) __attribute__((amdgpu_wave
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rm, dst + j * T + (i & 3) * 256, 16, lane * 16, src * 4, 0, 0);
     }
   };
-  lds_dma_barrier();
+  dec_barrier();
   const Bias32 fb1[2] = {bias_ld(mlp + F_B1, hf), bias_ld(mlp + F_B1 + 32, hf)};   // before the DMA
   __builtin_amdgcn_sched_barrier(0);
   seg_feat23(B1, 0);
@@ -406,7 +418,7 @@ __global__ __launch_bounds__((NW1<MODE, HRIMG> * 64)) __attribute__((amdgpu_wave
   // the streamed steps (kt = 7 peeled: its DMA differs, and the loop's steps must all issue the same
   // number of DMA pieces for the compiler's vmcnt bookkeeping to stay exact across the back edge)
   auto feat_step = [&](int kt, bool last) {
-    lds_dma_barrier();
+    dec_barrier();
     // this step's bias is loaded before the next segment's DMA is issued, so waiting for it does not
     // wait for the DMA (vmcnt counts in issue order)
     const Bias32 b2 = bias_ld(mlp + F_B2 + kt * 32, hf);
@@ -484,7 +496,7 @@ __global__ __launch_bounds__((NW1<MODE, HRIMG> * 64)) __attribute__((amdgpu_wave
     }
   }
   // flow layers 0/1 live in B1 (prefetched during the last feat segment, or at the start)
-  lds_dma_barrier();
+  dec_barrier();
   const Bias32 lb1[2] = {bias_ld(mlp + L_B1, hf), bias_ld(mlp + L_B1 + 32, hf)};   // before the DMA
   __builtin_amdgcn_sched_barrier(0);
   auto seg_flow23 = [&](float* dst, int kt) {   // W2 rows kt (2 tiles); W3 is resident (W3V)
@@ -507,7 +519,7 @@ __global__ __launch_bounds__((NW1<MODE, HRIMG> * 64)) __attribute__((amdgpu_wave
       for (int r = 0; r < 16; ++r) z[ot][r] = siren_sin<F16>(z[ot][r] * ACC_S<F16>);
     }
   }
-  if (L1B0 || OCC4) lds_dma_barrier();   // layer 1 (OCC3: its second output tile) landed in B0
+  if (L1B0 || OCC4) dec_barrier();   // layer 1 (OCC3: its second output tile) landed in B0
   if (OCC4) seg_flow23(B1, 0);             // every wave is done with layer 0's B1
   {
     const XT<F16> zs[2] = {xop<F16>(z[0]), xop<F16>(z[1])};
@@ -523,7 +535,7 @@ __global__ __launch_bounds__((NW1<MODE, HRIMG> * 64)) __attribute__((amdgpu_wave
   const XT<F16> x1f[2] = {xop<F16>(x1[0]), xop<F16>(x1[1])};
   float fl[4] = {0.f, 0.f, 0.f, 0.f};
   auto flow_step = [&](int kt, bool last) {   // kt = 7 peeled (see feat_step)
-    lds_dma_barrier();
+    dec_barrier();
     const Bias32 b2 = bias_ld(mlp + L_B2 + kt * 32, hf);   // before the DMA (see feat_step)
     __builtin_amdgcn_sched_barrier(0);
     // OCC4: segment 0 sits in B1, so the buffers alternate the other way round
@@ -611,7 +623,7 @@ __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DE
     }
     asm volatile("" ::: "memory");
     gather64(q, HRF, 64, 0, bilin(g1x, g1y, WW, HH), hf);   // q_feat1 -> W0 columns 0..63
-    lds_dma_barrier();
+    dec_barrier();
     dma_tiles<DEC2_NW>(B1, rm, E_W1, 4, wv, lane);
     {
       const XT<F16> qs[2] = {xop<F16>(q[0]), xop<F16>(q[1])};
@@ -631,7 +643,7 @@ __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DE
       for (int r = 0; r < 16; ++r) x0[ot][r] = siren_sin<F16>(z[ot][r] * ACC_S<F16>);
     }
   }
-  lds_dma_barrier();
+  dec_barrier();
   const Bias32 eb1[2] = {bias_ld(mlp + E_B1, hf), bias_ld(mlp + E_B1 + 32, hf)};   // before the DMA
   __builtin_amdgcn_sched_barrier(0);
   auto seg_l23_first = [&](float* dst) {
@@ -663,7 +675,7 @@ __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DE
 #pragma unroll
   for (int ot = 0; ot < 8; ++ot) a3[ot] = f32x16{0};
   auto l23_step = [&](int kt, bool last) {   // kt = 7 peeled (see k_dec1's feat_step)
-    lds_dma_barrier();
+    dec_barrier();
     const Bias32 b2 = bias_ld(mlp + E_B2 + kt * 32, hf);   // before the DMA (see k_dec1)
     __builtin_amdgcn_sched_barrier(0);
     float* cur = (kt & 1) ? B1 : B0;
@@ -682,7 +694,7 @@ __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DE
   l23_step(7, true);
   // layer 3 sine streamed into layer 4 (256 -> 3, linear, VALU dot products); W4 sits in B0 as
   // plain rows, followed by the layer-3 biases (E_W4V_B3; kt = 7 prefetch)
-  lds_dma_barrier();
+  dec_barrier();
   float o4[3] = {0.f, 0.f, 0.f};
 #pragma unroll
   for (int kt = 0; kt < 8; ++kt) {
@@ -854,7 +866,7 @@ __global__ __launch_bounds__(DEC2Q_NWV * 64) __attribute__((amdgpu_waves_per_eu(
       }
     asm volatile("" ::: "memory");
     gather_q(g, HRF, 64, 0, bilin(g1x, g1y, WW, HH), q);   // q_feat1 -> W0 columns 0..63
-    lds_dma_barrier();                                      // layer 0 landed in B0
+    dec_barrier();                                      // layer 0 landed in B0
     dma_tiles<NW>(B1, rm, Q_W1, 4, wv, lane);
     {
       const XQ qs[2] = {xq(g[0]), xq(g[1])};
@@ -876,7 +888,7 @@ __global__ __launch_bounds__(DEC2Q_NWV * 64) __attribute__((amdgpu_waves_per_eu(
         for (int e = 0; e < 4; ++e) x0[ot].s[s][e] = siren_sin<1>(z[ot].s[s][e] * ACC_S<1>);
     }
   }
-  lds_dma_barrier();   // layer 1 landed in B1; every wave is done with layer 0's B0
+  dec_barrier();   // layer 1 landed in B1; every wave is done with layer 0's B0
   // layer-1 biases before the next segment's LDS-DMA: vmcnt counts in issue order, so a bias load issued
   // after the DMA would wait for the DMA too (as k_dec1 / k_dec2 do)
   const R32 eb1[2] = {bias_q(mlp + E_B1, q), bias_q(mlp + E_B1 + 32, q)};
@@ -901,7 +913,7 @@ __global__ __launch_bounds__(DEC2Q_NWV * 64) __attribute__((amdgpu_waves_per_eu(
   for (int ot = 0; ot < 8; ++ot) a3[ot].s[0] = a3[ot].s[1] = f32x4{0.f, 0.f, 0.f, 0.f};
   constexpr int NSEG = 8 / KTS;
   auto l23_step = [&](int sg, bool last) {
-    lds_dma_barrier();   // segment sg landed; every wave is done with the other buffer
+    dec_barrier();   // segment sg landed; every wave is done with the other buffer
     R32 b2[KTS];
 #pragma unroll
     for (int k = 0; k < KTS; ++k) b2[k] = bias_q(mlp + E_B2 + (sg * KTS + k) * 32, q);   // before the DMA
@@ -927,7 +939,7 @@ __global__ __launch_bounds__(DEC2Q_NWV * 64) __attribute__((amdgpu_waves_per_eu(
   l23_step(NSEG - 1, true);
   // layer 3 sine streamed into layer 4 (256 -> 3, VALU dot products over this lane's 64 features); W4 rows
   // and the layer-3 biases in the buffer the last segment did not use (k_dec2's tile)
-  lds_dma_barrier();
+  dec_barrier();
   float* const B4 = ((NSEG - 1) & 1) ? B0 : B1;
   float o4[3] = {0.f, 0.f, 0.f};
 #pragma unroll

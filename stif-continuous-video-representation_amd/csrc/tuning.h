@@ -111,6 +111,7 @@ static_assert(DCNSEP_EXP == 0 || DCNSEP_EXP == 1 || DCNSEP_EXP == 3 || DCNSEP_EX
 static_assert(DEC1_OCC >= 2 && DEC1_OCC <= 4, "DEC1_OCC: k_dec1 is laid out for 2, 3 or 4 workgroups per CU");
 static_assert(DEC2_Q16 == 0 || DEC2_Q16 == 1, "DEC2_Q16: 0 (k_dec2) or 1 (k_dec2q)");
 #ifndef DEC_EXP
-#define DEC_EXP 0          // probe: 1 no MLP weight streaming into LDS (wrong results)
+#define DEC_EXP 0          // probes: 1 no MLP weight streaming into LDS, 2 segment barriers without the vmcnt(0)
+                           // wait for the segment (wrong results)
 #endif
-static_assert(DEC_EXP == 0 || DEC_EXP == 1, "DEC_EXP");
+static_assert(DEC_EXP == 0 || DEC_EXP == 1 || DEC_EXP == 2, "DEC_EXP");
