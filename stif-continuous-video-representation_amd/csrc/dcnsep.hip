@@ -79,7 +79,9 @@ STIF_DEV void wait_vm(int n) {
   switch (n) {
     case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
     case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
     case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
     case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
     case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
     case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
@@ -132,11 +134,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_
     }
   };
   // the packed weights of step k (the instructions past the step's 14 KB load zeros)
+  // DCNSEP_WTRIM: only the 14 pieces that carry data are issued (waves 0-1: 4, waves 2-3: 3, wave-uniform counts the
+  // phase-1 waits follow); else 16 with two all-pad pieces (every wave 4)
   auto stage_w = [&](int k, int slot) {
     float* dst = smem + OFF_W + slot * 4096;
 #pragma unroll
     for (int j = 0; j < WK_INS / NW; ++j) {
       const int i = wv + j * NW;
+      if (DCNSEP_WTRIM && i >= MT * 2) continue;   // wave-uniform
       const unsigned voff = i < MT * 2 ? (unsigned)((k * WK_F + i * 256) * 4 + lane * 16) : 0x80000000u;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rwom, dst + i * 256, 16, voff, 0, 0, 0);
     }
@@ -196,7 +201,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_
       const int k = 9 * c + t;
       // this step's weights (and, at a chunk start, its data) landed in every wave; the DMA issued in the
       // last two steps (weights of k + 1, the side stage of tap 1) may stay in flight
-      constexpr int WQ = WK_INS / NW;   // weight DMA instructions per wave and step
+      // weight DMA instructions per wave and step (DCNSEP_WTRIM: wave-uniform, 4 or 3)
+      const int WQ = (DCNSEP_WTRIM && NW == 4) ? (wv < MT * 2 - 3 * NW ? 4 : 3) : WK_INS / NW;
       if (t == 2 || t == 3) wait_vm(c < 3 ? WQ + D_INS / NW : (PAIR_AHEAD ? WQ + P_INS / NW : WQ));
       else if (t == 8 && c == 3) wait_vm(0);
       else wait_vm(WQ);

@@ -69,6 +69,9 @@ static_assert(WINO_UPQ == 0 || WINO_UPQ == 1, "WINO_UPQ");
 #ifndef DCNSEP_TP_WAIT
 #define DCNSEP_TP_WAIT 0   // diagnostic (TAPPIPE): tap t + 1's corner reads drained before tap t's blend
 #endif
+#ifndef DCNSEP_WTRIM
+#define DCNSEP_WTRIM 0     // phase-1 weight stage without its two all-pad DMA pieces per step (NW 4)
+#endif
 #ifndef DCNSEP_NT
 #define DCNSEP_NT 0        // cache-policy bits (aux) of the feature / input tile LDS-DMA (2 = nt)
 #endif
