@@ -55,14 +55,26 @@ def traced(groups, epi=0, status=None):
     orig(groups, epi=epi, status=st)
     ref = [g["out"].clone() for g in groups]
     same, stats = [], [int(st.item())]
+    diffs = []
     for _ in range(3):
         st2 = torch.zeros(1, dtype=torch.int32, device="cuda")
         g2 = [dict(g, out=torch.full_like(g["out"], float("nan"))) for g in groups]
         orig(g2, epi=epi, status=st2)
         same.append(all(torch.equal(a["out"], b) for a, b in zip(g2, ref)))
+        if os.environ.get("DIFF"):
+            for gi, (a, b) in enumerate(zip(g2, ref)):
+                d = (a["out"] - b).abs()
+                if bool((d > 0).any()):
+                    nz = (d > 0).nonzero()
+                    H, W = b.shape[1], b.shape[2]
+                    diffs.append(f"g{gi}: {int(nz.shape[0])} el, max|d| {float(d.max()):.3e} (max|out| {float(b.abs().max()):.2e}), "
+                                 f"max rel {float((d / b.abs().clamp_min(1e-6)).max()):.2e}; ch<32 {int((nz[:, 3] < 32).sum())}, "
+                                 f"row%4 {torch.bincount(nz[:, 1] % 4, minlength=4).tolist()}, x%32<8 {int((nz[:, 2] % 32 < 8).sum())}, "
+                                 f"border(<=2 px) {int(((nz[:, 1] <= 2) | (nz[:, 1] >= H - 3) | (nz[:, 2] <= 2) | (nz[:, 2] >= W - 3)).sum())}, "
+                                 f"items {torch.bincount(nz[:, 0], minlength=b.shape[0]).tolist()}")
         stats.append(int(st2.item()))
     nonfin = sum(int((~torch.isfinite(r)).sum()) for r in ref)
-    rows.append((len(groups), tuple(groups[0]["out"].shape), stats, same, nonfin))
+    rows.append((len(groups), tuple(groups[0]["out"].shape), stats, same, nonfin, diffs[:4]))
     if status is not None and stats[0]:
         status.fill_(1)
 
@@ -77,3 +89,5 @@ finally:
     ops.dcn_sep = orig
 for r in rows:
     print(f"  launch groups={r[0]} out={r[1]} status(run, reruns)={r[2]} identical={r[3]} nonfinite={r[4]}")
+    for d in r[5]:
+        print("      diff", d)
