@@ -74,6 +74,14 @@ constexpr int LDS_F = PAIR_AHEAD ? OFF_XW + PW_PAD_F : OFF_W + RING * 4096;
 static_assert(D_F <= OFF_D1 && WK_F <= 4096 && NW * 1024 <= D_F && LDS_F * 4 <= (NW == 8 ? 160 : 80) * 1024 &&
               (PAIR_AHEAD ? OFF_YW + PW_PAD_F <= OFF_XW : OFF_XW + PW_PAD_F <= LDS_F), "LDS map");
 
+#if DCNSEP_TP_DUMP
+// diagnostic dump target (stif_dcnsep_dump_set): per thread 4 pairs x (9 taps x 8 blended samples + 32 accumulators),
+// then the 112 phase-1 results phase 2 reads (offsets, sigmoid(mask)), then 4 pairs x 9 taps x the 4 corner weights
+__device__ float* g_tp_dump;
+// + pair 0 tap 0's eight corner vectors and four weights stored right before the blend (TP_DUMP 2: before, else after)
+constexpr int TPD_F = 4 * (9 * 8 + 32) + 112 + 4 * 9 * 4 + 32;
+#endif
+
 // vmcnt waits with an immediate operand (the counts are wave-uniform)
 STIF_DEV void wait_vm(int n) {
   switch (n) {
@@ -279,6 +287,15 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_
   }
   const bool bad = not_finite(chk);
   report_range(a.status, bad);
+#if DCNSEP_TP_DUMP
+  if (g_tp_dump) {
+    float* d = g_tp_dump + ((size_t)blockIdx.x * (64 * NW) + tid) * TPD_F + 4 * (9 * 8 + 32);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int r = 0; r < 16; r += 4) st4(d + 16 * m + r, f32x4{om[m][r], om[m][r + 1], om[m][r + 2], om[m][r + 3]});
+  }
+#endif
 
   // ---------------------------------------------------------------- phase 2: deformable conv
   // bilinear sample of this lane half's group (channels 16 pa + 8 h .. + 7: a0 = quad 2h, a1 = quad 2h + 1)
@@ -473,7 +490,28 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_
         }
       }
 #endif
+#if DCNSEP_TP_DUMP == 2
+      if (g_tp_dump && pa == 0 && t == 0) {
+        float* d = g_tp_dump + ((size_t)blockIdx.x * (64 * NW) + tid) * TPD_F;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) st4(d + TPD_F - 32 + 4 * k, cur.v[k]);
+        st4(d + 4 * (9 * 8 + 32) + 112, f32x4{cur.w1, cur.w2, cur.w3, cur.w4});
+      }
+#endif
       finish(cur, a0, a1);
+#if DCNSEP_TP_DUMP
+      if (g_tp_dump) {
+        float* d = g_tp_dump + ((size_t)blockIdx.x * (64 * NW) + tid) * TPD_F + pa * (9 * 8 + 32) + t * 8;
+        st4(d, a0);
+        st4(d + 4, a1);
+        if (DCNSEP_TP_DUMP == 1 || pa || t)
+          st4(g_tp_dump + ((size_t)blockIdx.x * (64 * NW) + tid) * TPD_F + 4 * (9 * 8 + 32) + 112 + (pa * 9 + t) * 4,
+              f32x4{cur.w1, cur.w2, cur.w3, cur.w4});
+        if (DCNSEP_TP_DUMP == 1 && pa == 0 && t == 0)
+#pragma unroll
+          for (int k = 0; k < 8; ++k) st4(g_tp_dump + ((size_t)blockIdx.x * (64 * NW) + tid) * TPD_F + TPD_F - 32 + 4 * k, cur.v[k]);
+      }
+#endif
       f16x8 ah, al;
       split_f16x3(a0, a1, ah, al);
       acc0 = mfma16h(ah, bh0, acc0);
@@ -485,6 +523,16 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_
       __builtin_amdgcn_sched_barrier(0);
       if (t < 8) cur = nxt;
     }
+#if DCNSEP_TP_DUMP
+    if (g_tp_dump) {
+      float* d = g_tp_dump + ((size_t)blockIdx.x * (64 * NW) + tid) * TPD_F + pa * (9 * 8 + 32) + 72;
+#pragma unroll
+      for (int r = 0; r < 16; r += 4) {
+        st4(d + r, f32x4{acc0[r], acc0[r + 1], acc0[r + 2], acc0[r + 3]});
+        st4(d + 16 + r, f32x4{acc1[r], acc1[r + 1], acc1[r + 2], acc1[r + 3]});
+      }
+    }
+#endif
 #else
     // a tap-level software pipeline (tap t + 1's corner reads issued before tap t's blend, one more
     // sample set live) measured 4 % faster in the C0 step but made the outputs depend on the launch's
@@ -545,6 +593,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_
 }
 
 }  // namespace
+
+#if DCNSEP_TP_DUMP
+extern "C" int stif_dcnsep_dump_set(float* p) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_tp_dump), &p, sizeof(p)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int stif_dcn_sep_nhwc(const stif_dcn_sep_args* pa, void* stream) {
   if (!pa) return stif_fail(STIF_E_INVALID, "stif_dcn_sep_nhwc: null args");

@@ -60,6 +60,9 @@ static_assert(WINO_UPQ == 0 || WINO_UPQ == 1, "WINO_UPQ");
 #ifndef DCNSEP_TP_CHECK
 #define DCNSEP_TP_CHECK 0  // diagnostic (TAPPIPE): every staged corner / B fragment read checked against HBM (printf)
 #endif
+#ifndef DCNSEP_TP_DUMP
+#define DCNSEP_TP_DUMP 0   // diagnostic (TAPPIPE): per-thread dump of every tap's blended samples and each pair's accumulators
+#endif
 #ifndef DCNSEP_P1_SAFE
 #define DCNSEP_P1_SAFE 0   // diagnostic: phase-1 steps behind full drains and __syncthreads
 #endif
