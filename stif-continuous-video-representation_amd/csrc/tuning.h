@@ -24,7 +24,8 @@ static_assert(WINO_UPQ == 0 || WINO_UPQ == 1, "WINO_UPQ");
 #ifndef WINO_EXP
 #define WINO_EXP 0         // probes: 1 no LDS-DMA after the first phase, 2 no B refills, 3 no output exchange,
                            // 4 no x2-upsample expansion (in1_mode 2), 5 RELU-epilogue convs store nothing,
-                           // 6 k_wino_om stores nothing (out-of-range store offsets)
+                           // 6 k_wino_om stores nothing (out-of-range store offsets), 7 RELU-epilogue convs do a
+                           // third chunk-pair pass per phase (1.5x work: a conv1 over its 1-px halo) and store nothing
 #endif
 
 // ---- k_dcn (dcn.hip): the DCN core of the two-kernel path and the _ext drop-in at the STIF shape

@@ -355,23 +355,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
           if (p + 1 < NP) stage(cur, p + 1, (gp + 1) & 1);
           else if (has_next) stage(nxt, 0, (gp + 1) & 1);
         }
+        // probe 7 (the fused ResidualBlock's conv1 cost floor): the RELU conv does a third chunk-pair pass per
+        // phase (chunks 0, 1 again) = 1.5x its transform / split / MFMA work, the work of a conv1 over the
+        // 1-px halo of the next conv's tile, and stores nothing (as probe 5)
+        constexpr int SPN = (WINO_EXP == 7 && EPI == STIF_EPI_RELU) ? PSUB / 2 + 1 : PSUB / 2;
 #pragma unroll
-        for (int sp = 0; sp < PSUB / 2; ++sp) {
+        for (int sp = 0; sp < SPN; ++sp) {
           // chunk pair (2 sp, 2 sp + 1): lane half h holds channels 4h..4h+3 of both, i.e. the 8
           // K values of a 32x32x16 f16 MFMA; transform both, split all four j, then fetch the next
           // pair's first chunk so its LDS reads hide under this pair's MFMAs
           f32x4 va[4], vb[4];
           xform(rd, va);
-          xread(buf, 2 * sp + 1, rd);
+          xread(buf, (2 * sp + 1) % PSUB, rd);
           xform(rd, vb);
-          const int q = p * (PSUB / 2) + sp;
+          const int q = p * (PSUB / 2) + sp % (PSUB / 2);
           const float* wq = wsl + (size_t)q * 16384;
           const float* wq1 = q + 1 < NQ ? wq + 16384 : wnx;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             f16x8 ah, al;
             split_f16x3(va[j], vb[j], ah, al);
-            if (j == XREAD_J && 2 * sp + 2 < PSUB) xread(buf, 2 * sp + 2, rd);
+            if (j == XREAD_J && 2 * sp + 2 < 2 * SPN) xread(buf, (2 * sp + 2) % PSUB, rd);
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
               acc[j][u] = mfma16h(ah, bh[j & 1][u], acc[j][u]);
@@ -544,7 +548,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, cn), ro2, voff(nt, k), 0, 0);
           continue;
         }
-        if (WINO_EXP != 5 || EPI != STIF_EPI_RELU)   // probe 5: the ResidualBlock's conv1 stores nothing
+        if ((WINO_EXP != 5 && WINO_EXP != 7) || EPI != STIF_EPI_RELU)   // probes 5, 7: the ResidualBlock's conv1 stores nothing
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, y), ro,
                                                  voff(nt, k), 0, 0);
       }

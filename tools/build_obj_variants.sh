@@ -8,7 +8,7 @@ SRC=$1; shift
 PKG=stif-continuous-video-representation_amd
 make -s -j8 > /dev/null
 NOPK=""
-case " wino decoder conv resample " in *" $SRC "*) NOPK="-Xclang -target-feature -Xclang -packed-fp32-ops";; esac
+case " wino decoder conv resample dcnsep dcn " in *" $SRC "*) NOPK="-Xclang -target-feature -Xclang -packed-fp32-ops";; esac
 for v in "$@"; do
   flags=""
   for f in ${v//+/ }; do flags="$flags -D$f"; done
