@@ -35,6 +35,51 @@ def test_library_exports_every_header_symbol(stif):
     assert set(stif._lib.EXPORTS) >= names
 
 
+def _device_code_objects(path):
+    """The gfx950 code objects of a HIP shared library: its .hip_fatbin holds one clang offload bundle per
+    translation unit (magic, entry count, then per entry offset / size / target-triple, little-endian u64)."""
+    import struct
+    data = open(path, "rb").read()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    out, pos = [], data.find(magic)
+    while pos >= 0:
+        n = struct.unpack_from("<Q", data, pos + 24)[0]
+        q = pos + 32
+        for _ in range(n):
+            off, size, tlen = struct.unpack_from("<QQQ", data, q)
+            triple = data[q + 24:q + 24 + tlen].decode()
+            q += 24 + tlen
+            if "amdgcn" in triple and "gfx950" in triple:
+                out.append((triple, data[pos + off:pos + off + size]))
+        pos = data.find(magic, pos + 24)
+    return out
+
+
+def test_device_code_has_no_packed_fp32(stif, tmp_path):
+    """No kernel may use packed fp32 VALU (v_pk_fma/mul/add_f32): beside MFMAs it is slower than two scalar ops, and in
+    the tap-pipelined DCN_sep schedule its results depended on the co-resident workgroup (DESIGN.md section 3d,
+    profiles/r06_tappipe_dump_bisect.log).  Makefile: NOPK_SRC lists every .hip object."""
+    import shutil
+    import subprocess
+    objdump = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    if not os.path.exists(objdump) or shutil.which("/opt/rocm/lib/llvm/bin/llvm-objdump") is None:
+        pytest.skip("llvm-objdump not available")
+    lib = stif._lib.LIB_PATH
+    cos = _device_code_objects(lib)
+    csrc = os.path.join(REPO, "stif-continuous-video-representation_amd", "csrc")
+    kernels = [f for f in os.listdir(csrc) if f.endswith(".hip") and "__global__" in open(os.path.join(csrc, f)).read()]
+    assert len(cos) >= len(kernels), (len(cos), kernels)
+    total = 0
+    for i, (triple, co) in enumerate(cos):
+        f = tmp_path / f"co{i}.elf"
+        f.write_bytes(co)
+        asm = subprocess.run([objdump, "-d", "--mcpu=gfx950", str(f)], capture_output=True, text=True, check=True).stdout
+        n_ins = len(re.findall(r"^\s+v_\w+", asm, re.M))
+        total += n_ins
+        assert not re.search(r"\bv_pk_(fma|mul|add)_f32\b", asm), f"packed fp32 in code object {i} ({triple})"
+    assert total > 10000   # the disassembly really covered the kernels
+
+
 def _unpack_conv(wd, cout_pad, cin, ks, nt):
     """inverse of the [slice][chunk][tap][nt][lane][4] packing -> [cout_pad][cin][ks][ks]"""
     ns = cout_pad // (32 * nt)
