@@ -237,28 +237,31 @@ STIF_DEV f32x4 img_sample(const float* __restrict__ I, const Bilin& b, int hf) {
 // waves per workgroup of k_dec1: 4-wave workgroups, DEC1_OCC per CU -- by default 4 (36 KB LDS, <= 128 VGPRs
 // each; the HRIMG variants stay at 3: 52 KB, <= 168, and MODE 2 at 2: 69 KB): the waves sharing a SIMD come from different
 // workgroups, so one's segment barrier, gather or sin stretch overlaps the others' MFMAs
-constexpr int DEC_NW = DEC1_NW;
 constexpr int DEC2_NW = 4;   // k_dec2: 8 layer-3 accumulator tiles (128 VGPRs) live
 constexpr int SEG = 10;      // max tiles per segment (k_dec2)
 constexpr int SEG1 = 8;      // max tiles per segment (k_dec1)
 
 // Buffer loads with the tile offset in SGPRs: the per-lane operand is the same lane*16 for every
 // tile (flat global_load_lds would keep a 64-bit VGPR address per hoisted tile live).
-template <int NW>
-STIF_DEV void dma_tiles(float* dst, __amdgpu_buffer_rsrc_t rm, int src, int ntiles, int wv, int lane) {
-#if DEC_EXP == 1   // timing probe: no weight streaming (the MLPs run on whatever the LDS holds)
+// Probes: DEC_EXP 1 issues no weight DMA at all; DEC_EXP 3 issues every piece with an out-of-range offset (the
+// same instructions, no memory traffic: the LDS receives zeros)
+STIF_DEV void dec_dma(__amdgpu_buffer_rsrc_t rm, float* dst, int lane, int soff) {
+#if DEC_EXP == 1
   return;
 #endif
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rm, dst, 16, DEC_EXP == 3 ? 0x80000000u : (unsigned)(lane * 16), soff, 0, 0);
+}
+template <int NW>
+STIF_DEV void dma_tiles(float* dst, __amdgpu_buffer_rsrc_t rm, int src, int ntiles, int wv, int lane) {
   if ((ntiles * 4) % NW == 0) {
     // the same number of pieces per wave, known at compile time: the compiler counts them in vmcnt, so
     // waiting for a load issued before the DMA does not wait for the DMA
 #pragma unroll
     for (int i = 0; i < ntiles * 4 / NW; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rm, dst + (wv + i * NW) * 256, 16, lane * 16,
-                                               (src + (wv + i * NW) * 256) * 4, 0, 0);
+      dec_dma(rm, dst + (wv + i * NW) * 256, lane, (src + (wv + i * NW) * 256) * 4);
   } else {
     for (int k = wv; k < ntiles * 4; k += NW)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rm, dst + k * 256, 16, lane * 16, (src + k * 256) * 4, 0, 0);
+      dec_dma(rm, dst + k * 256, lane, (src + k * 256) * 4);
   }
 }
 
@@ -395,7 +398,7 @@ __global__ __launch_bounds__((NW1<MODE, HRIMG> * 64)) __attribute__((amdgpu_wave
     for (int r = 0; r < 16 / DEC_NW; ++r) {
       const int i = wv + r * DEC_NW, j = i >> 2;
       const int src = (j < 2 ? F_W2 + (kt * 2 + j) * T : F_W3 + ((j - 2) * 8 + kt) * T) + (i & 3) * 256;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rm, dst + j * T + (i & 3) * 256, 16, lane * 16, src * 4, 0, 0);
+      dec_dma(rm, dst + j * T + (i & 3) * 256, lane, src * 4);
     }
   };
   dec_barrier();
@@ -425,14 +428,18 @@ __global__ __launch_bounds__((NW1<MODE, HRIMG> * 64)) __attribute__((amdgpu_wave
     __builtin_amdgcn_sched_barrier(0);
     float* cur = (kt & 1) ? B0 : B1;
     float* nxt = (kt & 1) ? B1 : B0;
-    if (!last) seg_feat23(nxt, kt + 1);
-    else {   // prefetch flow layer 0 (4 tiles) + layer 1 (4 tiles; OCC3: its first output tile)
-      dma_tiles<DEC_NW>(nxt, rm, L_W0, 4, wv, lane);
-      if (!OCC4) dma_tiles<DEC_NW>(nxt + 4 * T, rm, L_W1, OCC3 ? 2 : 4, wv, lane);
-    }
+    auto dma_next = [&]() {
+      if (!last) seg_feat23(nxt, kt + 1);
+      else {   // prefetch flow layer 0 (4 tiles) + layer 1 (4 tiles; OCC3: its first output tile)
+        dma_tiles<DEC_NW>(nxt, rm, L_W0, 4, wv, lane);
+        if (!OCC4) dma_tiles<DEC_NW>(nxt + 4 * T, rm, L_W1, OCC3 ? 2 : 4, wv, lane);
+      }
+    };
+    if (!DEC_DMA_LATE) dma_next();
     f32x16 acc = f32x16{0};
     tile_mma<F16>(acc, cur, x1s[0], lane);
     tile_mma<F16>(acc, cur + T, x1s[1], lane);
+    if (DEC_DMA_LATE) dma_next();
     const XT<F16> h2 = xop<F16>(bias_sin<F16>(acc, b2));
     tile_mma<F16>(hr[0], cur + 2 * T, h2, lane);
     tile_mma<F16>(hr[1], cur + 3 * T, h2, lane);
@@ -541,10 +548,11 @@ __global__ __launch_bounds__((NW1<MODE, HRIMG> * 64)) __attribute__((amdgpu_wave
     // OCC4: segment 0 sits in B1, so the buffers alternate the other way round
     float* cur = OCC4 ? ((kt & 1) ? B0 : B1) : (kt & 1) ? B1 : (L1B0 && kt == 0 ? B0 + 2 * T : B0);
     float* nxt = OCC4 ? ((kt & 1) ? B1 : B0) : (kt & 1) ? B0 : B1;
-    if (!last) seg_flow23(nxt, kt + 1);
+    if (!last && !DEC_DMA_LATE) seg_flow23(nxt, kt + 1);
     f32x16 acc = f32x16{0};
     tile_mma<F16>(acc, cur, x1f[0], lane);
     tile_mma<F16>(acc, cur + T, x1f[1], lane);
+    if (!last && DEC_DMA_LATE) seg_flow23(nxt, kt + 1);
     const f32x16 h2 = bias_sin<F16>(acc, b2);
     narrow_dot<4>(fl, W3V, kt, h2, hf);   // flow_imnet.net.3 (256 -> 4, linear)
   };
@@ -825,7 +833,7 @@ __global__ __launch_bounds__(DEC2Q_NWV * 64) __attribute__((amdgpu_waves_per_eu(
       const int i = wv + r * NW;                // piece i: tile j = i / 4 of the segment, quarter i % 4
       const int j = i >> 2, k = j / 10, jj = j - 10 * k, kt = sg * KTS + k;
       const int src = (jj < 2 ? Q_W2 + (kt * 2 + jj) * T : Q_W3 + ((jj - 2) * 8 + kt) * T) + (i & 3) * 256;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rm, dst + j * T + (i & 3) * 256, 16, lane * 16, src * 4, 0, 0);
+      dec_dma(rm, dst + j * T + (i & 3) * 256, lane, src * 4);
     }
   };
   const long long total = (long long)n * HH * WW;
@@ -920,8 +928,11 @@ __global__ __launch_bounds__(DEC2Q_NWV * 64) __attribute__((amdgpu_waves_per_eu(
     __builtin_amdgcn_sched_barrier(0);
     float* cur = (sg & 1) ? B1 : B0;
     float* nxt = (sg & 1) ? B0 : B1;
-    if (!last) seg_l23(nxt, sg + 1);
-    else dma_tiles<NW>(nxt, rm, E_W4V, 1, wv, lane);
+    auto dma_next = [&]() {
+      if (!last) seg_l23(nxt, sg + 1);
+      else dma_tiles<NW>(nxt, rm, E_W4V, 1, wv, lane);
+    };
+    if (!DEC_DMA_LATE) dma_next();
 #pragma unroll
     for (int k = 0; k < KTS; ++k) {
       const float* sk = cur + k * 10 * T;
@@ -929,6 +940,7 @@ __global__ __launch_bounds__(DEC2Q_NWV * 64) __attribute__((amdgpu_waves_per_eu(
       acc.s[0] = acc.s[1] = f32x4{0.f, 0.f, 0.f, 0.f};
       tile_q(acc, sk, x1s[0], lane);
       tile_q(acc, sk + T, x1s[1], lane);
+      if (DEC_DMA_LATE && k == 0) dma_next();
       const XQ h2 = xq(bias_sin_q(acc, b2[k]));
 #pragma unroll
       for (int ot = 0; ot < 8; ++ot) tile_q(a3[ot], sk + (2 + ot) * T, h2, lane);

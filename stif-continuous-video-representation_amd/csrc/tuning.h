@@ -106,6 +106,10 @@ static_assert(DCNSEP_EXP == 0 || DCNSEP_EXP == 1 || DCNSEP_EXP == 3 || DCNSEP_EX
 // fp32 and high-resolution-image stages)
 #define DEC2_Q16 1
 #endif
+#ifndef DEC_DMA_LATE
+#define DEC_DMA_LATE 0     // decoders: issue the next weight segment's LDS-DMA after the step's first (layer-2) MFMAs, in the
+                           // sine / split stretch, instead of right after the segment barrier
+#endif
 #ifndef DEC2Q_NW
 #define DEC2Q_NW 8         // k_dec2q waves per workgroup (8: two 80-KB workgroups per CU; 16: one 160-KB workgroup)
 #endif
@@ -119,6 +123,7 @@ static_assert(DEC1_OCC >= 2 && DEC1_OCC <= 4, "DEC1_OCC: k_dec1 is laid out for 
 static_assert(DEC2_Q16 == 0 || DEC2_Q16 == 1, "DEC2_Q16: 0 (k_dec2) or 1 (k_dec2q)");
 #ifndef DEC_EXP
 #define DEC_EXP 0          // probes: 1 no MLP weight streaming into LDS, 2 segment barriers without the vmcnt(0)
-                           // wait for the segment (wrong results)
+                           // wait for the segment, 3 every weight DMA piece issued out of range (same instructions,
+                           // no memory traffic, zero weights) -- all with wrong results
 #endif
-static_assert(DEC_EXP == 0 || DEC_EXP == 1 || DEC_EXP == 2, "DEC_EXP");
+static_assert(DEC_EXP >= 0 && DEC_EXP <= 3, "DEC_EXP");
