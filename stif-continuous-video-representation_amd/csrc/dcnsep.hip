@@ -82,11 +82,20 @@ __device__ float* g_tp_dump;
 constexpr int TPD_F = 4 * (9 * 8 + 32) + 112 + 4 * 9 * 4 + 32;
 #endif
 
+#if DCNSEP_TRACE
+// per wave 8 u32: start (low bits), phase-1 end, phase-2 end, end (relative to start), phase-1 vmcnt-wait sum,
+// phase-1 barrier sum, phase-2 stage + wait sum, workgroup id
+__device__ unsigned* g_trace;
+STIF_DEV unsigned tstamp() { return (unsigned)__builtin_amdgcn_s_memtime(); }
+#endif
+
 // vmcnt waits with an immediate operand (the counts are wave-uniform)
 STIF_DEV void wait_vm(int n) {
   switch (n) {
     case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
     case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
     case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
     case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
     case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
@@ -105,6 +114,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_
   if (a.H < 0) reinterpret_cast<volatile float*>(solo_pad)[threadIdx.x] = 0.f;
 #endif
   const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, hf = lane >> 5;
+#if DCNSEP_TRACE
+  const unsigned tr_t0 = tstamp();
+  unsigned tr_vm = 0, tr_bar = 0, tr_p2w = 0, tr_p1e = 0, tr_p2e = 0;
+#endif
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = a.H, W = a.W;
   const int tiles_x = (W + TW - 1) / TW, tiles = tiles_x * ((H + NW - 1) / NW);
@@ -211,9 +224,16 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_
       // last two steps (weights of k + 1, the side stage of tap 1) may stay in flight
       // weight DMA instructions per wave and step (DCNSEP_WTRIM: wave-uniform, 4 or 3)
       const int WQ = (DCNSEP_WTRIM && NW == 4) ? (wv < MT * 2 - 3 * NW ? 4 : 3) : WK_INS / NW;
+#if DCNSEP_TRACE
+      const unsigned tr_a = tstamp();
+#endif
       if (t == 2 || t == 3) wait_vm(c < 3 ? WQ + D_INS / NW : (PAIR_AHEAD ? WQ + P_INS / NW : WQ));
       else if (t == 8 && c == 3) wait_vm(0);
       else wait_vm(WQ);
+#if DCNSEP_TRACE
+      const unsigned tr_b = tstamp();
+      tr_vm += tr_b - tr_a;
+#endif
       // a bare s_barrier: __syncthreads()'s workgroup fence would wait for vmcnt(0), i.e. for the DMA of
       // the next two steps too.  Every LDS read of the step that frees a ring slot has returned (its
       // MFMAs consumed it), and LDS-DMA visibility is the vmcnt wait above.
@@ -224,6 +244,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_
 #endif
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+#if DCNSEP_TRACE
+      tr_bar += tstamp() - tr_b;
+#endif
       // the first weight fragments right after the barrier; this step's data fragment was read and split
       // during the previous step (a chunk's first tap: read now), so the MFMAs start at once, and the
       // next steps' LDS-DMA is issued behind the first M-tile's MFMAs
@@ -265,6 +288,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_
   }
 #if DCNSEP_EXP == 1
   if (PAIR_AHEAD) stage_pair(0, smem + OFF_XT, smem + OFF_XW);
+#endif
+#if DCNSEP_TRACE
+  tr_p1e = tstamp() - tr_t0;
 #endif
   // slot s = 16 m + r of lane half h = component s % 3 (dy, dx, mask) of tap (s % 27) / 3 of group
   // 2 (s / 27) + h, packed row (r & 3) + 8 (r >> 2) + 4 h of M-tile m; bias, unscale, sigmoid(mask)
@@ -374,9 +400,15 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_
         lds_dma_barrier();
       }
 #else
+#if DCNSEP_TRACE
+      const unsigned tr_c = tstamp();
+#endif
       if (pa) __syncthreads();   // every wave is done with the previous pair's buffer
       stage_pair(pa, smem + OFF_XT, smem + OFF_XW);
-      lds_dma_barrier();
+      if (!DCNSEP_P2PROG) lds_dma_barrier();   // else per tap group in the tap loop
+#if DCNSEP_TRACE
+      tr_p2w += tstamp() - tr_c;
+#endif
 #endif
     }
     const float* st = smem + ((PAIR_AHEAD && (pa & 1)) ? OFF_YT : OFF_XT);
@@ -537,8 +569,19 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_
     // a tap-level software pipeline (tap t + 1's corner reads issued before tap t's blend, one more
     // sample set live) measured 4 % faster in the C0 step but made the outputs depend on the launch's
     // timing at two waves per SIMD; not kept
+    // DCNSEP_P2PROG (NW 4): each wave issued its stage pieces as 6 tile pieces, then one weight piece per tap in tap
+    // order (stage_pair: instruction wv + 4 j), so "tile + taps <= u landed" is vmcnt(8 - u) per wave, published to the
+    // other waves by the barrier after it (the reads follow the barrier)
+    static_assert(DCNSEP_P2PROG == 0 || (!PAIR_AHEAD && NW == 4 && T_INST == 24 && P_INS == 60 &&
+                                         (DCNSEP_P2PROG == 3 || DCNSEP_P2PROG == 9)), "DCNSEP_P2PROG");
+    constexpr int P2G = DCNSEP_P2PROG ? 9 / DCNSEP_P2PROG : 9;   // taps per wait group
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
+      if (DCNSEP_P2PROG && !PAIR_AHEAD && t % P2G == 0) {
+        wait_vm(8 - (t + P2G - 1));
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
       const int s = 27 * pa + 3 * t;   // this lane half's group 2 pa + h, tap t: slots s .. s + 2
       f32x4 a0, a1;
       sample(st, pa, t, om[s / 16][s % 16], om[(s + 1) / 16][(s + 1) % 16], om[(s + 2) / 16][(s + 2) % 16], a0, a1);
@@ -565,6 +608,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_
              "first %d\n", (int)blockIdx.x, wv, oy0, ox0, g, n, H, __builtin_popcountll(m), tp_bad, tp_badw, tp_first);
   }
 #endif
+#if DCNSEP_TRACE
+  tr_p2e = tstamp() - tr_t0;
+#endif
   if (!PAIR_AHEAD) __syncthreads();   // the epilogue blocks overwrite the pair buffer
   // epilogue through a per-wave LDS block -> coalesced 16-B stores (k_dcn's)
   float* out = a.out[g] + (size_t)n * a.out_item;
@@ -590,9 +636,24 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_
     }
   }
   report_range(a.status, not_finite(chk2));
+#if DCNSEP_TRACE
+  if (g_trace && lane == 0) {
+    const unsigned tr_end = tstamp() - tr_t0;
+    unsigned* d = g_trace + ((size_t)blockIdx.x * NW + wv) * 8;
+    typedef unsigned u32x4t __attribute__((ext_vector_type(4)));
+    *reinterpret_cast<u32x4t*>(d) = u32x4t{tr_t0, tr_p1e, tr_p2e, tr_end};
+    *reinterpret_cast<u32x4t*>(d + 4) = u32x4t{tr_vm, tr_bar, tr_p2w, blockIdx.x};
+  }
+#endif
 }
 
 }  // namespace
+
+#if DCNSEP_TRACE
+extern "C" int stif_dcnsep_trace_set(unsigned* p) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &p, sizeof(p)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 #if DCNSEP_TP_DUMP
 extern "C" int stif_dcnsep_dump_set(float* p) {

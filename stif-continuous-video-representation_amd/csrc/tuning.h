@@ -64,6 +64,13 @@ static_assert(WINO_UPQ == 0 || WINO_UPQ == 1, "WINO_UPQ");
 #ifndef DCNSEP_TP_DUMP
 #define DCNSEP_TP_DUMP 0   // diagnostic (TAPPIPE): per-thread dump of every tap's blended samples and each pair's accumulators
 #endif
+#ifndef DCNSEP_P2PROG
+#define DCNSEP_P2PROG 0    // fused DCN_sep phase 2 (NW 4): 0 = wait for the whole pair stage; 3 / 9 = wait in 3 / 9 steps (the
+                           // tile + the first taps' weights, then the next taps'), so the taps start while later weights land
+#endif
+#ifndef DCNSEP_TRACE
+#define DCNSEP_TRACE 0     // diagnostic: per-wave s_memtime sums of k_dcn_sep's waits and phases (stif_dcnsep_trace_set)
+#endif
 #ifndef DCNSEP_P1_SAFE
 #define DCNSEP_P1_SAFE 0   // diagnostic: phase-1 steps behind full drains and __syncthreads
 #endif
