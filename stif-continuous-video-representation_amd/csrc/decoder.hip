@@ -243,12 +243,10 @@ constexpr int SEG1 = 8;      // max tiles per segment (k_dec1)
 
 // Buffer loads with the tile offset in SGPRs: the per-lane operand is the same lane*16 for every
 // tile (flat global_load_lds would keep a 64-bit VGPR address per hoisted tile live).
-// Probes: DEC_EXP 1 issues no weight DMA at all; DEC_EXP 3 issues every piece with an out-of-range offset (the
-// same instructions, no memory traffic: the LDS receives zeros)
+// Probe DEC_EXP 3 issues every piece with an out-of-range offset (the same instructions, no memory traffic: the
+// LDS receives zeros).  (A probe that issued no DMA at all, the former DEC_EXP 1, measured nothing: with the
+// weight buffers never written the compiler folded most of the MFMAs, LDS reads and sines that read them.)
 STIF_DEV void dec_dma(__amdgpu_buffer_rsrc_t rm, float* dst, int lane, int soff) {
-#if DEC_EXP == 1
-  return;
-#endif
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rm, dst, 16, DEC_EXP == 3 ? 0x80000000u : (unsigned)(lane * 16), soff, 0, 0);
 }
 template <int NW>
@@ -570,6 +568,205 @@ __global__ __launch_bounds__((NW1<MODE, HRIMG> * 64)) __attribute__((amdgpu_wave
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Stage 1 with resident weights (DEC1_RES, split-fp16, LR-image inputs; measured, not the default): the streamed
+// k_dec1 has every 128-pixel workgroup stream all 244 KB of its weights through LDS behind per-segment barriers.
+// Here the stage runs as two persistent kernels, one 16-wave workgroup per CU, that load their network's weights
+// into LDS once and then walk 32-pixel blocks with no barrier and no stream:
+//   k_dec1f: feat_imnet (W1 | W2 | W3 = 36 tiles, 144 KB) -> HRfeat (64 per HR pixel, stored);
+//   k_dec1l: flow_imnet (W0 | W1 | W2 = 24 tiles + the plain [4][256] W3, 100 KB), its HRfeat operand read back
+//            from HBM (256 B per HR pixel) -> flow.
+// Same arithmetic, same order as k_dec1<0, false, 1> (bit-identical outputs), but 372 + 430 us vs 655 us at C0
+// (profiles/r06_dec_res.log): without stream and barriers k_dec1f runs at 0.37 and k_dec1l at 0.21 of their MFMA
+// time, so neither was what bounds stage 1.
+constexpr int RW = 16;   // waves per resident workgroup
+__global__ __launch_bounds__(RW * 64) __attribute__((amdgpu_waves_per_eu(4))) void k_dec1f(
+    const float* __restrict__ proj, const float* __restrict__ mlp, stif_dec_tables tb, const float* __restrict__ tq,
+    float* __restrict__ hrfeat, int n, int h, int w, int HH, int WW) {
+  __shared__ __attribute__((aligned(16))) float wr[36 * T];   // W1 (ot * 2 + kt) | W2 (kt * 2 + j) | W3 (ot * 8 + kt)
+  const int lane = threadIdx.x & 63, hf = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const __amdgpu_buffer_rsrc_t rm = mlp_rsrc(mlp);
+  dma_tiles<RW>(wr, rm, F_W1, 4, wv, lane);
+  dma_tiles<RW>(wr + 4 * T, rm, F_W2, 16, wv, lane);
+  dma_tiles<RW>(wr + 20 * T, rm, F_W3, 16, wv, lane);
+  lds_dma_barrier();
+  const long long total = (long long)n * HH * WW;
+  const long long nblk = (total + 31) / 32;
+  for (long long blk = (long long)blockIdx.x * RW + wv; blk < nblk; blk += (long long)gridDim.x * RW) {
+    // the weights in LDS are loop-invariant to the compiler, which would hoist their reads out of the block loop
+    // (and spill them): a memory clobber per block keeps every read next to its MFMAs
+    asm volatile("" ::: "memory");
+    const long long p = blk * 32 + (lane & 31);
+    const bool valid = p < total;
+    const long long pc = valid ? p : total - 1;
+    const int item = (int)(pc / ((long long)HH * WW));
+    const int rem = (int)(pc - (long long)item * HH * WW);
+    const int py = rem / WW, px = rem - py * WW;
+    const float t = tq[item];
+    const float* P = proj + (size_t)item * h * w * PROJ_C;
+    // layer 0: z = P1[nearest] + w_rel . rel + w_t * t (bias folded into P1)
+    f32x16 x0[2];
+    {
+      const float ry = tb.rel_y[py], rx = tb.rel_x[px];
+      const float* p1 = P + ((size_t)tb.near_y[py] * w + tb.near_x[px]) * PROJ_C;
+#pragma unroll
+      for (int ot = 0; ot < 2; ++ot)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int f = ot * 32 + 8 * v + 4 * hf;
+          const f32x4 z = ld4(p1 + f) + ld4(mlp + F_WRY + f) * ry + ld4(mlp + F_WRX + f) * rx + ld4(mlp + F_WT + f) * t;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) x0[ot][4 * v + e] = siren_sin<1>(z[e]);
+        }
+    }
+    // layer 1: 64 -> 64
+    f32x16 x1[2];
+    {
+      const Bias32 fb1[2] = {bias_ld(mlp + F_B1, hf), bias_ld(mlp + F_B1 + 32, hf)};
+      const XT<1> xs[2] = {xop<1>(x0[0]), xop<1>(x0[1])};
+#pragma unroll
+      for (int ot = 0; ot < 2; ++ot) {
+        f32x16 acc = f32x16{0};
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) tile_mma<1>(acc, wr + (ot * 2 + kt) * T, xs[kt], lane);
+        x1[ot] = bias_sin<1>(acc, fb1[ot]);
+      }
+    }
+    // layer 2 (64 -> 256, sine) tile by tile into layer 3 (256 -> 64, linear)
+    const XT<1> x1s[2] = {xop<1>(x1[0]), xop<1>(x1[1])};
+    f32x16 hr[2] = {f32x16{0}, f32x16{0}};
+#pragma unroll 1
+    for (int kt = 0; kt < 8; ++kt) {
+      const Bias32 b2 = bias_ld(mlp + F_B2 + kt * 32, hf);
+      f32x16 acc = f32x16{0};
+      tile_mma<1>(acc, wr + (4 + kt * 2) * T, x1s[0], lane);
+      tile_mma<1>(acc, wr + (5 + kt * 2) * T, x1s[1], lane);
+      const XT<1> h2 = xop<1>(bias_sin<1>(acc, b2));
+      tile_mma<1>(hr[0], wr + (20 + kt) * T, h2, lane);
+      tile_mma<1>(hr[1], wr + (28 + kt) * T, h2, lane);
+    }
+#pragma unroll
+    for (int ot = 0; ot < 2; ++ot) hr[ot] = bias_add<1>(hr[ot], mlp + F_B3 + ot * 32, hf);
+    if (valid) {
+      float* o = hrfeat + (size_t)pc * 64;
+#pragma unroll
+      for (int ot = 0; ot < 2; ++ot)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          f32x4 s4;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) s4[e] = hr[ot][4 * v + e];
+          st4(o + ot * 32 + 8 * v + 4 * hf, s4);
+        }
+    }
+  }
+}
+
+__global__ __launch_bounds__(RW * 64) __attribute__((amdgpu_waves_per_eu(4))) void k_dec1l(
+    const float* __restrict__ proj, const float* __restrict__ mlp, stif_dec_tables tb, const float* __restrict__ tq,
+    const float* __restrict__ hrfeat, float* __restrict__ flow, int n, int h, int w, int HH, int WW) {
+  __shared__ __attribute__((aligned(16))) float wr[25 * T];   // W0 (ot * 2 + kt) | W1 | W2 (kt * 2 + j) | W3 [4][256]
+  const int lane = threadIdx.x & 63, hf = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const __amdgpu_buffer_rsrc_t rm = mlp_rsrc(mlp);
+  dma_tiles<RW>(wr, rm, L_W0, 4, wv, lane);
+  dma_tiles<RW>(wr + 4 * T, rm, L_W1, 4, wv, lane);
+  dma_tiles<RW>(wr + 8 * T, rm, L_W2, 16, wv, lane);
+  dma_tiles<RW>(wr + 24 * T, rm, L_W3V, 1, wv, lane);
+  lds_dma_barrier();
+  const float* const W3V = wr + 24 * T;
+  const long long total = (long long)n * HH * WW;
+  const long long nblk = (total + 31) / 32;
+  for (long long blk = (long long)blockIdx.x * RW + wv; blk < nblk; blk += (long long)gridDim.x * RW) {
+    // the weights in LDS are loop-invariant to the compiler, which would hoist their reads out of the block loop
+    // (and spill them): a memory clobber per block keeps every read next to its MFMAs
+    asm volatile("" ::: "memory");
+    const long long p = blk * 32 + (lane & 31);
+    const bool valid = p < total;
+    const long long pc = valid ? p : total - 1;
+    const int item = (int)(pc / ((long long)HH * WW));
+    const int rem = (int)(pc - (long long)item * HH * WW);
+    const int py = rem / WW, px = rem - py * WW;
+    const float t = tq[item];
+    const float* P = proj + (size_t)item * h * w * PROJ_C;
+    // the pixel's own HRfeat (k_dec1f's output), in the register-tile order
+    f32x16 hr[2];
+    {
+      const float* hp = hrfeat + (size_t)pc * 64 + 4 * hf;
+#pragma unroll
+      for (int ot = 0; ot < 2; ++ot)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const f32x4 q = ld4(hp + ot * 32 + 8 * v);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) hr[ot][4 * v + e] = q[e];
+        }
+    }
+    // layer 0: W[:, :64] . HRfeat + bilinear(P2 at the HR centre) + w_t * t + b
+    f32x16 z[2];
+    {
+      Bilin b;
+      const int y0 = tb.by0[py], y1 = tb.by1[py], x0_ = tb.bx0[px], x1_ = tb.bx1[px];
+      const float wy0 = tb.wy0[py], wy1 = tb.wy1[py], wx0 = tb.wx0[px], wx1 = tb.wx1[px];
+      b.o00 = y0 * w + x0_; b.o01 = y0 * w + x1_; b.o10 = y1 * w + x0_; b.o11 = y1 * w + x1_;
+      b.w00 = wx0 * wy0; b.w01 = wx1 * wy0; b.w10 = wx0 * wy1; b.w11 = wx1 * wy1;
+      gather64_q(z, P, PROJ_C, 64, b, hf);
+#pragma unroll
+      for (int ot = 0; ot < 2; ++ot)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int f = ot * 32 + 8 * v + 4 * hf;
+          const f32x4 wt = ld4(mlp + L_WT + f), bb = ld4(mlp + L_B0 + f);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) z[ot][4 * v + e] = (z[ot][4 * v + e] + (wt[e] * t + bb[e])) * ACC_IN<1>;
+        }
+    }
+    {
+      const XT<1> hs[2] = {xop<1>(hr[0]), xop<1>(hr[1])};
+#pragma unroll
+      for (int ot = 0; ot < 2; ++ot) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) tile_mma<1>(z[ot], wr + (ot * 2 + kt) * T, hs[kt], lane);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) z[ot][r] = siren_sin<1>(z[ot][r] * ACC_S<1>);
+      }
+    }
+    f32x16 x1[2];
+    {
+      const Bias32 lb1[2] = {bias_ld(mlp + L_B1, hf), bias_ld(mlp + L_B1 + 32, hf)};
+      const XT<1> zs[2] = {xop<1>(z[0]), xop<1>(z[1])};
+#pragma unroll
+      for (int ot = 0; ot < 2; ++ot) {
+        f32x16 acc = f32x16{0};
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) tile_mma<1>(acc, wr + (4 + ot * 2 + kt) * T, zs[kt], lane);
+        x1[ot] = bias_sin<1>(acc, lb1[ot]);
+      }
+    }
+    const XT<1> x1f[2] = {xop<1>(x1[0]), xop<1>(x1[1])};
+    float fl[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int kt = 0; kt < 8; ++kt) {
+      const Bias32 b2 = bias_ld(mlp + L_B2 + kt * 32, hf);
+      f32x16 acc = f32x16{0};
+      tile_mma<1>(acc, wr + (8 + kt * 2) * T, x1f[0], lane);
+      tile_mma<1>(acc, wr + (9 + kt * 2) * T, x1f[1], lane);
+      const f32x16 h2 = bias_sin<1>(acc, b2);
+      narrow_dot<4>(fl, W3V, kt, h2, hf);
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) fl[c] += __shfl_xor(fl[c], 32);
+    if (valid && hf == 0) {
+      const f32x4 bb = ld4(mlp + L_B3);
+      f32x4 s4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s4[e] = fl[e] + bb[e];
+      st4(flow + (size_t)pc * 4, s4);
+    }
+  }
+}
+
 template <bool HRIMG, int F16>
 __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DEC2_WPE))) void k_dec2(const float* __restrict__ proj, const float* __restrict__ mlp,
                                                      const float* __restrict__ hrfeat, const float* __restrict__ flow,
@@ -736,8 +933,8 @@ __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DE
 // registers between layers as in k_dec2.  The layer-3 state halves (8 tiles x 8 floats = 64 VGPRs): 128 VGPRs,
 // four waves per SIMD.
 // Weight streaming (round 6): every workgroup streams the whole 372-KB weight set through its LDS, so the
-// stream is paid once per workgroup -- with 4-wave 64-pixel workgroups it cost more than half the kernel (a
-// probe without it, DEC_EXP = 1: C0 stage 2 1,160 -> 480 us, profiles/r06_dec_probe.log).  Workgroups are
+// stream is paid once per workgroup; its memory traffic costs ~10 % of the kernel (pieces issued out of range,
+// DEC_EXP 3: profiles/r06_dec_probe3.log).  Workgroups are
 // DEC2Q_NW waves (8: 128 pixels, two per CU; 16: 256 pixels, one per CU) and a segment is the layer-2 / -3
 // weights of DEC2Q_KTS whole layer-2 tiles kt (W2 rows kt + W3 column kt: 10 tiles each), double-buffered in
 // 2 x 40 KB (KTS 1) or 2 x 80 KB (KTS 2): the weight bytes per pixel halve / quarter and one barrier per kt
@@ -1082,6 +1279,11 @@ extern "C" int stif_dec_stage1_ex(const float* proj, const float* mlp, const sti
     else launch_dec1<2, false>(f16, total, st, proj, mlp, *tab, im, t, hrfeat, flow, n, h, w, HH, WW);
   } else if (img) {
     launch_dec1<0, true>(f16, total, st, proj, mlp, *tab, im, t, hrfeat, flow, n, h, w, HH, WW);
+  } else if (DEC1_RES && f16) {   // resident-weight feat and flow kernels (persistent, one workgroup per CU)
+    const long long nblk = (total + 31) / 32;
+    const unsigned grid = (unsigned)std::max<long long>(1, std::min<long long>(stif_num_cus(), (nblk + RW - 1) / RW));
+    hipLaunchKernelGGL(k_dec1f, dim3(grid), dim3(RW * 64), 0, st, proj, mlp, *tab, t, hrfeat, n, h, w, HH, WW);
+    hipLaunchKernelGGL(k_dec1l, dim3(grid), dim3(RW * 64), 0, st, proj, mlp, *tab, t, hrfeat, flow, n, h, w, HH, WW);
   } else {
     launch_dec1<0, false>(f16, total, st, proj, mlp, *tab, im, t, hrfeat, flow, n, h, w, HH, WW);
   }

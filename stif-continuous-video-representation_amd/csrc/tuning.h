@@ -113,6 +113,9 @@ static_assert(DCNSEP_EXP == 0 || DCNSEP_EXP == 1 || DCNSEP_EXP == 3 || DCNSEP_EX
 // fp32 and high-resolution-image stages)
 #define DEC2_Q16 1
 #endif
+#ifndef DEC1_RES
+#define DEC1_RES 0         // stage 1 (f16x3, LR image) as two persistent resident-weight kernels k_dec1f + k_dec1l
+#endif
 #ifndef DEC_DMA_LATE
 #define DEC_DMA_LATE 0     // decoders: issue the next weight segment's LDS-DMA after the step's first (layer-2) MFMAs, in the
                            // sine / split stretch, instead of right after the segment barrier
@@ -129,8 +132,9 @@ static_assert(DCNSEP_EXP == 0 || DCNSEP_EXP == 1 || DCNSEP_EXP == 3 || DCNSEP_EX
 static_assert(DEC1_OCC >= 2 && DEC1_OCC <= 4, "DEC1_OCC: k_dec1 is laid out for 2, 3 or 4 workgroups per CU");
 static_assert(DEC2_Q16 == 0 || DEC2_Q16 == 1, "DEC2_Q16: 0 (k_dec2) or 1 (k_dec2q)");
 #ifndef DEC_EXP
-#define DEC_EXP 0          // probes: 1 no MLP weight streaming into LDS, 2 segment barriers without the vmcnt(0)
-                           // wait for the segment, 3 every weight DMA piece issued out of range (same instructions,
-                           // no memory traffic, zero weights) -- all with wrong results
+#define DEC_EXP 0          // probes: 2 segment barriers without the vmcnt(0) wait for the segment, 3 every weight
+                           // DMA piece issued out of range (same instructions, no memory traffic, zero weights) --
+                           // both with wrong results.  (1, no DMA at all, is gone: the compiler folds the work that
+                           // reads never-written LDS, profiles/r06_dec_probe3.log)
 #endif
-static_assert(DEC_EXP >= 0 && DEC_EXP <= 3, "DEC_EXP");
+static_assert(DEC_EXP == 0 || DEC_EXP == 2 || DEC_EXP == 3, "DEC_EXP");
