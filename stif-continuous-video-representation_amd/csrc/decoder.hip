@@ -942,6 +942,11 @@ __global__ __launch_bounds__(DEC2_NW * 64) __attribute__((amdgpu_waves_per_eu(DE
 // compiler's vmcnt bookkeeping stays exact.
 // Gathers: each lane fetches its own quarter of a 64-channel block (16 corner loads in flight).
 constexpr int DEC2Q_NWV = DEC2Q_NW;
+#if DEC_TRACE
+// diagnostic (stif_dec_trace_set): per k_dec2q wave 8 u32 -- life, gathers (incl. the flow load), segment-barrier
+// waits, layer-2/3 span (its barriers included) -- s_memtime ticks
+__device__ unsigned* g_dtrace;
+#endif
 constexpr int KTS = DEC2Q_KTS;            // layer-2 tiles per segment
 constexpr int SEGQ = 10 * KTS;            // tiles per segment
 static_assert(40 * KTS % DEC2Q_NWV == 0 && 32 % DEC2Q_NWV == 0 && 16 % DEC2Q_NWV == 0 && 8 % KTS == 0,
@@ -1015,6 +1020,15 @@ __global__ __launch_bounds__(DEC2Q_NWV * 64) __attribute__((amdgpu_waves_per_eu(
     const float* __restrict__ flow, stif_dec_tables tb, const float* __restrict__ tq, float* __restrict__ out, int n,
     int h, int w, int HH, int WW, int* status) {
   __shared__ __attribute__((aligned(16))) float wbuf[2 * SEGQ * T];
+#if DEC_TRACE
+  const unsigned tr0 = (unsigned)__builtin_amdgcn_s_memtime();
+  unsigned tr_g = 0, tr_b = 0, tr_l23 = 0, tr_x;
+#define DTR_BEGIN() tr_x = (unsigned)__builtin_amdgcn_s_memtime()
+#define DTR_END(acc) acc += (unsigned)__builtin_amdgcn_s_memtime() - tr_x
+#else
+#define DTR_BEGIN()
+#define DTR_END(acc)
+#endif
   const int lane = threadIdx.x & 63, q = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   constexpr int NW = DEC2Q_NWV;
@@ -1045,6 +1059,7 @@ __global__ __launch_bounds__(DEC2Q_NWV * 64) __attribute__((amdgpu_waves_per_eu(
   const float* HRF = hrfeat + (size_t)item * HH * WW * 64;
 
   // warpgrid (warplayer.py:25-39) and the decoder's clamp (Sakuya_arch_test.py:428,441), as k_dec2
+  DTR_BEGIN();
   const f32x4 fv = ld4(flow + (size_t)pc * 4);
   const float lo = -1.f + 1e-6f, hi = 1.f - 1e-6f;
   const float dx = ((float)WW - 1.f) / 2.f, dy = ((float)HH - 1.f) / 2.f;
@@ -1071,7 +1086,10 @@ __global__ __launch_bounds__(DEC2Q_NWV * 64) __attribute__((amdgpu_waves_per_eu(
       }
     asm volatile("" ::: "memory");
     gather_q(g, HRF, 64, 0, bilin(g1x, g1y, WW, HH), q);   // q_feat1 -> W0 columns 0..63
+    DTR_END(tr_g);
+    DTR_BEGIN();
     dec_barrier();                                      // layer 0 landed in B0
+    DTR_END(tr_b);
     dma_tiles<NW>(B1, rm, Q_W1, 4, wv, lane);
     {
       const XQ qs[2] = {xq(g[0]), xq(g[1])};
@@ -1081,7 +1099,9 @@ __global__ __launch_bounds__(DEC2Q_NWV * 64) __attribute__((amdgpu_waves_per_eu(
         for (int kt = 0; kt < 2; ++kt) tile_q(z[ot], B0 + (ot * 4 + kt) * T, qs[kt], lane);
     }
     asm volatile("" ::: "memory");
+    DTR_BEGIN();
     gather_q(g, HRF, 64, 0, bilin(g2x, g2y, WW, HH), q);   // q_feat2 -> W0 columns 64..127
+    DTR_END(tr_g);
     const XQ qs[2] = {xq(g[0]), xq(g[1])};
 #pragma unroll
     for (int ot = 0; ot < 2; ++ot) {
@@ -1093,7 +1113,9 @@ __global__ __launch_bounds__(DEC2Q_NWV * 64) __attribute__((amdgpu_waves_per_eu(
         for (int e = 0; e < 4; ++e) x0[ot].s[s][e] = siren_sin<1>(z[ot].s[s][e] * ACC_S<1>);
     }
   }
+  DTR_BEGIN();
   dec_barrier();   // layer 1 landed in B1; every wave is done with layer 0's B0
+  DTR_END(tr_b);
   // layer-1 biases before the next segment's LDS-DMA: vmcnt counts in issue order, so a bias load issued
   // after the DMA would wait for the DMA too (as k_dec1 / k_dec2 do)
   const R32 eb1[2] = {bias_q(mlp + E_B1, q), bias_q(mlp + E_B1 + 32, q)};
@@ -1118,7 +1140,9 @@ __global__ __launch_bounds__(DEC2Q_NWV * 64) __attribute__((amdgpu_waves_per_eu(
   for (int ot = 0; ot < 8; ++ot) a3[ot].s[0] = a3[ot].s[1] = f32x4{0.f, 0.f, 0.f, 0.f};
   constexpr int NSEG = 8 / KTS;
   auto l23_step = [&](int sg, bool last) {
+    DTR_BEGIN();
     dec_barrier();   // segment sg landed; every wave is done with the other buffer
+    DTR_END(tr_b);
     R32 b2[KTS];
 #pragma unroll
     for (int k = 0; k < KTS; ++k) b2[k] = bias_q(mlp + E_B2 + (sg * KTS + k) * 32, q);   // before the DMA
@@ -1143,9 +1167,15 @@ __global__ __launch_bounds__(DEC2Q_NWV * 64) __attribute__((amdgpu_waves_per_eu(
       for (int ot = 0; ot < 8; ++ot) tile_q(a3[ot], sk + (2 + ot) * T, h2, lane);
     }
   };
+#if DEC_TRACE
+  const unsigned tr_l0 = (unsigned)__builtin_amdgcn_s_memtime();
+#endif
 #pragma unroll 1
   for (int sg = 0; sg < NSEG - 1; ++sg) l23_step(sg, false);
   l23_step(NSEG - 1, true);
+#if DEC_TRACE
+  tr_l23 = (unsigned)__builtin_amdgcn_s_memtime() - tr_l0;
+#endif
   // layer 3 sine streamed into layer 4 (256 -> 3, VALU dot products over this lane's 64 features); W4 rows
   // and the layer-3 biases in the buffer the last segment did not use (k_dec2's tile)
   dec_barrier();
@@ -1180,6 +1210,15 @@ __global__ __launch_bounds__(DEC2Q_NWV * 64) __attribute__((amdgpu_waves_per_eu(
     }
     report_range(status, bad);
   }
+#if DEC_TRACE
+  if (g_dtrace && lane == 0) {
+    typedef unsigned u32x4t __attribute__((ext_vector_type(4)));
+    *reinterpret_cast<u32x4t*>(g_dtrace + ((size_t)blockIdx.x * NW + wv) * 8) =
+        u32x4t{(unsigned)__builtin_amdgcn_s_memtime() - tr0, tr_g, tr_b, tr_l23};
+  }
+#endif
+#undef DTR_BEGIN
+#undef DTR_END
 }
 
 __global__ __launch_bounds__(256) void k_pack_lr(const float* __restrict__ f0, const float* __restrict__ f1,
@@ -1326,6 +1365,12 @@ extern "C" int stif_dec_stage2(const float* proj, const float* mlp, const float*
                                int h, int w, int HH, int WW, void* stream) {
   return stif_dec_stage2_ex(proj, mlp, hrfeat, flow, tab, img, t, out, n, h, w, HH, WW, 0, nullptr, stream);
 }
+
+#if DEC_TRACE
+extern "C" int stif_dec_trace_set(unsigned* p) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_dtrace), &p, sizeof(p)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int stif_dec_blend4(const float* const* pred, const float* const* wgt, float* out, int n, int HH, int WW,
                                void* stream) {

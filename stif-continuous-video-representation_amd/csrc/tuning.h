@@ -113,6 +113,9 @@ static_assert(DCNSEP_EXP == 0 || DCNSEP_EXP == 1 || DCNSEP_EXP == 3 || DCNSEP_EX
 // fp32 and high-resolution-image stages)
 #define DEC2_Q16 1
 #endif
+#ifndef DEC_TRACE
+#define DEC_TRACE 0        // diagnostic: k_dec2q per-wave s_memtime sums (gathers, segment barriers, layers 2/3)
+#endif
 #ifndef DEC1_RES
 #define DEC1_RES 0         // stage 1 (f16x3, LR image) as two persistent resident-weight kernels k_dec1f + k_dec1l
 #endif
