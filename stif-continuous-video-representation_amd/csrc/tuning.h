@@ -21,6 +21,9 @@ static_assert(WINO_UPQ == 0 || WINO_UPQ == 1, "WINO_UPQ");
 #ifndef WINO_NT
 #define WINO_NT 0          // cache-policy bits (aux) of the input-halo LDS-DMA (2 = nt)
 #endif
+#ifndef WINO_TRACE
+#define WINO_TRACE 0       // diagnostic: per-wave s_memtime sums of the ResidualBlock conv1 (stif_wino_trace_set)
+#endif
 #ifndef WINO_EXP
 #define WINO_EXP 0         // probes: 1 no LDS-DMA after the first phase, 2 no B refills, 3 no output exchange,
                            // 4 no x2-upsample expansion (in1_mode 2), 5 RELU-epilogue convs store nothing,

@@ -103,6 +103,11 @@ struct Tile {
 // Wave i = transform row i for both 32-cout halves (2 waves per SIMD, ~250 VGPRs).
 // dynamic schedule: the value each XCD counter holds before the launch (the host keeps the counters'
 // running totals, so nothing resets them at the end of a launch)
+#if WINO_TRACE
+// diagnostic (stif_wino_trace_set): per wave of the RELU-epilogue f16x3 k_wino (the ResidualBlock conv1) 4 u32 --
+// life, phase-end waits (vmcnt + barrier), epilogue (output-transform exchange + stores), tiles -- s_memtime ticks
+__device__ unsigned* g_wtrace;
+#endif
 struct SchedBase {
   unsigned b[8];
 };
@@ -291,6 +296,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   int Tn = T + nl;                                        // the next tile (static for the first two)
   const int dbase = xcd * per + 2 * nl;                   // dynamic tile d = dbase + counter value
   int par = 0;
+#if WINO_TRACE
+  const unsigned tr0 = (unsigned)__builtin_amdgcn_s_memtime();
+  unsigned tr_wait = 0, tr_epi = 0, tr_x = 0, ntile = 0;
+#endif
   if (T < tend) {
   Tile cur = tile_of(T);
   const float* wsl = wbase(cur);
@@ -394,8 +403,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         }
         // every load older than the last two blocks' B refills (8) -- the phase's LDS-DMA among
         // them -- has landed
+#if WINO_TRACE
+        tr_x = (unsigned)__builtin_amdgcn_s_memtime();
+#endif
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         __syncthreads();
+#if WINO_TRACE
+        tr_wait += (unsigned)__builtin_amdgcn_s_memtime() - tr_x;
+#endif
         publish(p);
         if (IN1 == 2 && p + 1 < NP && up_phase(p + 1)) {
           expand(cur, (gp + 1) & 1);
@@ -449,6 +464,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     // thread combines and stores (pixel, 4-cout) vectors as coalesced 16-B accesses (8 lanes = one
     // pixel's 128 B).  Row swizzle R ^ (bit2(tile) ^ b) keeps both the b32 writes (lane halves 4
     // tiles apart) and the b128 reads (16-lane groups = b 0/1 of one tile) conflict-free.
+#if WINO_TRACE
+    const unsigned tr_e0 = (unsigned)__builtin_amdgcn_s_memtime();
+    ++ntile;
+#endif
     float* ex = smem + ((gp - 1) & 1) * BUF_F;
     if (WINO_EXP == 3) {
       f32x16 sm = f32x16{0};
@@ -555,10 +574,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     }
     if (F16) report_range(a.status, not_finite(chk));   // a non-finite output makes the sum non-finite
     __syncthreads();   // exchange buffer free for the next tile's staging
+#if WINO_TRACE
+    tr_epi += (unsigned)__builtin_amdgcn_s_memtime() - tr_e0;
+#endif
     if (!has_next) break;
     advance();
   }
   }
+#if WINO_TRACE
+  if (g_wtrace && (tid & 63) == 0 && F16 && EPI == STIF_EPI_RELU) {
+    typedef unsigned u32x4t __attribute__((ext_vector_type(4)));
+    *reinterpret_cast<u32x4t*>(g_wtrace + ((size_t)blockIdx.x * 4 + wi) * 4) =
+        u32x4t{(unsigned)__builtin_amdgcn_s_memtime() - tr0, tr_wait, tr_epi, ntile};
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -843,6 +872,12 @@ int launch(const stif_conv_args& a, hipStream_t st) {
 }
 
 }  // namespace
+
+#if WINO_TRACE
+extern "C" int stif_wino_trace_set(unsigned* p) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_wtrace), &p, sizeof(p)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int stif_conv3x3_wino(const stif_conv_args* pa, void* stream) {
   if (!pa) return stif_fail(STIF_E_INVALID, "stif_conv3x3_wino: null args");
