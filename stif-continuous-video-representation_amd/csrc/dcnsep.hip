@@ -206,6 +206,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_
   if (false)
 #endif
   {
+#if DCNSEP_PRIO == 2
+  __builtin_amdgcn_s_setprio(2);   // phase 1 (MFMA stream) ahead of a co-resident phase-2 wave
+#endif
   stage_data(0, smem + OFF_D0);
   stage_w(0, 0);
   stage_w(1, 1);
@@ -379,6 +382,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(DCNSEP_
   }
 #if DCNSEP_TP_CHECK
   int tp_bad = 0, tp_badw = 0, tp_first = -1, tp_tap = 0;
+#endif
+#if DCNSEP_PRIO == 1
+  __builtin_amdgcn_s_setprio(2);   // phase 2 (VALU / latency-bound sampling) ahead of a co-resident phase-1 wave
+#elif DCNSEP_PRIO == 2
+  __builtin_amdgcn_s_setprio(0);
 #endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // pair 0 staged (NW 8) and the om biases loaded
   __syncthreads();                                    // phase-1 buffers free

@@ -67,6 +67,9 @@ static_assert(WINO_UPQ == 0 || WINO_UPQ == 1, "WINO_UPQ");
 #ifndef DCNSEP_TP_DUMP
 #define DCNSEP_TP_DUMP 0   // diagnostic (TAPPIPE): per-thread dump of every tap's blended samples and each pair's accumulators
 #endif
+#ifndef DCNSEP_PRIO
+#define DCNSEP_PRIO 0      // wave priority (s_setprio 2) for phase 2 (1) or phase 1 (2) of the fused DCN_sep
+#endif
 #ifndef DCNSEP_P2PROG
 #define DCNSEP_P2PROG 0    // fused DCN_sep phase 2 (NW 4): 0 = wait for the whole pair stage; 3 / 9 = wait in 3 / 9 steps (the
                            // tile + the first taps' weights, then the next taps'), so the taps start while later weights land
