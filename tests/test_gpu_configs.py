@@ -121,6 +121,24 @@ def test_c0_window_dcn_sep_launches_deterministic(stif, models):
     assert len(seen) >= 2 * 12 and all(seen), seen
 
 
+@pytest.mark.parametrize("mf", ["f16x3", "f32"])
+def test_c0_window_runs_bit_identical(models, mf):
+    """The whole C0 window (encoder, PCD, Bi-ConvLSTM, recon trunk on its side streams, both decoder stages) run three
+    times on the same frames gives the same latent and the same decoded frames bit for bit, in both operand modes:
+    no kernel of the path may depend on wave timing or co-residency (the property the packed-fp32 tap-pipelined
+    DCN_sep broke)."""
+    fr = synth(0, 7, 128, 128)
+    m = models[mf]
+    runs = []
+    with torch.no_grad():
+        for _ in range(3):
+            m.gen_feat_window(fr)
+            runs.append((m.feat.clone(), [o.clone() for o in m.decoding([torch.tensor([[0.5]]), torch.tensor([[0.75]])])]))
+    for feat, outs in runs[1:]:
+        assert torch.equal(feat, runs[0][0])
+        assert all(torch.equal(a, b) for a, b in zip(outs, runs[0][1]))
+
+
 CONFIG_CASES = {
     # BASELINE configs[1..4] at their full per-GPU sizes: (frames, H, W, output size or None, times)
     "C1": (7, 256, 256, None, [0.5]),
